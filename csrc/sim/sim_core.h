@@ -1,0 +1,965 @@
+// Batched coord-sim core: one discrete-event environment per call, shared by the HIP kernel
+// (one wave per env, state staged in LDS) and the host path (CPU tests / differential checks).
+//
+// Semantics follow the reference simulator (coordsim/, SimPy 4) and the scalar oracle in
+// gsc_amd/coordsim/: every SimPy event id is reproduced (process initialise events are URGENT,
+// timeouts and process completions NORMAL, FIFO on equal (time, priority)), so deterministic
+// configurations agree bit-for-bit with the oracle.  Process instances are explicit state
+// machines; see the per-process comments for the reference generator they implement.
+#pragma once
+#include "philox.h"
+
+namespace gsc {
+
+constexpr int kMaxC = 4;      // SFCs
+constexpr int kMaxF = 8;      // chain length
+constexpr int kMaxS = 8;      // distinct SFs
+constexpr int kMaxTTL = 8;
+constexpr int kNumStats = 16;
+
+enum ProcType : uint8_t {
+  P_FREE = 0, P_WRITER, P_MMPP, P_TRACE, P_ARRIVAL, P_HANDLE, P_DECIDE, P_FORWARD, P_PROCESS, P_REQUEST,
+  P_FINISH, P_RETLINK
+};
+// per-type resume states
+enum : uint8_t {
+  W_BEGIN = 0, W_INIT, W_AFTER,
+  M_START = 0, M_AFTER, M_UPDATE,
+  TR_INIT = 0, TR_AFTER,
+  A_LOOP = 0,
+  H_LOOP = 0, H_AFTER_DECIDE, H_AFTER_FWD, H_AFTER_PROC,
+  D_INIT = 0, D_RUN,
+  F_INIT = 0, F_AFTER_HOP,
+  PR_INIT = 0, PR_AFTER_REQ, PR_AFTER_WAIT,
+  RQ_INIT = 0, RQ_AFTER,
+  FI_INIT = 0, FI_AFTER,
+  RL_INIT = 0, RL_AFTER
+};
+enum DropReason { R_TTL = 0, R_DECISION = 1, R_LINK = 2, R_NODE = 3 };
+enum Objective { OBJ_PRIO_FLOW = 0, OBJ_SOFT_DEADLINE = 1, OBJ_SOFT_DEADLINE_EXP = 2, OBJ_WEIGHTED = 3 };
+enum Flags { FLAG_FLOW_OVERFLOW = 1, FLAG_PROC_OVERFLOW = 2, FLAG_EVENT_OVERFLOW = 4, FLAG_BAD_STATE = 8 };
+constexpr int16_t kStopProc = -2;
+
+struct Event {     // 16 B
+  double t;
+  uint32_t key;    // (priority << 31) | event id
+  int16_t proc;
+  uint16_t pad;
+};
+
+struct Proc {      // 32 B
+  uint8_t type, state;
+  int16_t flow, parent, a, b, c, ret, pad;
+  double x, y;
+};
+
+struct Flow {      // 56 B
+  double dr, duration, e2e, ttl, creation;
+  int32_t id;
+  int16_t node, egress, sfc, pos, cur_sf, ingress;
+  uint8_t departed, fwd_eg, dropped, proc_idx;
+};
+
+struct Header {
+  double now;
+  uint32_t eid;
+  int32_t n_events, flow_top, proc_top;
+  int32_t run_times, episode, run_count, topo;
+  uint32_t key0, key1;
+  uint64_t ctr;
+  int32_t total_flow_count, trace_index, flags, n;
+  int32_t gen, processed, dropped, active;
+  int32_t run_gen, run_processed, run_dropped, num_path_delays;
+  int32_t drop_reason[4];
+  int32_t num_proc_delays, max_events, max_procs, max_flows;
+  double total_e2e, total_path_delay, total_proc_delay;
+  double run_e2e, run_max_e2e, run_total_path_delay, run_avg_path_delay;
+  double ewma_flows, episode_return;
+};
+
+// Read-only per-topology tables (device or host memory).
+struct TopoDev {
+  int n, E, H, n_ing, n_eg, pad;
+  double diameter;
+  const double* cap;        // [n]
+  const double* pdelay;     // [n*n]
+  const int16_t* plen;      // [n*n]
+  const int16_t* pnodes;    // [n*n*H]
+  const int16_t* edge_id;   // [n*n]
+  const double* edge_cap;   // [E]
+  const int16_t* ingress;   // [n_ing]
+  const int16_t* egress;    // [n_eg]
+};
+
+struct SimConst {
+  int C, S, F;                       // sfcs, distinct SFs, action sf dim (max chain length)
+  int chain_len[kMaxC];
+  int chain[kMaxC * kMaxF];          // global SF index of each chain position
+  double pd_mean[kMaxS], pd_std[kMaxS], startup[kMaxS];
+  double run_duration;
+  int det_arrival, det_size;
+  double dr_mean, dr_std, size_shape;
+  int n_ttl;
+  double ttl[kMaxTTL];
+  double inter_arr_mean;
+  int use_states, mmpp_init;
+  double mmpp_mean[2], mmpp_switch[2];
+  int n_trace, trace_has_node;
+  const double* trace_time;
+  const int16_t* trace_node;         // -1: applies to every ingress
+  const double* trace_mean;          // NaN = None
+  const double* trace_cap;           // NaN = no cap column
+  // observation / reward
+  int n_obs;
+  int obs_feat[3];                   // 0 ingress_traffic, 1 node_load, 2 node_cap
+  int objective;
+  double w_flow, w_delay, w_node, w_inst;
+  double target_success;             // NaN = 'auto' (EWMA)
+  double soft_deadline, dropoff, min_delay;
+  double diameter;                   // <0: use topology APSP diameter
+  int episode_steps;
+  int n_pad;                         // model node padding (action/obs layout)
+  int same_seed_every_episode;
+};
+
+struct Dims {
+  int N, S, C, E, flow_cap, proc_cap, event_cap;
+};
+
+struct Layout {
+  int hdr, node_cap, node_rem, inter_arr, max_usage, run_drop_node, mmpp_state, sf_load, sf_start, proc_traffic,
+      requested, drop_locs, sched, wrr, link_rem, link_passed, flows, procs, events, flow_free, proc_free,
+      sf_present, placement, total;
+};
+
+GSC_HD int align16(int x) { return (x + 15) & ~15; }
+
+GSC_HD Layout make_layout(const Dims& d) {
+  Layout L;
+  int o = 0;
+#define GSC_TAKE(field, bytes) L.field = o; o += align16((int)(bytes));
+  GSC_TAKE(hdr, sizeof(Header));
+  GSC_TAKE(node_cap, 8 * d.N);
+  GSC_TAKE(node_rem, 8 * d.N);
+  GSC_TAKE(inter_arr, 8 * d.N);
+  GSC_TAKE(max_usage, 8 * d.N);
+  GSC_TAKE(run_drop_node, 4 * d.N);
+  GSC_TAKE(mmpp_state, 4 * d.N);
+  GSC_TAKE(sf_load, 8 * d.N * d.S);
+  GSC_TAKE(sf_start, 8 * d.N * d.S);
+  GSC_TAKE(proc_traffic, 8 * d.N * d.S);
+  GSC_TAKE(requested, 8 * d.N * d.C * d.S);
+  GSC_TAKE(drop_locs, 4 * d.N * (d.S + 1));
+  GSC_TAKE(sched, 8 * d.N * d.C * d.S * d.N);
+  GSC_TAKE(wrr, 4 * d.N * d.C * d.S * d.N);
+  GSC_TAKE(link_rem, 8 * d.E);
+  GSC_TAKE(link_passed, 8 * d.E);
+  GSC_TAKE(flows, sizeof(Flow) * d.flow_cap);
+  GSC_TAKE(procs, sizeof(Proc) * d.proc_cap);
+  GSC_TAKE(events, sizeof(Event) * d.event_cap);
+  GSC_TAKE(flow_free, 2 * d.flow_cap);
+  GSC_TAKE(proc_free, 2 * d.proc_cap);
+  GSC_TAKE(sf_present, d.N * d.S);
+  GSC_TAKE(placement, d.N * d.S);
+#undef GSC_TAKE
+  L.total = o;
+  return L;
+}
+
+// Typed view of one env's state blob.
+struct Env {
+  Header* h;
+  double *node_cap, *node_rem, *inter_arr, *max_usage, *sf_load, *sf_start, *proc_traffic, *requested, *sched,
+      *link_rem, *link_passed;
+  int32_t *run_drop_node, *mmpp_state, *drop_locs, *wrr;
+  Flow* flows;
+  Proc* procs;
+  Event* events;
+  int16_t *flow_free, *proc_free;
+  uint8_t *sf_present, *placement;
+  Dims d;
+
+  GSC_HD Env(char* base, const Layout& L, const Dims& dims) : d(dims) {
+    h = (Header*)(base + L.hdr);
+    node_cap = (double*)(base + L.node_cap);
+    node_rem = (double*)(base + L.node_rem);
+    inter_arr = (double*)(base + L.inter_arr);
+    max_usage = (double*)(base + L.max_usage);
+    run_drop_node = (int32_t*)(base + L.run_drop_node);
+    mmpp_state = (int32_t*)(base + L.mmpp_state);
+    sf_load = (double*)(base + L.sf_load);
+    sf_start = (double*)(base + L.sf_start);
+    proc_traffic = (double*)(base + L.proc_traffic);
+    requested = (double*)(base + L.requested);
+    drop_locs = (int32_t*)(base + L.drop_locs);
+    sched = (double*)(base + L.sched);
+    wrr = (int32_t*)(base + L.wrr);
+    link_rem = (double*)(base + L.link_rem);
+    link_passed = (double*)(base + L.link_passed);
+    flows = (Flow*)(base + L.flows);
+    procs = (Proc*)(base + L.procs);
+    events = (Event*)(base + L.events);
+    flow_free = (int16_t*)(base + L.flow_free);
+    proc_free = (int16_t*)(base + L.proc_free);
+    sf_present = (uint8_t*)(base + L.sf_present);
+    placement = (uint8_t*)(base + L.placement);
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// RNG helpers (per-env Philox stream; deterministic configs draw nothing)
+// ------------------------------------------------------------------------------------------------
+GSC_HD double rng_u01(Env& S) {
+  Philox4 r = philox4x32_10(S.h->key0, S.h->key1, S.h->ctr++);
+  return u01_53(r.v[0], r.v[1]);
+}
+GSC_HD double rng_normal(Env& S, double mean, double std) {
+  if (std == 0.0) return mean;
+  Philox4 r = philox4x32_10(S.h->key0, S.h->key1, S.h->ctr++);
+  const double u1 = 1.0 - u01_53(r.v[0], r.v[1]);  // (0, 1]
+  const double u2 = u01_53(r.v[2], r.v[3]);
+  return mean + std * (sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+}
+GSC_HD int rng_int(Env& S, int n) {
+  if (n <= 1) return 0;
+  int k = (int)(rng_u01(S) * n);
+  return k >= n ? n - 1 : k;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Event / process primitives (SimPy contract)
+// ------------------------------------------------------------------------------------------------
+GSC_HD void push_event(Env& S, double t, uint32_t prio, int16_t proc) {
+  Header* h = S.h;
+  const uint32_t key = (prio << 31) | (h->eid & 0x7fffffffu);
+  h->eid++;
+  if (h->n_events >= S.d.event_cap) { h->flags |= FLAG_EVENT_OVERFLOW; return; }
+  Event& e = S.events[h->n_events++];
+  e.t = t;
+  e.key = key;
+  e.proc = proc;
+  if (h->n_events > h->max_events) h->max_events = h->n_events;
+}
+GSC_HD void timeout(Env& S, int pid, double delay) { push_event(S, S.h->now + delay, 1u, (int16_t)pid); }
+
+GSC_HD int alloc_proc(Env& S, uint8_t type, uint8_t state, int flow, int parent) {
+  Header* h = S.h;
+  if (h->proc_top <= 0) { h->flags |= FLAG_PROC_OVERFLOW; return -1; }
+  const int pid = S.proc_free[--h->proc_top];
+  Proc& p = S.procs[pid];
+  p.type = type; p.state = state; p.flow = (int16_t)flow; p.parent = (int16_t)parent;
+  p.a = p.b = p.c = p.ret = 0; p.x = p.y = 0.0;
+  const int used = S.d.proc_cap - h->proc_top;
+  if (used > h->max_procs) h->max_procs = used;
+  return pid;
+}
+// env.process(gen): new process + URGENT initialise event.
+GSC_HD int spawn(Env& S, uint8_t type, uint8_t state, int flow, int parent) {
+  const int pid = alloc_proc(S, type, state, flow, parent);
+  if (pid < 0) { S.h->eid++; return -1; }
+  push_event(S, S.h->now, 0u, (int16_t)pid);
+  return pid;
+}
+// A process yields env.process(itself-again): re-initialise the same slot (recursive reference generators).
+GSC_HD void respawn_self(Env& S, int pid, uint8_t state) {
+  S.procs[pid].state = state;
+  push_event(S, S.h->now, 0u, (int16_t)pid);
+}
+// Generator return: completion event (NORMAL, delay 0); resumes the waiting parent if any.
+GSC_HD void proc_return(Env& S, int pid, int16_t value) {
+  const int parent = S.procs[pid].parent;
+  if (parent >= 0) {
+    S.procs[parent].ret = value;
+    push_event(S, S.h->now, 1u, (int16_t)parent);
+  } else {
+    S.h->eid++;
+  }
+  S.procs[pid].type = P_FREE;
+  S.proc_free[S.h->proc_top++] = (int16_t)pid;
+}
+
+GSC_HD int alloc_flow(Env& S) {
+  Header* h = S.h;
+  if (h->flow_top <= 0) { h->flags |= FLAG_FLOW_OVERFLOW; return -1; }
+  const int fid = S.flow_free[--h->flow_top];
+  const int used = S.d.flow_cap - h->flow_top;
+  if (used > h->max_flows) h->max_flows = used;
+  return fid;
+}
+GSC_HD void free_flow(Env& S, int fid) { S.flow_free[S.h->flow_top++] = (int16_t)fid; }
+
+// ------------------------------------------------------------------------------------------------
+// Metrics hooks (reference coordsim/metrics/metrics.py)
+// ------------------------------------------------------------------------------------------------
+GSC_HD void reset_run_metrics(Env& S, const SimConst& K, int n) {
+  Header* h = S.h;
+  h->run_gen = h->run_processed = h->run_dropped = 0;
+  h->run_e2e = h->run_max_e2e = h->run_total_path_delay = h->run_avg_path_delay = 0.0;
+  const int N = S.d.N, Sd = S.d.S, C = S.d.C;
+  for (int v = 0; v < N; ++v) { S.run_drop_node[v] = 0; S.max_usage[v] = 0.0; }
+  for (int i = 0; i < N * Sd; ++i) S.proc_traffic[i] = 0.0;
+  for (int i = 0; i < N * C * Sd; ++i) S.requested[i] = 0.0;
+  for (int i = 0; i < N * C * Sd * N; ++i) S.wrr[i] = 0;
+  (void)K; (void)n;
+}
+
+GSC_HD void dropped_flow(Env& S, Flow& f, int reason) {
+  Header* h = S.h;
+  f.dropped = 1;
+  h->dropped++; h->active--; h->run_dropped++;
+  const int sf = f.cur_sf < 0 ? S.d.S : f.cur_sf;
+  S.drop_locs[f.node * (S.d.S + 1) + sf]++;
+  S.run_drop_node[f.node]++;
+  if (f.ttl <= 0) reason = R_TTL;
+  h->drop_reason[reason]++;
+}
+
+GSC_HD void completed_flow(Env& S, const Flow& f) {
+  Header* h = S.h;
+  h->processed++; h->run_processed++; h->active--;
+  h->total_e2e += f.e2e;
+  h->run_e2e += f.e2e;
+  if (f.e2e > h->run_max_e2e) h->run_max_e2e = f.e2e;
+}
+
+GSC_HD void add_path_delay(Env& S, double d) {
+  Header* h = S.h;
+  h->num_path_delays++;
+  h->total_path_delay += d;
+  h->run_total_path_delay += d;
+  if (h->run_gen > 0) h->run_avg_path_delay = h->run_total_path_delay / h->run_gen;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Process handlers
+// ------------------------------------------------------------------------------------------------
+GSC_HD void end_flow(Env& S, int pid, int fid) {
+  free_flow(S, fid);
+  proc_return(S, pid, 0);
+}
+
+// FlowSimulator.handle_flow (flowsimulator.py:72-128)
+GSC_HD void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc& P = S.procs[pid];
+  const int fid = P.flow;
+  Flow& f = S.flows[fid];
+  for (;;) {
+    switch (P.state) {
+      case H_LOOP:
+        if (f.departed) {
+          completed_flow(S, f);
+          end_flow(S, pid, fid);
+          return;
+        }
+        P.state = H_AFTER_DECIDE;
+        spawn(S, P_DECIDE, D_INIT, fid, pid);
+        return;
+      case H_AFTER_DECIDE: {
+        const int nxt = P.ret;
+        if (nxt < 0) { dropped_flow(S, f, R_DECISION); end_flow(S, pid, fid); return; }
+        P.state = H_AFTER_FWD;
+        const int c = spawn(S, P_FORWARD, F_INIT, fid, pid);
+        if (c >= 0) S.procs[c].b = (int16_t)nxt;
+        return;
+      }
+      case H_AFTER_FWD:
+        if (!P.ret) { dropped_flow(S, f, R_LINK); end_flow(S, pid, fid); return; }
+        if (!f.fwd_eg) {
+          P.state = H_AFTER_PROC;
+          spawn(S, P_PROCESS, PR_INIT, fid, pid);
+          return;
+        }
+        P.state = H_LOOP;
+        break;
+      case H_AFTER_PROC:
+        if (!P.ret) { dropped_flow(S, f, R_NODE); end_flow(S, pid, fid); return; }
+        P.state = H_LOOP;
+        break;
+      default:
+        S.h->flags |= FLAG_BAD_STATE;
+        return;
+    }
+  }
+  (void)K; (void)T;
+}
+
+// DefaultDecisionMaker.decide_next_node (default_decision_maker.py:18-81): weighted round robin.
+GSC_HD void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc& P = S.procs[pid];
+  if (P.state == D_INIT) {
+    P.state = D_RUN;
+    timeout(S, pid, 0.0);
+    return;
+  }
+  Flow& f = S.flows[P.flow];
+  if (f.ttl <= 0) { proc_return(S, pid, -1); return; }
+  if (f.fwd_eg) {
+    if (f.egress < 0) f.egress = f.node;
+    proc_return(S, pid, f.egress);
+    return;
+  }
+  const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
+  const int sf = K.chain[f.sfc * kMaxF + f.pos];
+  f.cur_sf = (int16_t)sf;
+  S.requested[(f.node * C + f.sfc) * Sd + sf] += f.dr;
+  const int row = ((f.node * C + f.sfc) * Sd + sf) * N;
+  const double* p = S.sched + row;
+  int32_t* cnt = S.wrr + row;
+  long total = 0;
+  for (int d = 0; d < n; ++d) total += cnt[d];
+  int best = 0;
+  double best_v = -1e300;
+  for (int d = 0; d < n; ++d) {
+    const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0;
+    const double diff = p[d] > 0 ? p[d] - ratio : -1.0;
+    if (diff > best_v) { best_v = diff; best = d; }
+  }
+  cnt[best]++;
+  proc_return(S, pid, (int16_t)best);
+}
+
+// DefaultFlowForwarder.forward_flow (default_forwarder.py:21-90) + return_link_resources.
+GSC_HD void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc& P = S.procs[pid];
+  Flow& f = S.flows[P.flow];
+  const int n = T.n;
+  const int nxt = P.b;
+  if (P.state == F_INIT) {
+    const int cur = f.node;
+    const double pd = (cur != nxt) ? T.pdelay[cur * n + nxt] : 0.0;
+    if (f.ttl - pd <= 0) { f.ttl = 0; proc_return(S, pid, 0); return; }
+    if (cur == f.egress && f.fwd_eg) f.departed = 1;
+    if (cur == nxt) { proc_return(S, pid, 1); return; }
+    P.a = (int16_t)cur;
+    P.c = 0;
+    P.x = pd;
+  } else {  // F_AFTER_HOP
+    const int hop = T.pnodes[(P.a * n + nxt) * T.H + P.c];
+    const int e = T.edge_id[f.node * n + hop];
+    const int c = spawn(S, P_RETLINK, RL_INIT, -1, -1);
+    if (c >= 0) { S.procs[c].a = (int16_t)e; S.procs[c].x = f.dr; S.procs[c].y = f.duration; }
+    f.node = (int16_t)hop;
+    P.c++;
+    if (P.c >= T.plen[P.a * n + nxt]) {
+      add_path_delay(S, P.x);
+      f.e2e += P.x;
+      f.ttl -= P.x;
+      proc_return(S, pid, 1);
+      return;
+    }
+  }
+  // next hop
+  const int hop = T.pnodes[(P.a * n + nxt) * T.H + P.c];
+  const int cur = f.node;
+  const int e = T.edge_id[cur * n + hop];
+  if (S.link_rem[e] - f.dr >= 0) {
+    S.link_rem[e] -= f.dr;
+  } else {
+    proc_return(S, pid, 0);
+    return;
+  }
+  S.link_passed[e] += f.dr;
+  const double hd = T.pdelay[cur * n + hop];
+  if (hop == f.egress && f.fwd_eg) f.departed = 1;
+  P.state = F_AFTER_HOP;
+  timeout(S, pid, hd);
+  (void)K;
+}
+
+GSC_HD void run_retlink(Env& S, int pid) {
+  Proc& P = S.procs[pid];
+  if (P.state == RL_INIT) {
+    P.state = RL_AFTER;
+    timeout(S, pid, P.y);
+    return;
+  }
+  S.link_rem[P.a] += P.x;
+  proc_return(S, pid, 0);
+}
+
+// DefaultFlowProcessor.process_flow (default_processor.py:14-50) + get_processing_delay.
+GSC_HD void run_process(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc& P = S.procs[pid];
+  const int fid = P.flow;
+  Flow& f = S.flows[fid];
+  const int Sd = S.d.S;
+  if (P.state == PR_INIT) {
+    const int node = f.node;
+    const int sf = K.chain[f.sfc * kMaxF + f.pos];
+    f.cur_sf = (int16_t)sf;
+    if (!S.placement[node * Sd + sf]) { proc_return(S, pid, 0); return; }
+    const double pd = fabs(rng_normal(S, K.pd_mean[sf], K.pd_std[sf]));
+    if (f.ttl - pd <= 0) { f.ttl = 0; proc_return(S, pid, 0); return; }
+    S.h->num_proc_delays++;
+    S.h->total_proc_delay += pd;
+    f.e2e += pd;
+    f.ttl -= pd;
+    if (pd == 0.0) { proc_return(S, pid, 0); return; }  // reference: `if not processing_delay`
+    P.x = pd;
+    P.a = (int16_t)node;
+    P.b = (int16_t)sf;
+    P.state = PR_AFTER_REQ;
+    const int c = spawn(S, P_REQUEST, RQ_INIT, fid, pid);
+    if (c >= 0) { S.procs[c].a = (int16_t)node; S.procs[c].b = (int16_t)sf; }
+    return;
+  }
+  if (P.state == PR_AFTER_REQ) {
+    if (!P.ret) { proc_return(S, pid, 0); return; }
+    P.state = PR_AFTER_WAIT;
+    timeout(S, pid, P.x);
+    return;
+  }
+  // PR_AFTER_WAIT: spawn finish_processing, return True
+  const int c = spawn(S, P_FINISH, FI_INIT, fid, -1);
+  if (c >= 0) { S.procs[c].a = P.a; S.procs[c].b = P.b; }
+  proc_return(S, pid, 1);
+  (void)T;
+}
+
+// BaseFlowProcessor.request_resources (base_processor.py:51-101).
+GSC_HD void run_request(Env& S, const SimConst& K, int pid) {
+  Proc& P = S.procs[pid];
+  if (P.state == RQ_AFTER) { proc_return(S, pid, 1); return; }
+  Flow& f = S.flows[P.flow];
+  const int node = P.a, sf = P.b, Sd = S.d.S;
+  double demanded = 0.0;
+  for (int s = 0; s < Sd; ++s)
+    if (S.sf_present[node * Sd + s]) demanded += S.sf_load[node * Sd + s] + (s == sf ? f.dr : 0.0);
+  const double cap = S.node_cap[node];
+  if (!(demanded <= cap)) { proc_return(S, pid, 0); return; }
+  f.proc_idx++;
+  S.proc_traffic[node * Sd + sf] += f.dr;
+  S.sf_load[node * Sd + sf] += f.dr;
+  S.node_rem[node] = cap - demanded;
+  if (demanded > S.max_usage[node]) S.max_usage[node] = demanded;
+  const double ready = S.sf_start[node * Sd + sf] + K.startup[sf];
+  if (!(ready <= S.h->now)) {
+    const double rem = ready - S.h->now;
+    if (f.ttl - rem <= 0) { f.ttl = 0; proc_return(S, pid, 0); return; }
+    f.e2e += rem;
+    f.ttl -= rem;
+    P.state = RQ_AFTER;
+    timeout(S, pid, rem);
+    return;
+  }
+  proc_return(S, pid, 1);
+}
+
+// BaseFlowProcessor.finish_processing (base_processor.py:103-135).
+GSC_HD void run_finish(Env& S, const SimConst& K, int pid) {
+  Proc& P = S.procs[pid];
+  const int Sd = S.d.S;
+  if (P.state == FI_INIT) {
+    Flow& f = S.flows[P.flow];
+    f.pos++;
+    if (f.pos == K.chain_len[f.sfc]) f.fwd_eg = 1;
+    P.x = f.dr;
+    P.state = FI_AFTER;
+    timeout(S, pid, f.duration);
+    return;
+  }
+  const int node = P.a, sf = P.b;
+  S.sf_load[node * Sd + sf] -= P.x;
+  if (S.sf_load[node * Sd + sf] == 0.0 && !S.placement[node * Sd + sf]) S.sf_present[node * Sd + sf] = 0;
+  double used = 0.0;
+  for (int s = 0; s < Sd; ++s)
+    if (S.sf_present[node * Sd + s]) used += S.sf_load[node * Sd + s];
+  S.node_rem[node] = S.node_cap[node] - used;
+  proc_return(S, pid, 0);
+}
+
+// FlowSimulator.init_arrival + DefaultFlowGenerator.generate_flow.
+GSC_HD void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc& P = S.procs[pid];
+  const int node = P.a;
+  const double mean = S.inter_arr[node];
+  if (mean != mean) { proc_return(S, pid, 0); return; }  // None: arrivals at this node stop
+  Header* h = S.h;
+  h->total_flow_count++;
+  const double inter = K.det_arrival ? mean : -log(1.0 - rng_u01(S)) * mean;
+  double dr, size;
+  for (;;) {
+    dr = rng_normal(S, K.dr_mean, K.dr_std);
+    size = K.det_size ? K.size_shape : exp(-log(1.0 - rng_u01(S)) / K.size_shape);  // pareto(a) + 1
+    if (dr >= 0.0 && size >= 0.0) break;
+  }
+  const int sfc = rng_int(S, K.C);
+  const int eg = T.n_eg > 0 ? T.egress[rng_int(S, T.n_eg)] : -1;
+  const double ttl = K.ttl[rng_int(S, K.n_ttl)];
+  const int fid = alloc_flow(S);
+  if (fid >= 0) {
+    Flow& f = S.flows[fid];
+    f.dr = dr;
+    f.duration = (size / dr) * 1000.0;
+    f.e2e = 0.0;
+    f.ttl = ttl;
+    f.creation = h->now;
+    f.id = h->total_flow_count;
+    f.node = (int16_t)node;
+    f.ingress = (int16_t)node;
+    f.egress = (int16_t)eg;
+    f.sfc = (int16_t)sfc;
+    f.pos = 0;
+    f.cur_sf = -1;
+    f.departed = f.fwd_eg = f.dropped = f.proc_idx = 0;
+    h->gen++; h->run_gen++; h->active++;
+    if (spawn(S, P_HANDLE, H_LOOP, fid, -1) < 0) free_flow(S, fid);
+  } else {
+    h->eid++;  // keep event ids aligned with the oracle even on overflow
+  }
+  timeout(S, pid, inter);
+}
+
+// ResultWriter.begin_writing / write_network_state: the run-window clock.
+GSC_HD void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc& P = S.procs[pid];
+  switch (P.state) {
+    case W_BEGIN:
+    case W_AFTER:
+      respawn_self(S, pid, W_INIT);
+      return;
+    default:  // W_INIT
+      reset_run_metrics(S, K, T.n);
+      P.state = W_AFTER;
+      timeout(S, pid, K.run_duration);
+      return;
+  }
+}
+
+// SimulatorParams.start_mmpp / update_state: 2-state MMPP arrivals.
+GSC_HD void run_mmpp(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc& P = S.procs[pid];
+  if (P.state == M_START) {
+    P.state = M_AFTER;
+    timeout(S, pid, K.run_duration);
+    return;
+  }
+  if (P.state == M_AFTER) {
+    respawn_self(S, pid, M_UPDATE);
+    return;
+  }
+  for (int i = 0; i < T.n_ing; ++i) {
+    const int v = T.ingress[i];
+    int st = S.mmpp_state[v];
+    if (rng_u01(S) < K.mmpp_switch[st]) st = 1 - st;
+    S.mmpp_state[v] = st;
+  }
+  for (int i = 0; i < T.n_ing; ++i) S.inter_arr[T.ingress[i]] = K.mmpp_mean[S.mmpp_state[T.ingress[i]]];
+  P.state = M_AFTER;
+  timeout(S, pid, K.run_duration);
+}
+
+// TraceProcessor.process_trace.
+GSC_HD void run_trace(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc& P = S.procs[pid];
+  const int i = S.h->trace_index;
+  if (P.state == TR_INIT) {
+    double w = K.trace_time[i] - S.h->now - 1.0;
+    if (w < 0) w = 0;
+    P.state = TR_AFTER;
+    timeout(S, pid, w);
+    return;
+  }
+  const double mean = K.trace_mean[i];
+  if (K.trace_has_node) {
+    const int v = K.trace_node[i];
+    if (mean != mean) {
+      S.inter_arr[v] = mean;
+    } else {
+      S.inter_arr[v] = mean;
+      const double cap = K.trace_cap[i];
+      if (cap == cap) S.node_cap[v] = cap;
+    }
+  } else {
+    for (int k = 0; k < T.n_ing; ++k) S.inter_arr[T.ingress[k]] = mean;
+  }
+  if (i < K.n_trace - 1) {
+    S.h->trace_index++;
+    respawn_self(S, pid, TR_INIT);  // env.process(process_trace()) ...
+    S.h->eid++;                     // ... then this generator returns (completion, no waiter)
+  } else {
+    proc_return(S, pid, 0);
+  }
+}
+
+GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  switch (S.procs[pid].type) {
+    case P_HANDLE: run_handle(S, K, T, pid); break;
+    case P_DECIDE: run_decide(S, K, T, pid); break;
+    case P_FORWARD: run_forward(S, K, T, pid); break;
+    case P_PROCESS: run_process(S, K, T, pid); break;
+    case P_REQUEST: run_request(S, K, pid); break;
+    case P_FINISH: run_finish(S, K, pid); break;
+    case P_RETLINK: run_retlink(S, pid); break;
+    case P_ARRIVAL: run_arrival(S, K, T, pid); break;
+    case P_WRITER: run_writer(S, K, T, pid); break;
+    case P_MMPP: run_mmpp(S, K, T, pid); break;
+    case P_TRACE: run_trace(S, K, T, pid); break;
+    default: S.h->flags |= FLAG_BAD_STATE; break;
+  }
+}
+
+GSC_HD bool ev_less(const Event& a, const Event& b) { return a.t < b.t || (a.t == b.t && a.key < b.key); }
+
+// Serial event selection (host, and the fallback inside the device loop).
+GSC_HD int argmin_event_serial(const Env& S) {
+  const int ne = S.h->n_events;
+  int best = 0;
+  for (int i = 1; i < ne; ++i)
+    if (ev_less(S.events[i], S.events[best])) best = i;
+  return best;
+}
+
+GSC_HD void remove_event(Env& S, int idx) {
+  const int last = --S.h->n_events;
+  if (idx != last) S.events[idx] = S.events[last];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Episode init / controller apply / observation + reward epilogue
+// ------------------------------------------------------------------------------------------------
+GSC_HD void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo, uint32_t seed, int episode) {
+  Header* h = S.h;
+  const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
+  const double ewma = h->ewma_flows;
+  // zero header
+  {
+    char* p = (char*)h;
+    for (int i = 0; i < (int)sizeof(Header); ++i) p[i] = 0;
+  }
+  h->topo = topo;
+  h->ewma_flows = episode <= 1 ? 1.0 : ewma;
+  h->episode = episode;
+  h->n = n;
+  h->run_times = 1;
+  h->key0 = seed;
+  h->key1 = K.same_seed_every_episode ? 0x5eedu : (0x5eedu ^ ((uint32_t)episode * 0x9E3779B9u));
+  h->ctr = 0;
+  for (int v = 0; v < N; ++v) {
+    const double cap = v < n ? T.cap[v] : 0.0;
+    S.node_cap[v] = cap;
+    S.node_rem[v] = cap;
+    S.inter_arr[v] = 0.0 / 0.0;  // NaN = None
+    S.mmpp_state[v] = 0;
+  }
+  for (int i = 0; i < N * Sd; ++i) { S.sf_present[i] = 0; S.placement[i] = 0; S.sf_load[i] = 0; S.sf_start[i] = 0; }
+  for (int i = 0; i < N * (Sd + 1); ++i) S.drop_locs[i] = 0;
+  for (int i = 0; i < N * C * Sd * N; ++i) S.sched[i] = 0.0;
+  for (int e = 0; e < S.d.E; ++e) { S.link_rem[e] = e < T.E ? T.edge_cap[e] : 0.0; S.link_passed[e] = 0.0; }
+  h->flow_top = S.d.flow_cap;
+  for (int i = 0; i < S.d.flow_cap; ++i) S.flow_free[i] = (int16_t)(S.d.flow_cap - 1 - i);
+  h->proc_top = S.d.proc_cap;
+  for (int i = 0; i < S.d.proc_cap; ++i) { S.proc_free[i] = (int16_t)(S.d.proc_cap - 1 - i); S.procs[i].type = P_FREE; }
+  reset_run_metrics(S, K, n);
+  // reference order: writer, (MMPP), (trace), arrivals; then one env.step()
+  spawn(S, P_WRITER, W_BEGIN, -1, -1);
+  if (K.use_states) {
+    for (int i = 0; i < T.n_ing; ++i) {
+      S.mmpp_state[T.ingress[i]] = K.mmpp_init;
+      S.inter_arr[T.ingress[i]] = K.mmpp_mean[K.mmpp_init];
+    }
+    spawn(S, P_MMPP, M_START, -1, -1);
+  } else {
+    for (int i = 0; i < T.n_ing; ++i) S.inter_arr[T.ingress[i]] = K.inter_arr_mean;
+  }
+  if (K.n_trace > 0) spawn(S, P_TRACE, TR_INIT, -1, -1);
+  for (int i = 0; i < T.n_ing; ++i) {
+    const int pid = spawn(S, P_ARRIVAL, A_LOOP, -1, -1);
+    if (pid >= 0) S.procs[pid].a = T.ingress[i];
+  }
+  // DurationController.get_init_state: env.step()
+  const int idx = argmin_event_serial(S);
+  const Event ev = S.events[idx];
+  remove_event(S, idx);
+  h->now = ev.t;
+  if (ev.proc >= 0) dispatch(S, K, T, ev.proc);
+}
+
+// SimulatorWrapper.apply (placement derivation) + DurationController.get_next_state prologue.
+// The schedule table S.sched must already hold this step's action.
+GSC_HD void controller_prologue(Env& S, const SimConst& K, const TopoDev& T) {
+  const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
+  for (int i = 0; i < N * Sd; ++i) S.placement[i] = 0;
+  // follow positive weights from every active ingress along each chain (add_placement_recursive)
+  for (int c = 0; c < K.C; ++c) {
+    uint64_t fr[4] = {0, 0, 0, 0};  // node bitset (n <= 256)
+    for (int i = 0; i < T.n_ing; ++i) {
+      const int v = T.ingress[i];
+      if (S.inter_arr[v] == S.inter_arr[v]) fr[v >> 6] |= 1ull << (v & 63);
+    }
+    for (int k = 0; k < K.chain_len[c]; ++k) {
+      const int sf = K.chain[c * kMaxF + k];
+      uint64_t nx[4] = {0, 0, 0, 0};
+      for (int src = 0; src < n; ++src) {
+        if (!((fr[src >> 6] >> (src & 63)) & 1)) continue;
+        const double* row = S.sched + ((src * C + c) * Sd + sf) * N;
+        for (int dst = 0; dst < n; ++dst) {
+          if (row[dst] > 0) {
+            S.placement[dst * Sd + sf] = 1;
+            nx[dst >> 6] |= 1ull << (dst & 63);
+          }
+        }
+      }
+      for (int w = 0; w < 4; ++w) fr[w] = nx[w];
+    }
+  }
+  // available_sf rebuild: keep SFs that still carry load, (re)create placed ones
+  const double now = S.h->now;
+  for (int v = 0; v < n; ++v)
+    for (int s = 0; s < Sd; ++s) {
+      const int i = v * Sd + s;
+      if (S.sf_present[i] && S.sf_load[i] != 0.0) continue;
+      if (S.placement[i]) { S.sf_present[i] = 1; S.sf_load[i] = 0.0; S.sf_start[i] = now; }
+      else S.sf_present[i] = 0;
+    }
+}
+
+GSC_HD void schedule_stop(Env& S, const SimConst& K) {
+  const double T_end = K.run_duration * S.h->run_times;
+  push_event(S, S.h->now + (T_end - S.h->now), 0u, kStopProc);
+}
+
+// Host / serial event loop until the stop event.
+GSC_HD void run_until_stop_serial(Env& S, const SimConst& K, const TopoDev& T) {
+  for (;;) {
+    if (S.h->n_events <= 0) { S.h->flags |= FLAG_BAD_STATE; return; }
+    const int idx = argmin_event_serial(S);
+    const Event ev = S.events[idx];
+    remove_event(S, idx);
+    S.h->now = ev.t;
+    if (ev.proc == kStopProc) return;
+    dispatch(S, K, T, ev.proc);
+  }
+}
+
+// Observation [n_pad, n_obs] (float32, max-normalised), reward and per-run stats.
+GSC_HD float clip01(float x) { return x < 0.f ? 0.f : (x > 1.f ? 1.f : x); }
+
+GSC_HD float obs_feature(const Env& S, const SimConst& K, int q, int v) {
+  const int Sd = S.d.S, C = S.d.C;
+  if (q == 0) {  // ingress traffic of the chain's first SF (the last SFC with traffic wins, as in the reference)
+    float t = 0.f;
+    for (int c = 0; c < K.C; ++c) {
+      bool any = false;
+      for (int s = 0; s < Sd; ++s) any |= S.requested[(v * C + c) * Sd + s] != 0.0;
+      if (any) t = (float)S.requested[(v * C + c) * Sd + K.chain[c * kMaxF]];
+    }
+    return t;
+  }
+  const double cap = S.node_cap[v];
+  if (q == 2) return (float)cap;
+  double use = 0.0;
+  for (int s = 0; s < Sd; ++s) use += S.proc_traffic[v * Sd + s];
+  return cap == 0.0 ? 1.f : (float)(use / cap);
+}
+
+GSC_HD void write_obs(const Env& S, const SimConst& K, const TopoDev& T, float* obs) {
+  const int n = T.n;
+  for (int j = 0; j < K.n_obs; ++j) {
+    const int q = K.obs_feat[j];
+    float mx = 0.f;
+    for (int v = 0; v < n; ++v) {
+      const float x = obs_feature(S, K, q, v);
+      mx = (v == 0 || x > mx) ? x : mx;
+    }
+    const float den = mx + 1e-3f;
+    for (int v = 0; v < K.n_pad; ++v) obs[v * K.n_obs + j] = v < n ? clip01(obs_feature(S, K, q, v) / den) : 0.f;
+  }
+}
+
+GSC_HD float compute_reward(Env& S, const SimConst& K, const TopoDev& T) {
+  Header* h = S.h;
+  const int succ = h->run_processed, drop = h->run_dropped, Sd = S.d.S, n = T.n;
+  double succ_ratio = 0.0, fr = 0.0;
+  if (succ + drop > 0) {
+    succ_ratio = (double)succ / (succ + drop);
+    fr = (double)(succ - drop) / (succ + drop);
+  }
+  const double diam = K.diameter > 0 ? K.diameter : T.diameter;
+  const double avg = succ > 0 ? h->run_e2e / succ : 0.0;
+  const double delay = avg > K.min_delay ? avg : K.min_delay;
+  double dr;
+  if (succ_ratio == 0.0) dr = -1.0;
+  else {
+    dr = ((K.min_delay - delay) / diam) + 1.0;
+    dr = dr < -1 ? -1 : (dr > 1 ? 1 : dr);
+  }
+  double used = 0.0, inst = 0.0;
+  for (int v = 0; v < n; ++v) {
+    int cnt = 0;
+    for (int s = 0; s < Sd; ++s) cnt += S.placement[v * Sd + s];
+    inst += cnt;
+    if (cnt > 0) used += Sd > 1 ? ((double)(cnt - 1) / (Sd - 1)) * 0.5 + 0.5 : 1.0;
+  }
+  double nr = 2 * (-used / n) + 1;
+  double ir = 2 * (-inst / ((double)n * Sd)) + 1;
+  switch (K.objective) {
+    case OBJ_PRIO_FLOW: {
+      nr = ir = 0;
+      double target = K.target_success;
+      if (target != target) {
+        target = 0.9 * h->ewma_flows;
+        h->ewma_flows = 0.5 * succ_ratio + 0.5 * h->ewma_flows;
+      }
+      if (succ_ratio < target) dr = -1;
+      break;
+    }
+    case OBJ_SOFT_DEADLINE:
+      nr = ir = 0;
+      if (delay > K.soft_deadline) fr = -1;
+      else {
+        dr = -K.soft_deadline / diam;
+        dr = dr < -1 ? -1 : (dr > 1 ? 1 : dr);
+      }
+      break;
+    case OBJ_SOFT_DEADLINE_EXP: {
+      fr = nr = ir = 0;
+      double util = 1.0;
+      if (delay > K.soft_deadline) {
+        util = -log10((1.0 / K.dropoff) * (delay - K.soft_deadline));
+        util = util < 0 ? 0 : (util > 1 ? 1 : util);
+      }
+      dr = succ_ratio * util;
+      break;
+    }
+    default:
+      fr *= K.w_flow; dr *= K.w_delay; nr *= K.w_node; ir *= K.w_inst;
+  }
+  return (float)(fr + dr + nr + ir);
+}
+
+GSC_HD void write_stats(const Env& S, float* st) {
+  const Header* h = S.h;
+  st[0] = (float)h->run_processed;
+  st[1] = (float)h->run_dropped;
+  st[2] = (float)h->run_gen;
+  st[3] = (float)(h->run_processed > 0 ? h->run_e2e / h->run_processed : 0.0);
+  st[4] = (float)h->processed;
+  st[5] = (float)h->dropped;
+  st[6] = (float)h->gen;
+  st[7] = (float)h->active;
+  st[8] = (float)h->drop_reason[0];
+  st[9] = (float)h->drop_reason[1];
+  st[10] = (float)h->drop_reason[2];
+  st[11] = (float)h->drop_reason[3];
+  st[12] = (float)h->flags;
+  st[13] = (float)h->max_events;
+  st[14] = (float)h->max_procs;
+  st[15] = (float)h->max_flows;
+}
+
+// Copy this step's (post-processed) action block into the schedule table.
+GSC_HD void load_action(Env& S, const SimConst& K, const TopoDev& T, const float* act, int lane, int nlanes) {
+  const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n, P = K.n_pad;
+  const int total = n * C * Sd * n;
+  for (int i = lane; i < total; i += nlanes) {
+    const int dst = i % n;
+    int r = i / n;
+    const int sf = r % Sd; r /= Sd;
+    const int c = r % C;
+    const int src = r / C;
+    S.sched[((src * C + c) * Sd + sf) * N + dst] = (double)act[((src * K.C + c) * K.F + sf) * P + dst];
+  }
+}
+
+}  // namespace gsc
