@@ -1,6 +1,13 @@
-// Registry of HIP op launchers exposed to Python (filled as kernels are added).
+// Registry of HIP op launchers exposed to Python.
 #include <pybind11/pybind11.h>
 namespace py = pybind11;
 namespace gsc {
-void register_ops(py::module_& m) { (void)m; }
+void register_explore(py::module_& m);
+void register_gnn(py::module_& m);
+void register_optim(py::module_& m);
+void register_ops(py::module_& m) {
+  register_explore(m);
+  register_gnn(m);
+  register_optim(m);
+}
 }  // namespace gsc

@@ -21,7 +21,7 @@ namespace py = pybind11;
 
 namespace gsc {
 
-constexpr long kMaxEventsPerStep = 50000000;  // runaway guard (no GPU hang on a bad state)
+constexpr long kMaxEventsPerStep = 4000000;  // runaway guard (no GPU hang on a bad state)
 
 struct SimArgs {
   char* states;

@@ -1,0 +1,263 @@
+"""DDPG learner + batched device trainer.
+
+Learner (reference ``SimpleDDPG._update_critic/_update_actor/_update_target_networks``,
+``simple_ddpg.py:204-234``), per update on a replay batch:
+
+    y  = r + (1 - d) * gamma * Q'(s', clamp(mu'(s'), -1, 1))            (Q5: clamp kept)
+    Lq = mse(Q(s, a), y)                   -> Adam(critic)  (+ Polyak of the critic target)
+    La = -mean(Q(s, mu(s)))                -> Adam(actor)   (+ Polyak of the actor target)
+
+Each network lives in one flat fp32 buffer (:class:`FlatParams`), so an update is: fused GNN
+kernels + MLP GEMMs (bf16 autocast, fp32 master weights) + one all-reduce per network (data
+parallel) + one fused Adam/Polyak kernel per network.  The critic's parameters are frozen while
+the actor loss is differentiated (the reference computes and later discards those gradients).
+
+Trainer: E environments of the batched simulator step in lockstep; one iteration =
+act (actor forward) -> exploration + post-processing kernel -> simulator kernel -> replay add
+-> ``updates_per_step`` learner updates of ``batch_size`` samples.
+"""
+from __future__ import annotations
+
+import copy
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from gsc_amd.models import Actor, GraphSet, QNetwork
+from gsc_amd.ops import FlatParams, FusedAdamPolyak, explore_postprocess
+from gsc_amd.parallel.dist import DistInfo, allreduce_sum_, broadcast_tensors
+from gsc_amd.sim.batched import BatchedSimulator
+from .replay import Batch, DeviceReplay
+
+
+class DDPGLearner:
+    def __init__(self, cfg: dict, obs_dim: int, action_dim: int, graphs: GraphSet, C: int, F_: int, device,
+                 dist_info: Optional[DistInfo] = None, amp_bf16: Optional[bool] = None, seed: int = 0):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.graphs = graphs
+        self.dist = dist_info or DistInfo()
+        torch.manual_seed(seed)
+        self.actor = Actor(cfg, obs_dim, action_dim).to(self.device)
+        self.critic = QNetwork(cfg, obs_dim, action_dim).to(self.device)
+        self.target_actor = copy.deepcopy(self.actor)
+        self.target_critic = copy.deepcopy(self.critic)
+        self.actor_flat = FlatParams(self.actor)
+        self.critic_flat = FlatParams(self.critic)
+        self.target_actor_flat = FlatParams(self.target_actor)
+        self.target_critic_flat = FlatParams(self.target_critic)
+        for m in (self.target_actor, self.target_critic):
+            for p in m.parameters():
+                p.requires_grad_(False)
+        # identical replicas on every rank
+        broadcast_tensors([self.actor_flat.flat, self.critic_flat.flat, self.target_actor_flat.flat,
+                           self.target_critic_flat.flat])
+        lr = float(cfg.get("learning_rate", 1e-3))
+        tau = float(cfg.get("target_model_update", 1e-4))
+        self.gamma = float(cfg.get("gamma", 0.99))
+        self.critic_opt = FusedAdamPolyak(self.critic_flat, lr=lr, target=self.target_critic_flat, tau=tau)
+        self.actor_opt = FusedAdamPolyak(self.actor_flat, lr=lr, target=self.target_actor_flat, tau=tau)
+        self.masks = graphs.action_masks(C, F_)
+        self.amp = (self.device.type == "cuda") if amp_bf16 is None else bool(amp_bf16)
+        self.updates = 0
+        self.last: Dict[str, torch.Tensor] = {}
+
+    def _autocast(self):
+        if self.amp:
+            return torch.autocast(device_type=self.device.type, dtype=torch.bfloat16)
+        return torch.autocast(device_type=self.device.type, enabled=False)
+
+    @torch.no_grad()
+    def act(self, obs: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:
+        with self._autocast():
+            return self.actor(obs, topo, self.graphs, self.masks).float()
+
+    def _allreduce(self, flat: FlatParams):
+        return allreduce_sum_(flat.grad, async_op=True)
+
+    def update(self, b: Batch) -> None:
+        g, masks = self.graphs, self.masks
+        inv_world = 1.0 / self.dist.world_size
+        with torch.no_grad(), self._autocast():
+            a2 = self.target_actor(b.next_obs, b.topo, g, masks).float().clamp(-1, 1)
+            q2 = self.target_critic(b.next_obs, b.topo, g, masks, a2).float().view(-1)
+            y = b.rewards + (1 - b.dones) * self.gamma * q2
+        with self._autocast():
+            q = self.critic(b.obs, b.topo, g, masks, b.actions).float().view(-1)
+            lq = F.mse_loss(q, y)
+        grads = torch.autograd.grad(lq, self.critic_flat.params)
+        self.critic_flat.set_grads(grads)
+        h_c = self._allreduce(self.critic_flat)
+        # actor forward overlaps the critic-gradient all-reduce (it does not read critic weights)
+        with self._autocast():
+            a = self.actor(b.obs, b.topo, g, masks)
+        if h_c is not None:
+            h_c.wait()
+        self.critic_opt.step(grad_scale=inv_world)
+        for p in self.critic_flat.params:
+            p.requires_grad_(False)
+        with self._autocast():
+            la = -self.critic(b.obs, b.topo, g, masks, a).float().mean()
+        grads = torch.autograd.grad(la, self.actor_flat.params)
+        for p in self.critic_flat.params:
+            p.requires_grad_(True)
+        self.actor_flat.set_grads(grads)
+        h_a = self._allreduce(self.actor_flat)
+        if h_a is not None:
+            h_a.wait()
+        self.actor_opt.step(grad_scale=inv_world)
+        self.updates += 1
+        self.last = {"qf1_loss": lq.detach(), "actor_loss": la.detach(), "qf1_values": q.detach().mean()}
+
+    # checkpointing --------------------------------------------------------------------------
+    def state_dict(self) -> dict:
+        return {"actor": self.actor_flat.view().detach().clone(), "critic": self.critic_flat.view().detach().clone(),
+                "target_actor": self.target_actor_flat.view().detach().clone(),
+                "target_critic": self.target_critic_flat.view().detach().clone(),
+                "actor_opt": self.actor_opt.state_dict(), "critic_opt": self.critic_opt.state_dict(),
+                "updates": self.updates}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.actor_flat.load_flat_(sd["actor"].to(self.device))
+        self.critic_flat.load_flat_(sd["critic"].to(self.device))
+        self.target_actor_flat.load_flat_(sd["target_actor"].to(self.device))
+        self.target_critic_flat.load_flat_(sd["target_critic"].to(self.device))
+        self.actor_opt.load_state_dict({k: (v.to(self.device) if torch.is_tensor(v) else v)
+                                        for k, v in sd["actor_opt"].items()})
+        self.critic_opt.load_state_dict({k: (v.to(self.device) if torch.is_tensor(v) else v)
+                                         for k, v in sd["critic_opt"].items()})
+        self.updates = int(sd.get("updates", 0))
+
+
+@dataclass
+class TrainerConfig:
+    num_envs: int = 256
+    batch_size: Optional[int] = None        # default: 100 * num_envs (reference: 100 samples per env step)
+    updates_per_step: int = 1
+    learning_starts: Optional[int] = None   # iterations; default: nb_steps_warmup_critic
+    replay_capacity: Optional[int] = None   # default: mem_limit * num_envs (capped)
+    replay_cap_max: int = 2_000_000
+    seed: int = 0
+    check_every: int = 50
+    overlap_sim: bool = True                # run the simulator kernel on its own stream, concurrent with updates
+
+
+class BatchedTrainer:
+    """E lockstep environments on the device simulator + DDPG learner (one process per GPU)."""
+
+    def __init__(self, cfg: dict, sim: BatchedSimulator, tcfg: TrainerConfig, dist_info: Optional[DistInfo] = None,
+                 network_schedule: Optional[Sequence[int]] = None, period: int = 0):
+        self.cfg = cfg
+        self.sim = sim
+        self.t = tcfg
+        self.dist = dist_info or DistInfo()
+        self.device = sim.device
+        self.E = sim.E
+        self.graphs = GraphSet(sim.topologies, sim.n_pad, self.device)
+        self.learner = DDPGLearner(cfg, sim.n_obs, sim.action_dim, self.graphs, sim.C, sim.F, self.device,
+                                   self.dist, seed=tcfg.seed)
+        cap = tcfg.replay_capacity or min(int(cfg.get("mem_limit", 10000)) * self.E, tcfg.replay_cap_max)
+        self.replay = DeviceReplay(max(cap, self.E), sim.n_pad, sim.n_obs, sim.action_dim, self.device,
+                                   seed=tcfg.seed + 7919 * self.dist.rank)
+        self.batch_size = tcfg.batch_size or 100 * self.E
+        self.learning_starts = (tcfg.learning_starts if tcfg.learning_starts is not None
+                                else int(cfg.get("nb_steps_warmup_critic", 200)))
+        self.rand_mu = float(cfg.get("rand_mu", 0.0))
+        self.rand_sigma = float(cfg.get("rand_sigma", 0.3))
+        self.global_step = 0
+        self.episode = 0
+        self.schedule = list(network_schedule) if network_schedule else [0]
+        self.period = int(period) if period else 0
+        self.sim.set_topologies(self.schedule[0])
+        self.obs = self.sim.reset().clone()
+        self.topo = self.sim.topo_cur.to(torch.int64).clone()
+        self.masks = self.learner.masks
+        self.act_buf = torch.empty(self.E, sim.action_dim, device=self.device)
+        # device-side metric accumulators (read back only when logging)
+        self.acc_succ = torch.zeros((), dtype=torch.float64, device=self.device)
+        self.acc_drop = torch.zeros((), dtype=torch.float64, device=self.device)
+        self.acc_return = torch.zeros((), dtype=torch.float64, device=self.device)
+        self.acc_episodes = torch.zeros((), dtype=torch.float64, device=self.device)
+        self.episode_returns: List[float] = []
+        self.sim_stream = (torch.cuda.Stream(self.device) if self.device.type == "cuda" and tcfg.overlap_sim
+                           else None)
+
+    def _schedule_next(self) -> None:
+        """Network scheduler: topology used by the episode that starts after this step."""
+        steps = self.sim.episode_steps
+        if (self.global_step + 1) % steps == 0:
+            nxt = self.episode + 1
+            idx = (nxt // self.period) % len(self.schedule) if self.period else 0
+            self.sim.set_topologies(self.schedule[idx])
+
+    def step(self) -> None:
+        warm = self.global_step < self.learning_starts
+        mu = self.learner.act(self.obs, self.topo)
+        act = explore_postprocess(mu, self.masks.index_select(0, self.topo), self.sim.n_pad, warm, self.rand_mu,
+                                  self.rand_sigma, seed=self.t.seed * 131 + self.dist.rank, step=self.global_step,
+                                  out=self.act_buf)
+        self._schedule_next()
+        train = self.global_step >= self.learning_starts - 1 and len(self.replay) > 0
+        if self.sim_stream is not None and train:
+            # simulator kernel (one wave per env) runs concurrently with the learner update, which
+            # samples transitions already in the replay ring (up to the previous step)
+            main = torch.cuda.current_stream(self.device)
+            self.sim_stream.wait_stream(main)
+            with torch.cuda.stream(self.sim_stream):
+                out = self.sim.step(act)
+            for _ in range(self.t.updates_per_step):
+                self.learner.update(self.replay.sample(self.batch_size))
+            main.wait_stream(self.sim_stream)
+            train = False
+        else:
+            out = self.sim.step(act)
+        self.replay.add(self.obs, self.topo, act, out.reward, out.next_obs, out.done)
+        st = out.stats
+        self.acc_succ += st[:, 0].sum()
+        self.acc_drop += st[:, 1].sum()
+        d = out.done.to(torch.float64)
+        self.acc_return += (out.ep_return.to(torch.float64) * d).sum()
+        self.acc_episodes += d.sum()
+        self.obs.copy_(out.obs)
+        if (self.global_step + 1) % self.sim.episode_steps == 0:
+            self.episode += 1
+            self.topo = self.sim.topo_next.to(torch.int64).clone()
+        if train:
+            for _ in range(self.t.updates_per_step):
+                self.learner.update(self.replay.sample(self.batch_size))
+        self.global_step += 1
+        if self.t.check_every and self.global_step % self.t.check_every == 0:
+            self.sim.check_flags()
+
+    def metrics(self, reset: bool = True) -> dict:
+        vals = torch.stack([self.acc_succ, self.acc_drop, self.acc_return, self.acc_episodes])
+        allreduce_sum_(vals)
+        s, d, r, e = [float(v) for v in vals.cpu()]
+        if reset:
+            for t in (self.acc_succ, self.acc_drop, self.acc_return, self.acc_episodes):
+                t.zero_()
+        out = {"success_ratio": s / (s + d) if s + d > 0 else 0.0, "succ": s, "drop": d, "episodes": e,
+               "mean_episode_return": r / e if e > 0 else float("nan")}
+        for k, v in self.learner.last.items():
+            out[k] = float(v)
+        return out
+
+    def state_dict(self) -> dict:
+        return {"learner": self.learner.state_dict(), "global_step": self.global_step, "episode": self.episode,
+                "sim_states": self.sim.states.cpu(), "obs": self.obs.cpu(), "topo": self.topo.cpu(),
+                "replay": self.replay.state_dict(), "rng": self.replay.gen.get_state()}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.learner.load_state_dict(sd["learner"])
+        self.global_step = int(sd["global_step"])
+        self.episode = int(sd["episode"])
+        self.sim.states.copy_(sd["sim_states"].to(self.device))
+        self.obs.copy_(sd["obs"].to(self.device))
+        self.topo = sd["topo"].to(self.device)
+        self.replay.load_state_dict(sd["replay"])
+        self.replay.gen.set_state(sd["rng"])

@@ -1,0 +1,89 @@
+"""Per-topology message-passing tables for batched GNN evaluation.
+
+The reference collates PyG ``Data`` objects into a ``Batch`` every update (``buffer.py:64-84``).
+Here every topology used in a run is registered once; a batch of graphs is then just
+``(x [B, n_pad, F], topo_id [B])``.  For each topology the table holds the GATv2 message list
+in PyG order — the bidirectional edges of ``from_networkx`` followed by one self loop per node
+(``GATv2Conv(add_self_loops=True)``) — padded to ``M`` messages, plus in-degrees and the node
+mask used by ``global_mean_pool``.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import numpy as np
+import torch
+
+from gsc_amd.coordsim.reader import Topology
+
+
+class GraphSet:
+    def __init__(self, topologies: Sequence[Topology], n_pad: int, device="cpu"):
+        self.topologies = list(topologies)
+        self.n_pad = int(n_pad)
+        T = len(self.topologies)
+        msgs = []
+        for t in self.topologies:
+            ei = t.edge_index()
+            keep = ei[0] != ei[1]
+            ei = ei[:, keep]
+            loops = np.arange(t.n, dtype=np.int64)
+            msgs.append((np.concatenate([ei[0], loops]), np.concatenate([ei[1], loops])))
+        self.M = max(len(s) for s, _ in msgs)
+        src = np.zeros((T, self.M), np.int64)
+        dst = np.zeros((T, self.M), np.int64)
+        valid = np.zeros((T, self.M), bool)
+        deg = np.ones((T, self.n_pad), np.float32)
+        node_mask = np.zeros((T, self.n_pad), np.float32)
+        n_nodes = np.zeros(T, np.float32)
+        for i, (t, (s, d)) in enumerate(zip(self.topologies, msgs)):
+            m = len(s)
+            src[i, :m], dst[i, :m], valid[i, :m] = s, d, True
+            cnt = np.bincount(d, minlength=self.n_pad).astype(np.float32)
+            deg[i] = np.maximum(cnt, 1.0)
+            node_mask[i, :t.n] = 1.0
+            n_nodes[i] = t.n
+        dev = torch.device(device)
+        self.src = torch.from_numpy(src).to(dev)
+        self.dst = torch.from_numpy(dst).to(dev)
+        self.valid = torch.from_numpy(valid).to(dev)
+        self.deg = torch.from_numpy(deg).to(dev)
+        self.node_mask = torch.from_numpy(node_mask).to(dev)
+        self.n_nodes = torch.from_numpy(n_nodes).to(dev)
+        # int32/int16 copies for the HIP kernels
+        self.src_i32 = self.src.to(torch.int32)
+        self.dst_i32 = self.dst.to(torch.int32)
+        self.num_msgs = torch.tensor([len(s) for s, _ in msgs], dtype=torch.int32, device=dev)
+        # CSR views of the message list (stable in message order) for the fused HIP kernels:
+        # messages into each node (softmax + aggregation) and out of each node (d x_l).
+        self.max_nodes = max(t.n for t in self.topologies)
+        in_ptr = np.zeros((T, self.n_pad + 1), np.int32)
+        out_ptr = np.zeros((T, self.n_pad + 1), np.int32)
+        in_msg = np.zeros((T, self.M), np.int32)
+        out_msg = np.zeros((T, self.M), np.int32)
+        for i, (s, d) in enumerate(msgs):
+            for key, ptr, lst in ((d, in_ptr, in_msg), (s, out_ptr, out_msg)):
+                order = np.argsort(key, kind="stable")
+                lst[i, :len(order)] = order
+                cnt = np.bincount(key, minlength=self.n_pad)
+                ptr[i, 1:] = np.cumsum(cnt)
+        self.in_ptr = torch.from_numpy(in_ptr).to(dev)
+        self.in_msg = torch.from_numpy(in_msg).to(dev)
+        self.out_ptr = torch.from_numpy(out_ptr).to(dev)
+        self.out_msg = torch.from_numpy(out_msg).to(dev)
+        self.n_nodes_i32 = self.n_nodes.to(torch.int32)
+
+    @property
+    def num_topologies(self) -> int:
+        return len(self.topologies)
+
+    def to(self, device) -> "GraphSet":
+        return GraphSet(self.topologies, self.n_pad, device)
+
+    def action_masks(self, C: int, F: int) -> torch.Tensor:
+        """``[T, n_pad*C*F*n_pad]`` masks with ones on each topology's real ``[:n, :, :, :n]`` block."""
+        P = self.n_pad
+        out = torch.zeros((self.num_topologies, P, C, F, P), dtype=torch.float32)
+        for i, t in enumerate(self.topologies):
+            out[i, :t.n, :, :, :t.n] = 1
+        return out.reshape(self.num_topologies, -1).to(self.src.device)

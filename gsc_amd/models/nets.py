@@ -1,0 +1,117 @@
+"""Actor and critic (reference: ``src/rlsp/agents/models.py:55-154``).
+
+Actor (graph mode): ``emb = GNN(obs)``; ``MLP([emb | mask]) * mask`` with PyG ``MLP`` semantics
+(ReLU between layers, plain last layer, no norm) and **no output squashing** (Q6).
+Critic: ``MLP([GNN(obs) | mask | action]) -> Q``.
+
+The action mask is a per-topology constant, so its contribution to the first layer,
+``mask @ W1[:, H:H+A]^T``, is evaluated once per topology and added like a bias instead of
+multiplying a ``[B, A]`` block of known zeros/ones (bit-for-bit the same function and the same
+gradients — autograd sees the mask columns of ``W1`` through that per-topology product).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .gnn import GNNEmbedder
+from .graphs import GraphSet
+
+
+def select_rows(table: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:
+    """``table[topo]`` for a per-topology table ``[T, D]``.
+
+    A single topology broadcasts (no [B, D] materialisation, and the backward is a plain column
+    sum); several topologies use a one-hot GEMM, whose backward is again a GEMM instead of an
+    atomic scatter-add of B rows into T rows."""
+    if table.shape[0] == 1:
+        return table
+    onehot = F.one_hot(topo, table.shape[0]).to(table.dtype)
+    return onehot @ table
+
+
+class MaskedInputMLP(nn.Module):
+    """PyG-style MLP whose input is ``[dense | mask(topology) | extra]``; mask block folded per topology."""
+
+    def __init__(self, dense_dim: int, mask_dim: int, extra_dim: int, hidden: Sequence[int], out_dim: int):
+        super().__init__()
+        self.dense_dim, self.mask_dim, self.extra_dim = dense_dim, mask_dim, extra_dim
+        dims = [dense_dim + mask_dim + extra_dim, *hidden, out_dim]
+        self.layers = nn.ModuleList([nn.Linear(dims[i], dims[i + 1]) for i in range(len(dims) - 1)])
+
+    @property
+    def first(self) -> nn.Linear:
+        return self.layers[0]
+
+    def first_layer(self, dense, topo, masks, extra=None):
+        W = self.first.weight
+        D, A = self.dense_dim, self.mask_dim
+        h = F.linear(dense, W[:, :D], self.first.bias)
+        topo_bias = F.linear(masks, W[:, D:D + A])           # [T, h1]
+        h = h + select_rows(topo_bias, topo)
+        if extra is not None:
+            h = h + F.linear(extra, W[:, D + A:])
+        return h
+
+    def forward(self, dense, topo, masks, extra=None):
+        h = self.first_layer(dense, topo, masks, extra)
+        for layer in self.layers[1:]:
+            h = layer(F.relu(h))
+        return h
+
+    def forward_full(self, x):
+        """Unfolded reference: ``x`` is the explicit concatenation (used by tests)."""
+        h = x
+        for i, layer in enumerate(self.layers):
+            h = layer(h if i == 0 else F.relu(h))
+        return h
+
+
+def _embedder(cfg: dict, in_dim: int) -> GNNEmbedder:
+    return GNNEmbedder(input_dim=in_dim, hidden_dim=int(cfg["GNN_features"]), num_layers=int(cfg["GNN_num_layers"]),
+                       aggr=cfg.get("GNN_aggr", "mean"), num_iter=int(cfg["GNN_num_iter"]))
+
+
+class Actor(nn.Module):
+    def __init__(self, cfg: dict, obs_dim: int, action_dim: int, low=0.0, high=1.0):
+        super().__init__()
+        if not cfg.get("graph_mode", True):
+            raise NotImplementedError("non-graph (flat) mode is dimensionally broken in the reference (Q13)")
+        self.embedder = _embedder(cfg, obs_dim)
+        H = self.embedder.hidden_dim
+        self.action_dim = action_dim
+        self.mlp = MaskedInputMLP(H, action_dim, 0, list(cfg["actor_hidden_layer_nodes"]), action_dim)
+        self.low, self.high = float(low), float(high)
+
+    def forward(self, x, topo, graphs: GraphSet, masks: torch.Tensor):
+        emb = self.embedder(x, topo, graphs)
+        out = self.mlp(emb, topo, masks)
+        return out * select_rows(masks, topo)
+
+    def scale_action(self, a):
+        return 2.0 * ((a - self.low) / (self.high - self.low)) - 1.0
+
+    def unscale_action(self, a):
+        return self.low + (0.5 * (a + 1.0) * (self.high - self.low))
+
+
+class QNetwork(nn.Module):
+    def __init__(self, cfg: dict, obs_dim: int, action_dim: int):
+        super().__init__()
+        if not cfg.get("graph_mode", True):
+            raise NotImplementedError("non-graph (flat) mode is dimensionally broken in the reference (Q13)")
+        self.embedder = _embedder(cfg, obs_dim)
+        H = self.embedder.hidden_dim
+        self.mlp = MaskedInputMLP(H, action_dim, action_dim, list(cfg["critic_hidden_layer_nodes"]), 1)
+
+    def forward(self, x, topo, graphs: GraphSet, masks: torch.Tensor, action: torch.Tensor):
+        emb = self.embedder(x, topo, graphs)
+        return self.mlp(emb, topo, masks, action)
+
+
+def count_params(m: nn.Module) -> int:
+    return sum(p.numel() for p in m.parameters())

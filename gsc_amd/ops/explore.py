@@ -1,0 +1,78 @@
+"""Exploration noise + schedule post-processing (reference ``simple_ddpg.py:182-201, 338-395``).
+
+Per env: ``a = unscale(scale(mu(s)) + N(rand_mu, rand_sigma))`` clipped to ``[0, 1]`` (warm-up:
+``U[0,1) * mask``), then for every ``(src, sfc, sf)`` slice of ``n_pad`` destination weights,
+twice: zero weights below the threshold and renormalise (all-zero -> uniform ``round(1/P, 10)``,
+residual of the rounded sum added to the first element that can absorb it).
+
+``explore_postprocess`` dispatches to the fused HIP kernel for CUDA tensors (one thread per
+slice, fp64 arithmetic like the reference's Python floats) and to the vectorised PyTorch
+reference below otherwise.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+ACCURACY = math.sqrt(torch.finfo(torch.float64).eps)
+
+
+def _round10(x: torch.Tensor) -> torch.Tensor:
+    return torch.round(x * 1e10) / 1e10
+
+
+def normalize_slices_reference(p: torch.Tensor, threshold: float = 0.1, passes: int = 2) -> torch.Tensor:
+    """p [..., P] float64 -> thresholded, normalised weights (vectorised reference)."""
+    p = p.to(torch.float64)
+    P = p.shape[-1]
+    for _ in range(passes):
+        p = torch.where(p >= threshold, p, torch.zeros_like(p))
+        s = p.sum(-1, keepdim=True)
+        uni = torch.full_like(p, round(1.0 / P, 10))
+        div = _round10(p / torch.where(s == 0, torch.ones_like(s), s))
+        keep = (1 - s).abs() <= ACCURACY
+        out = torch.where(s == 0, uni, torch.where(keep, p, div))
+        resid = 1 - out.sum(-1, keepdim=True)
+        # first index whose value can absorb the residual
+        ok = (out + resid) >= 0
+        first = torch.argmax(ok.to(torch.int8), dim=-1, keepdim=True)
+        add = torch.zeros_like(out).scatter_(-1, first, resid)
+        p = out + add
+    return p
+
+
+def explore_postprocess_reference(mu: torch.Tensor, mask: torch.Tensor, n_pad: int, warmup: bool,
+                                  rand_mu: float, rand_sigma: float, generator: Optional[torch.Generator] = None,
+                                  threshold: float = 0.1, passes: int = 2) -> torch.Tensor:
+    E, A = mu.shape
+    if warmup:
+        a = torch.rand(E, A, generator=generator, device=mu.device, dtype=torch.float32) * mask
+    else:
+        noise = torch.randn(E, A, generator=generator, device=mu.device, dtype=torch.float32) * rand_sigma + rand_mu
+        scaled = 2.0 * mu.float() - 1.0 + noise
+        a = (0.5 * (scaled + 1.0)).clamp(0.0, 1.0)
+    out = normalize_slices_reference(a.double().view(E, A // n_pad, n_pad), threshold, passes)
+    return out.view(E, A).float()
+
+
+def explore_postprocess(mu: torch.Tensor, mask: torch.Tensor, n_pad: int, warmup: bool, rand_mu: float,
+                        rand_sigma: float, seed: int, step: int, threshold: float = 0.1, passes: int = 2,
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """mu [E, A] actor output, mask [E, A] -> post-processed actions [E, A] (float32)."""
+    if mu.is_cuda:
+        from gsc_amd.native import load
+        nat = load()
+        E, A = mu.shape
+        mu = mu.contiguous().float()
+        mask = mask.contiguous().float()
+        if out is None:
+            out = torch.empty(E, A, device=mu.device, dtype=torch.float32)
+        nat.explore_postprocess(mu.data_ptr(), mask.data_ptr(), out.data_ptr(), E, A, n_pad, int(warmup),
+                                float(rand_mu), float(rand_sigma), int(seed) & 0xffffffff, int(step),
+                                float(threshold), int(passes), torch.cuda.current_stream(mu.device).cuda_stream)
+        return out
+    g = torch.Generator(device=mu.device)
+    g.manual_seed((int(seed) * 1000003 + int(step)) & 0x7fffffffffffffff)
+    return explore_postprocess_reference(mu, mask, n_pad, warmup, rand_mu, rand_sigma, g, threshold, passes)

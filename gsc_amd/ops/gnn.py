@@ -1,0 +1,93 @@
+"""Autograd wrapper around the fused HIP GATv2 embedder kernels (``csrc/ops/gnn.hip``)."""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from gsc_amd.native import load as load_native
+
+
+def _tables(graphs) -> dict:
+    t = getattr(graphs, "_kernel_tables", None)
+    if t is None:
+        t = dict(src=graphs.src_i32.data_ptr(), dst=graphs.dst_i32.data_ptr(), in_ptr=graphs.in_ptr.data_ptr(),
+                 in_msg=graphs.in_msg.data_ptr(), out_ptr=graphs.out_ptr.data_ptr(),
+                 out_msg=graphs.out_msg.data_ptr(), deg=graphs.deg.data_ptr(), nnodes=graphs.n_nodes_i32.data_ptr(),
+                 nmsgs=graphs.num_msgs.data_ptr(), M=int(graphs.M), NM=int(graphs.max_nodes))
+        graphs._kernel_tables = t
+    return t
+
+
+def _layer_of(embedder) -> List[int]:
+    seq = [0]
+    if embedder.num_layers > 1:
+        for _ in range(embedder.num_iter):
+            seq.extend(range(1, embedder.num_layers))
+    return seq
+
+
+def _flat(params: List[torch.Tensor]) -> torch.Tensor:
+    """Contiguous fp32 view of the embedder parameters (zero-copy when they already are one flat run)."""
+    first = params[0]
+    total = sum(p.numel() for p in params)
+    base = first.data_ptr()
+    contiguous = all(p.is_contiguous() for p in params)
+    off = 0
+    for p in params:
+        if not contiguous or p.data_ptr() != base + off * 4 or p.dtype != torch.float32:
+            return torch.cat([q.detach().reshape(-1).float() for q in params])
+        off += p.numel()
+    return first.detach().reshape(-1) if total == first.numel() else \
+        torch.as_strided(first.detach(), (total,), (1,))
+
+
+_PARTIALS = {}
+
+
+class _GnnEmbed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, topo, graphs, meta, *params):
+        nat = load_native()
+        B, P, Fin = x.shape
+        H, layer_of = meta
+        flat = _flat(list(params))
+        x = x.contiguous().float()
+        topo = topo.to(torch.int32).contiguous()
+        emb = torch.empty(B, H, device=x.device, dtype=torch.float32)
+        if B > 0:
+            nat.gnn_forward(_tables(graphs), flat.data_ptr(), x.data_ptr(), topo.data_ptr(), emb.data_ptr(), B, P, Fin,
+                            H, layer_of, torch.cuda.current_stream(x.device).cuda_stream)
+        ctx.save_for_backward(x, topo, flat)
+        ctx.graphs, ctx.meta = graphs, meta
+        ctx.shapes = [p.shape for p in params]
+        return emb
+
+    @staticmethod
+    def backward(ctx, demb):
+        nat = load_native()
+        x, topo, flat = ctx.saved_tensors
+        H, layer_of = ctx.meta
+        B, P, Fin = x.shape
+        grad = torch.empty_like(flat)
+        rows = 1024
+        key = (x.device, flat.numel())
+        partials = _PARTIALS.get(key)
+        if partials is None:
+            partials = _PARTIALS[key] = torch.empty(rows, flat.numel(), device=x.device, dtype=torch.float32)
+        nat.gnn_backward(_tables(ctx.graphs), flat.data_ptr(), x.data_ptr(), topo.data_ptr(),
+                         demb.contiguous().float().data_ptr(), partials.data_ptr(), rows, grad.data_ptr(), B, P, Fin,
+                         H, layer_of, torch.cuda.current_stream(x.device).cuda_stream)
+        out, off = [], 0
+        for s in ctx.shapes:
+            n = 1
+            for d in s:
+                n *= d
+            out.append(grad[off:off + n].view(s))
+            off += n
+        return (None, None, None, None, *out)
+
+
+def gnn_embed(embedder, x: torch.Tensor, topo: torch.Tensor, graphs) -> torch.Tensor:
+    params = embedder.flat_parameters()
+    return _GnnEmbed.apply(x, topo, graphs, (embedder.hidden_dim, _layer_of(embedder)), *params)

@@ -1,0 +1,104 @@
+"""Flat parameter buffers + fused Adam/Polyak (``csrc/ops/optim.hip``).
+
+``FlatParams`` re-points every parameter of a module at a slice of one contiguous fp32 buffer,
+so a whole network is one tensor for the optimizer kernel, for the Polyak update and for the
+single data-parallel all-reduce of its gradient.  Semantics match ``torch.optim.Adam`` defaults
+(the reference optimizer, ``simple_ddpg.py:162-163``) followed by the Polyak soft update
+(``simple_ddpg.py:229-234``).
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional
+
+import torch
+import torch.nn as nn
+
+
+class FlatParams:
+    def __init__(self, module: nn.Module, align: int = 4):
+        self.module = module
+        self.params: List[nn.Parameter] = [p for p in module.parameters()]
+        total = 0
+        self.offsets = []
+        for p in self.params:
+            self.offsets.append(total)
+            total += p.numel()
+        self.numel = total
+        dev = self.params[0].device
+        pad = (-total) % align
+        self.flat = torch.zeros(total + pad, device=dev, dtype=torch.float32)
+        for p, o in zip(self.params, self.offsets):
+            self.flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
+            p.data = self.flat[o:o + p.numel()].view_as(p)
+        self.grad = torch.zeros_like(self.flat)
+
+    def view(self) -> torch.Tensor:
+        return self.flat[: self.numel]
+
+    def grad_view(self) -> torch.Tensor:
+        return self.grad[: self.numel]
+
+    def set_grads(self, grads: Iterable[Optional[torch.Tensor]]) -> torch.Tensor:
+        """Write per-parameter gradients (``None`` = zero) into the flat gradient buffer."""
+        for p, o, g in zip(self.params, self.offsets, grads):
+            dst = self.grad[o:o + p.numel()]
+            if g is None:
+                dst.zero_()
+            else:
+                dst.copy_(g.reshape(-1))
+        return self.grad
+
+    def load_flat_(self, src: torch.Tensor) -> None:
+        self.flat[: self.numel].copy_(src[: self.numel])
+
+
+class FusedAdamPolyak:
+    """Adam over a :class:`FlatParams` buffer with an optional fused Polyak update of a target buffer."""
+
+    def __init__(self, flat: FlatParams, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 target: Optional[FlatParams] = None, tau: float = 0.0):
+        self.fp = flat
+        self.lr, self.betas, self.eps, self.wd = float(lr), betas, float(eps), float(weight_decay)
+        self.target, self.tau = target, float(tau)
+        self.m = torch.zeros_like(flat.flat)
+        self.v = torch.zeros_like(flat.flat)
+        self.step_count = 0
+
+    def state_dict(self) -> dict:
+        return {"m": self.m, "v": self.v, "step": self.step_count, "lr": self.lr, "betas": self.betas,
+                "eps": self.eps}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.step_count = int(sd["step"])
+
+    @torch.no_grad()
+    def step(self, grad_scale: float = 1.0) -> None:
+        self.step_count += 1
+        p, g = self.fp.flat, self.fp.grad
+        t = self.target.flat if self.target is not None else None
+        if p.is_cuda:
+            from gsc_amd.native import load
+            load().adam_polyak(p.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                               t.data_ptr() if t is not None else 0, p.numel(), self.lr, self.betas[0],
+                               self.betas[1], self.eps, self.step_count, self.tau if t is not None else 0.0,
+                               float(grad_scale), self.wd, torch.cuda.current_stream(p.device).cuda_stream)
+            return
+        adam_polyak_reference(p, g * grad_scale, self.m, self.v, t, self.step_count, self.lr, self.betas, self.eps,
+                              self.tau, self.wd)
+
+
+@torch.no_grad()
+def adam_polyak_reference(p, g, m, v, target, step, lr, betas, eps, tau, weight_decay=0.0):
+    b1, b2 = betas
+    if weight_decay:
+        g = g + weight_decay * p
+    m.lerp_(g, 1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    bc1 = 1 - b1 ** step
+    bc2s = (1 - b2 ** step) ** 0.5
+    denom = (v.sqrt() / bc2s).add_(eps)
+    p.addcdiv_(m, denom, value=-(lr / bc1))
+    if target is not None:
+        target.copy_(tau * p + (1 - tau) * target)
