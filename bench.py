@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--agent-config", default="configs/config/agent/sample_agent.yaml")
     ap.add_argument("--device", default=None)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-overlap", action="store_true", help="run the simulator on the learner's stream")
     args = ap.parse_args()
 
     import torch
@@ -62,7 +63,8 @@ def main():
     sim = load_batched_from_paths([args.network], args.service, args.sim_config, cfg, args.envs, device=device,
                                   seed=args.seed * 1000 + info.rank)
     tcfg = TrainerConfig(num_envs=args.envs, batch_size=args.batch_size, updates_per_step=args.updates_per_step,
-                         learning_starts=1, seed=args.seed + 17 * info.rank, check_every=0)
+                         learning_starts=1, seed=args.seed + 17 * info.rank, check_every=0,
+                         overlap_sim=not args.no_overlap)
     trainer = BatchedTrainer(cfg, sim, tcfg, info)
 
     def sync():
@@ -115,6 +117,7 @@ def main():
                 "total_envs": total_envs,
                 "learner_batch_per_gpu": trainer.batch_size,
                 "updates_per_step": args.updates_per_step,
+                "sim_learner_overlap": not args.no_overlap,
                 "topology": os.path.basename(args.network),
                 "device": torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu",
             },

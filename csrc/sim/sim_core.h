@@ -40,24 +40,25 @@ enum Objective { OBJ_PRIO_FLOW = 0, OBJ_SOFT_DEADLINE = 1, OBJ_SOFT_DEADLINE_EXP
 enum Flags { FLAG_FLOW_OVERFLOW = 1, FLAG_PROC_OVERFLOW = 2, FLAG_EVENT_OVERFLOW = 4, FLAG_BAD_STATE = 8 };
 constexpr int16_t kStopProc = -2;
 
-struct Event {     // 16 B
+struct alignas(16) Event {  // 16 B
   double t;
   uint32_t key;    // (priority << 31) | event id
   int16_t proc;
   uint16_t pad;
 };
 
-struct Proc {      // 32 B
+struct alignas(16) Proc {  // 32 B
   uint8_t type, state;
   int16_t flow, parent, a, b, c, ret, pad;
   double x, y;
 };
 
-struct Flow {      // 56 B
+struct alignas(16) Flow {  // 64 B: four 16-byte LDS accesses per copy
   double dr, duration, e2e, ttl, creation;
   int32_t id;
   int16_t node, egress, sfc, pos, cur_sf, ingress;
   uint8_t departed, fwd_eg, dropped, proc_idx;
+  int32_t pad0, pad1;
 };
 
 struct Header {
@@ -291,7 +292,7 @@ GSC_HD void free_flow(Env& S, int fid) { S.flow_free[S.h->flow_top++] = (int16_t
 // ------------------------------------------------------------------------------------------------
 // Metrics hooks (reference coordsim/metrics/metrics.py)
 // ------------------------------------------------------------------------------------------------
-GSC_HD void reset_run_metrics(Env& S, const SimConst& K, int n) {
+GSC_HD_CALL void reset_run_metrics(Env& S, const SimConst& K, int n) {
   Header* h = S.h;
   h->run_gen = h->run_processed = h->run_dropped = 0;
   h->run_e2e = h->run_max_e2e = h->run_total_path_delay = h->run_avg_path_delay = 0.0;
@@ -303,7 +304,7 @@ GSC_HD void reset_run_metrics(Env& S, const SimConst& K, int n) {
   (void)K; (void)n;
 }
 
-GSC_HD void dropped_flow(Env& S, Flow& f, int reason) {
+GSC_HD_CALL void dropped_flow(Env& S, Flow& f, int reason) {
   Header* h = S.h;
   f.dropped = 1;
   h->dropped++; h->active--; h->run_dropped++;
@@ -311,10 +312,16 @@ GSC_HD void dropped_flow(Env& S, Flow& f, int reason) {
   S.drop_locs[f.node * (S.d.S + 1) + sf]++;
   S.run_drop_node[f.node]++;
   if (f.ttl <= 0) reason = R_TTL;
-  h->drop_reason[reason]++;
+  // constant-index updates keep the header promotable to registers
+  switch (reason) {
+    case R_TTL: h->drop_reason[0]++; break;
+    case R_DECISION: h->drop_reason[1]++; break;
+    case R_LINK: h->drop_reason[2]++; break;
+    default: h->drop_reason[3]++; break;
+  }
 }
 
-GSC_HD void completed_flow(Env& S, const Flow& f) {
+GSC_HD_CALL void completed_flow(Env& S, const Flow& f) {
   Header* h = S.h;
   h->processed++; h->run_processed++; h->active--;
   h->total_e2e += f.e2e;
@@ -332,6 +339,10 @@ GSC_HD void add_path_delay(Env& S, double d) {
 
 // ------------------------------------------------------------------------------------------------
 // Process handlers
+//
+// Each handler works on register copies of its process record (and flow record) — two/four
+// 16-byte LDS loads — and writes back only what it changed before yielding.  A process that
+// returns is freed by proc_return (its record is never written back afterwards).
 // ------------------------------------------------------------------------------------------------
 GSC_HD void end_flow(Env& S, int pid, int fid) {
   free_flow(S, fid);
@@ -339,25 +350,26 @@ GSC_HD void end_flow(Env& S, int pid, int fid) {
 }
 
 // FlowSimulator.handle_flow (flowsimulator.py:72-128)
-GSC_HD void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  Proc& P = S.procs[pid];
+GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  const Proc P = S.procs[pid];
   const int fid = P.flow;
-  Flow& f = S.flows[fid];
+  Flow f = S.flows[fid];
+  uint8_t state = P.state;
   for (;;) {
-    switch (P.state) {
+    switch (state) {
       case H_LOOP:
         if (f.departed) {
           completed_flow(S, f);
           end_flow(S, pid, fid);
           return;
         }
-        P.state = H_AFTER_DECIDE;
+        S.procs[pid].state = H_AFTER_DECIDE;
         spawn(S, P_DECIDE, D_INIT, fid, pid);
         return;
       case H_AFTER_DECIDE: {
         const int nxt = P.ret;
         if (nxt < 0) { dropped_flow(S, f, R_DECISION); end_flow(S, pid, fid); return; }
-        P.state = H_AFTER_FWD;
+        S.procs[pid].state = H_AFTER_FWD;
         const int c = spawn(S, P_FORWARD, F_INIT, fid, pid);
         if (c >= 0) S.procs[c].b = (int16_t)nxt;
         return;
@@ -365,15 +377,15 @@ GSC_HD void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid) {
       case H_AFTER_FWD:
         if (!P.ret) { dropped_flow(S, f, R_LINK); end_flow(S, pid, fid); return; }
         if (!f.fwd_eg) {
-          P.state = H_AFTER_PROC;
+          S.procs[pid].state = H_AFTER_PROC;
           spawn(S, P_PROCESS, PR_INIT, fid, pid);
           return;
         }
-        P.state = H_LOOP;
+        state = H_LOOP;
         break;
       case H_AFTER_PROC:
         if (!P.ret) { dropped_flow(S, f, R_NODE); end_flow(S, pid, fid); return; }
-        P.state = H_LOOP;
+        state = H_LOOP;
         break;
       default:
         S.h->flags |= FLAG_BAD_STATE;
@@ -384,33 +396,34 @@ GSC_HD void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid) {
 }
 
 // DefaultDecisionMaker.decide_next_node (default_decision_maker.py:18-81): weighted round robin.
-GSC_HD void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  Proc& P = S.procs[pid];
+GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  const Proc P = S.procs[pid];
   if (P.state == D_INIT) {
-    P.state = D_RUN;
+    S.procs[pid].state = D_RUN;
     timeout(S, pid, 0.0);
     return;
   }
-  Flow& f = S.flows[P.flow];
+  Flow f = S.flows[P.flow];
   if (f.ttl <= 0) { proc_return(S, pid, -1); return; }
   if (f.fwd_eg) {
-    if (f.egress < 0) f.egress = f.node;
-    proc_return(S, pid, f.egress);
+    if (f.egress < 0) S.flows[P.flow].egress = f.node;
+    proc_return(S, pid, f.egress < 0 ? f.node : f.egress);
     return;
   }
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
   const int sf = K.chain[f.sfc * kMaxF + f.pos];
-  f.cur_sf = (int16_t)sf;
+  S.flows[P.flow].cur_sf = (int16_t)sf;
   S.requested[(f.node * C + f.sfc) * Sd + sf] += f.dr;
   const int row = ((f.node * C + f.sfc) * Sd + sf) * N;
   const double* p = S.sched + row;
   int32_t* cnt = S.wrr + row;
-  long total = 0;
+  int total = 0;
   for (int d = 0; d < n; ++d) total += cnt[d];
   int best = 0;
   double best_v = -1e300;
+  const double inv_total = total > 0 ? 1.0 : 0.0;
   for (int d = 0; d < n; ++d) {
-    const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0;
+    const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0 * inv_total;
     const double diff = p[d] > 0 ? p[d] - ratio : -1.0;
     if (diff > best_v) { best_v = diff; best = d; }
   }
@@ -419,16 +432,17 @@ GSC_HD void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid) {
 }
 
 // DefaultFlowForwarder.forward_flow (default_forwarder.py:21-90) + return_link_resources.
-GSC_HD void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  Proc& P = S.procs[pid];
-  Flow& f = S.flows[P.flow];
+GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc P = S.procs[pid];
+  const int fid = P.flow;
+  Flow f = S.flows[fid];
   const int n = T.n;
   const int nxt = P.b;
   if (P.state == F_INIT) {
     const int cur = f.node;
     const double pd = (cur != nxt) ? T.pdelay[cur * n + nxt] : 0.0;
-    if (f.ttl - pd <= 0) { f.ttl = 0; proc_return(S, pid, 0); return; }
-    if (cur == f.egress && f.fwd_eg) f.departed = 1;
+    if (f.ttl - pd <= 0) { S.flows[fid].ttl = 0; proc_return(S, pid, 0); return; }
+    if (cur == f.egress && f.fwd_eg) { f.departed = 1; S.flows[fid].departed = 1; }
     if (cur == nxt) { proc_return(S, pid, 1); return; }
     P.a = (int16_t)cur;
     P.c = 0;
@@ -444,6 +458,10 @@ GSC_HD void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid) {
       add_path_delay(S, P.x);
       f.e2e += P.x;
       f.ttl -= P.x;
+      Flow& fm = S.flows[fid];
+      fm.node = f.node;
+      fm.e2e = f.e2e;
+      fm.ttl = f.ttl;
       proc_return(S, pid, 1);
       return;
     }
@@ -452,24 +470,28 @@ GSC_HD void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid) {
   const int hop = T.pnodes[(P.a * n + nxt) * T.H + P.c];
   const int cur = f.node;
   const int e = T.edge_id[cur * n + hop];
-  if (S.link_rem[e] - f.dr >= 0) {
-    S.link_rem[e] -= f.dr;
+  Flow& fm = S.flows[fid];
+  fm.node = f.node;
+  const double lrem = S.link_rem[e];
+  if (lrem - f.dr >= 0) {
+    S.link_rem[e] = lrem - f.dr;
   } else {
     proc_return(S, pid, 0);
     return;
   }
   S.link_passed[e] += f.dr;
   const double hd = T.pdelay[cur * n + hop];
-  if (hop == f.egress && f.fwd_eg) f.departed = 1;
+  if (hop == f.egress && f.fwd_eg) fm.departed = 1;
   P.state = F_AFTER_HOP;
+  S.procs[pid] = P;
   timeout(S, pid, hd);
   (void)K;
 }
 
-GSC_HD void run_retlink(Env& S, int pid) {
-  Proc& P = S.procs[pid];
+GSC_HD_CALL void run_retlink(Env& S, int pid) {
+  const Proc P = S.procs[pid];
   if (P.state == RL_INIT) {
-    P.state = RL_AFTER;
+    S.procs[pid].state = RL_AFTER;
     timeout(S, pid, P.y);
     return;
   }
@@ -478,34 +500,36 @@ GSC_HD void run_retlink(Env& S, int pid) {
 }
 
 // DefaultFlowProcessor.process_flow (default_processor.py:14-50) + get_processing_delay.
-GSC_HD void run_process(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  Proc& P = S.procs[pid];
+GSC_HD_CALL void run_process(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  Proc P = S.procs[pid];
   const int fid = P.flow;
-  Flow& f = S.flows[fid];
   const int Sd = S.d.S;
   if (P.state == PR_INIT) {
+    Flow f = S.flows[fid];
     const int node = f.node;
     const int sf = K.chain[f.sfc * kMaxF + f.pos];
-    f.cur_sf = (int16_t)sf;
+    Flow& fm = S.flows[fid];
+    fm.cur_sf = (int16_t)sf;
     if (!S.placement[node * Sd + sf]) { proc_return(S, pid, 0); return; }
     const double pd = fabs(rng_normal(S, K.pd_mean[sf], K.pd_std[sf]));
-    if (f.ttl - pd <= 0) { f.ttl = 0; proc_return(S, pid, 0); return; }
+    if (f.ttl - pd <= 0) { fm.ttl = 0; proc_return(S, pid, 0); return; }
     S.h->num_proc_delays++;
     S.h->total_proc_delay += pd;
-    f.e2e += pd;
-    f.ttl -= pd;
+    fm.e2e = f.e2e + pd;
+    fm.ttl = f.ttl - pd;
     if (pd == 0.0) { proc_return(S, pid, 0); return; }  // reference: `if not processing_delay`
     P.x = pd;
     P.a = (int16_t)node;
     P.b = (int16_t)sf;
     P.state = PR_AFTER_REQ;
+    S.procs[pid] = P;
     const int c = spawn(S, P_REQUEST, RQ_INIT, fid, pid);
     if (c >= 0) { S.procs[c].a = (int16_t)node; S.procs[c].b = (int16_t)sf; }
     return;
   }
   if (P.state == PR_AFTER_REQ) {
     if (!P.ret) { proc_return(S, pid, 0); return; }
-    P.state = PR_AFTER_WAIT;
+    S.procs[pid].state = PR_AFTER_WAIT;
     timeout(S, pid, P.x);
     return;
   }
@@ -517,17 +541,18 @@ GSC_HD void run_process(Env& S, const SimConst& K, const TopoDev& T, int pid) {
 }
 
 // BaseFlowProcessor.request_resources (base_processor.py:51-101).
-GSC_HD void run_request(Env& S, const SimConst& K, int pid) {
-  Proc& P = S.procs[pid];
+GSC_HD_CALL void run_request(Env& S, const SimConst& K, int pid) {
+  const Proc P = S.procs[pid];
   if (P.state == RQ_AFTER) { proc_return(S, pid, 1); return; }
-  Flow& f = S.flows[P.flow];
+  Flow f = S.flows[P.flow];
   const int node = P.a, sf = P.b, Sd = S.d.S;
   double demanded = 0.0;
   for (int s = 0; s < Sd; ++s)
     if (S.sf_present[node * Sd + s]) demanded += S.sf_load[node * Sd + s] + (s == sf ? f.dr : 0.0);
   const double cap = S.node_cap[node];
   if (!(demanded <= cap)) { proc_return(S, pid, 0); return; }
-  f.proc_idx++;
+  Flow& fm = S.flows[P.flow];
+  fm.proc_idx = f.proc_idx + 1;
   S.proc_traffic[node * Sd + sf] += f.dr;
   S.sf_load[node * Sd + sf] += f.dr;
   S.node_rem[node] = cap - demanded;
@@ -535,10 +560,10 @@ GSC_HD void run_request(Env& S, const SimConst& K, int pid) {
   const double ready = S.sf_start[node * Sd + sf] + K.startup[sf];
   if (!(ready <= S.h->now)) {
     const double rem = ready - S.h->now;
-    if (f.ttl - rem <= 0) { f.ttl = 0; proc_return(S, pid, 0); return; }
-    f.e2e += rem;
-    f.ttl -= rem;
-    P.state = RQ_AFTER;
+    if (f.ttl - rem <= 0) { fm.ttl = 0; proc_return(S, pid, 0); return; }
+    fm.e2e = f.e2e + rem;
+    fm.ttl = f.ttl - rem;
+    S.procs[pid].state = RQ_AFTER;
     timeout(S, pid, rem);
     return;
   }
@@ -546,21 +571,25 @@ GSC_HD void run_request(Env& S, const SimConst& K, int pid) {
 }
 
 // BaseFlowProcessor.finish_processing (base_processor.py:103-135).
-GSC_HD void run_finish(Env& S, const SimConst& K, int pid) {
-  Proc& P = S.procs[pid];
+GSC_HD_CALL void run_finish(Env& S, const SimConst& K, int pid) {
+  const Proc P = S.procs[pid];
   const int Sd = S.d.S;
   if (P.state == FI_INIT) {
-    Flow& f = S.flows[P.flow];
-    f.pos++;
-    if (f.pos == K.chain_len[f.sfc]) f.fwd_eg = 1;
-    P.x = f.dr;
-    P.state = FI_AFTER;
+    const Flow f = S.flows[P.flow];
+    Flow& fm = S.flows[P.flow];
+    const int pos = f.pos + 1;
+    fm.pos = (int16_t)pos;
+    if (pos == K.chain_len[f.sfc]) fm.fwd_eg = 1;
+    Proc& pm = S.procs[pid];
+    pm.x = f.dr;
+    pm.state = FI_AFTER;
     timeout(S, pid, f.duration);
     return;
   }
   const int node = P.a, sf = P.b;
-  S.sf_load[node * Sd + sf] -= P.x;
-  if (S.sf_load[node * Sd + sf] == 0.0 && !S.placement[node * Sd + sf]) S.sf_present[node * Sd + sf] = 0;
+  const double load = S.sf_load[node * Sd + sf] - P.x;
+  S.sf_load[node * Sd + sf] = load;
+  if (load == 0.0 && !S.placement[node * Sd + sf]) S.sf_present[node * Sd + sf] = 0;
   double used = 0.0;
   for (int s = 0; s < Sd; ++s)
     if (S.sf_present[node * Sd + s]) used += S.sf_load[node * Sd + s];
@@ -569,9 +598,8 @@ GSC_HD void run_finish(Env& S, const SimConst& K, int pid) {
 }
 
 // FlowSimulator.init_arrival + DefaultFlowGenerator.generate_flow.
-GSC_HD void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  Proc& P = S.procs[pid];
-  const int node = P.a;
+GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  const int node = S.procs[pid].a;
   const double mean = S.inter_arr[node];
   if (mean != mean) { proc_return(S, pid, 0); return; }  // None: arrivals at this node stop
   Header* h = S.h;
@@ -588,7 +616,7 @@ GSC_HD void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid) {
   const double ttl = K.ttl[rng_int(S, K.n_ttl)];
   const int fid = alloc_flow(S);
   if (fid >= 0) {
-    Flow& f = S.flows[fid];
+    Flow f;
     f.dr = dr;
     f.duration = (size / dr) * 1000.0;
     f.e2e = 0.0;
@@ -602,6 +630,9 @@ GSC_HD void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid) {
     f.pos = 0;
     f.cur_sf = -1;
     f.departed = f.fwd_eg = f.dropped = f.proc_idx = 0;
+    f.pad0 = 0;
+    f.pad1 = 0;
+    S.flows[fid] = f;
     h->gen++; h->run_gen++; h->active++;
     if (spawn(S, P_HANDLE, H_LOOP, fid, -1) < 0) free_flow(S, fid);
   } else {
@@ -611,23 +642,22 @@ GSC_HD void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid) {
 }
 
 // ResultWriter.begin_writing / write_network_state: the run-window clock.
-GSC_HD void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  Proc& P = S.procs[pid];
-  switch (P.state) {
+GSC_HD_CALL void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+  switch (S.procs[pid].state) {
     case W_BEGIN:
     case W_AFTER:
       respawn_self(S, pid, W_INIT);
       return;
     default:  // W_INIT
       reset_run_metrics(S, K, T.n);
-      P.state = W_AFTER;
+      S.procs[pid].state = W_AFTER;
       timeout(S, pid, K.run_duration);
       return;
   }
 }
 
 // SimulatorParams.start_mmpp / update_state: 2-state MMPP arrivals.
-GSC_HD void run_mmpp(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+GSC_HD_CALL void run_mmpp(Env& S, const SimConst& K, const TopoDev& T, int pid) {
   Proc& P = S.procs[pid];
   if (P.state == M_START) {
     P.state = M_AFTER;
@@ -650,7 +680,7 @@ GSC_HD void run_mmpp(Env& S, const SimConst& K, const TopoDev& T, int pid) {
 }
 
 // TraceProcessor.process_trace.
-GSC_HD void run_trace(Env& S, const SimConst& K, const TopoDev& T, int pid) {
+GSC_HD_CALL void run_trace(Env& S, const SimConst& K, const TopoDev& T, int pid) {
   Proc& P = S.procs[pid];
   const int i = S.h->trace_index;
   if (P.state == TR_INIT) {
@@ -718,15 +748,11 @@ GSC_HD void remove_event(Env& S, int idx) {
 // ------------------------------------------------------------------------------------------------
 // Episode init / controller apply / observation + reward epilogue
 // ------------------------------------------------------------------------------------------------
-GSC_HD void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo, uint32_t seed, int episode) {
+GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo, uint32_t seed, int episode) {
   Header* h = S.h;
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
   const double ewma = h->ewma_flows;
-  // zero header
-  {
-    char* p = (char*)h;
-    for (int i = 0; i < (int)sizeof(Header); ++i) p[i] = 0;
-  }
+  *h = Header{};
   h->topo = topo;
   h->ewma_flows = episode <= 1 ? 1.0 : ewma;
   h->episode = episode;
@@ -777,30 +803,35 @@ GSC_HD void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo, uint
 
 // SimulatorWrapper.apply (placement derivation) + DurationController.get_next_state prologue.
 // The schedule table S.sched must already hold this step's action.
-GSC_HD void controller_prologue(Env& S, const SimConst& K, const TopoDev& T) {
+GSC_HD_CALL void controller_prologue(Env& S, const SimConst& K, const TopoDev& T) {
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
   for (int i = 0; i < N * Sd; ++i) S.placement[i] = 0;
   // follow positive weights from every active ingress along each chain (add_placement_recursive)
   for (int c = 0; c < K.C; ++c) {
-    uint64_t fr[4] = {0, 0, 0, 0};  // node bitset (n <= 256)
+    uint64_t f0 = 0, f1 = 0, f2 = 0, f3 = 0;  // node bitset (n <= 256)
     for (int i = 0; i < T.n_ing; ++i) {
       const int v = T.ingress[i];
-      if (S.inter_arr[v] == S.inter_arr[v]) fr[v >> 6] |= 1ull << (v & 63);
+      if (S.inter_arr[v] == S.inter_arr[v]) {
+        const uint64_t b = 1ull << (v & 63);
+        if (v < 64) f0 |= b; else if (v < 128) f1 |= b; else if (v < 192) f2 |= b; else f3 |= b;
+      }
     }
     for (int k = 0; k < K.chain_len[c]; ++k) {
       const int sf = K.chain[c * kMaxF + k];
-      uint64_t nx[4] = {0, 0, 0, 0};
+      uint64_t n0 = 0, n1 = 0, n2 = 0, n3 = 0;
       for (int src = 0; src < n; ++src) {
-        if (!((fr[src >> 6] >> (src & 63)) & 1)) continue;
+        const uint64_t w = src < 64 ? f0 : (src < 128 ? f1 : (src < 192 ? f2 : f3));
+        if (!((w >> (src & 63)) & 1)) continue;
         const double* row = S.sched + ((src * C + c) * Sd + sf) * N;
         for (int dst = 0; dst < n; ++dst) {
           if (row[dst] > 0) {
             S.placement[dst * Sd + sf] = 1;
-            nx[dst >> 6] |= 1ull << (dst & 63);
+            const uint64_t b = 1ull << (dst & 63);
+            if (dst < 64) n0 |= b; else if (dst < 128) n1 |= b; else if (dst < 192) n2 |= b; else n3 |= b;
           }
         }
       }
-      for (int w = 0; w < 4; ++w) fr[w] = nx[w];
+      f0 = n0; f1 = n1; f2 = n2; f3 = n3;
     }
   }
   // available_sf rebuild: keep SFs that still carry load, (re)create placed ones
@@ -853,7 +884,7 @@ GSC_HD float obs_feature(const Env& S, const SimConst& K, int q, int v) {
   return cap == 0.0 ? 1.f : (float)(use / cap);
 }
 
-GSC_HD void write_obs(const Env& S, const SimConst& K, const TopoDev& T, float* obs) {
+GSC_HD_CALL void write_obs(const Env& S, const SimConst& K, const TopoDev& T, float* obs) {
   const int n = T.n;
   for (int j = 0; j < K.n_obs; ++j) {
     const int q = K.obs_feat[j];
@@ -867,7 +898,7 @@ GSC_HD void write_obs(const Env& S, const SimConst& K, const TopoDev& T, float* 
   }
 }
 
-GSC_HD float compute_reward(Env& S, const SimConst& K, const TopoDev& T) {
+GSC_HD_CALL float compute_reward(Env& S, const SimConst& K, const TopoDev& T) {
   Header* h = S.h;
   const int succ = h->run_processed, drop = h->run_dropped, Sd = S.d.S, n = T.n;
   double succ_ratio = 0.0, fr = 0.0;

@@ -42,10 +42,12 @@ struct SimArgs {
   float* ep_return;          // [E]  return of the episode that just finished (valid where done)
   int E;
   int use_lds;
+  long topo_stage;           // bytes of LDS reserved for the staged topology tables
+  unsigned long long* prof;  // optional [E, 4] cycle counters: select, dispatch, merge, events (diagnostic)
+  unsigned long long* prof_types;  // optional [E, 16, 2] dispatch cycles / count per process type
 };
 
-GSC_HD void step_epilogue(Env& S, const SimArgs& a, int env) {
-  const SimConst& K = a.K;
+GSC_HD void step_epilogue(Env& S, const SimArgs& a, const SimConst& K, int env) {
   const TopoDev& T = a.topos[S.h->topo];
   const long ostride = (long)K.n_pad * K.n_obs;
   S.h->run_times++;
@@ -85,7 +87,8 @@ __device__ __forceinline__ void copy16(char* dst, const char* src, long bytes, i
 }
 
 __device__ __forceinline__ int argmin_event_wave(const Env& S, int lane) {
-  const int ne = S.h->n_events;
+  // the header copy is authoritative in lane 0 (the only lane that runs handlers)
+  const int ne = __builtin_amdgcn_readfirstlane(S.h->n_events);
   double bt = 1e300;
   uint32_t bk = 0xffffffffu;
   int bi = -1;
@@ -104,49 +107,242 @@ __device__ __forceinline__ int argmin_event_wave(const Env& S, int lane) {
   return bi;
 }
 
-__device__ __forceinline__ void device_step_env(const SimArgs& a, char* base, int env, int lane) {
-  Env S(base, a.L, a.D);
-  const TopoDev& T = a.topos[S.h->topo];
-  load_action(S, a.K, T, a.actions + (long)env * a.action_stride, lane, 64);
-  __syncthreads();
+// Bytes of LDS used to stage SimConst + the env's topology tables in front of the state blob.
+__host__ __device__ inline long topo_stage_bytes(const Dims& D, int H) {
+  const long n2 = (long)D.N * D.N;
+  return align16(sizeof(TopoDev)) + align16((int)(8 * D.N)) + align16((int)(8 * n2)) + align16((int)(2 * n2)) +
+         align16((int)(2 * n2 * H)) + align16((int)(2 * n2)) + align16((int)(8 * D.E)) + 2 * align16(2 * D.N);
+}
+__host__ __device__ inline long const_stage_bytes() { return align16(sizeof(SimConst)); }
+
+// Copy one topology's tables into LDS and return a TopoDev whose pointers address the copies.
+__device__ __forceinline__ TopoDev stage_topo(const TopoDev& g, char* dst, int lane) {
+  TopoDev t = g;
+  const int n = g.n, n2 = n * n;
+  char* p = dst;
+  auto put = [&](const void* src, int bytes) -> char* {
+    char* d = p;
+    const int w = bytes >> 1;  // 16-bit granules (every table is 2- or 8-byte typed)
+    for (int i = lane; i < w; i += 64) reinterpret_cast<int16_t*>(d)[i] = reinterpret_cast<const int16_t*>(src)[i];
+    p += align16(bytes);
+    return d;
+  };
+  t.cap = (const double*)put(g.cap, 8 * n);
+  t.pdelay = (const double*)put(g.pdelay, 8 * n2);
+  t.plen = (const int16_t*)put(g.plen, 2 * n2);
+  t.pnodes = (const int16_t*)put(g.pnodes, 2 * n2 * g.H);
+  t.edge_id = (const int16_t*)put(g.edge_id, 2 * n2);
+  t.edge_cap = (const double*)put(g.edge_cap, 8 * (g.E > 0 ? g.E : 1));
+  t.ingress = (const int16_t*)put(g.ingress, 2 * (g.n_ing > 0 ? g.n_ing : 1));
+  t.egress = (const int16_t*)put(g.egress, 2 * (g.n_eg > 0 ? g.n_eg : 1));
+  return t;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Sorted pending-event queue held in VGPRs across the wave: entry s*64+l lives in lane l, set s.
+// pop = readfirstlane + DPP wave_shl:1, insert = ballot/popcount rank + DPP wave_shr:1 — no LDS.
+// ------------------------------------------------------------------------------------------------
+constexpr int DPP_WAVE_SHL1 = 0x130;
+constexpr int DPP_WAVE_SHR1 = 0x138;
+
+template <int QS>
+struct RegQueue {
+  uint32_t tlo[QS], thi[QS], key[QS];
+  int32_t proc[QS];
+  int n;
+};
+
+__device__ __forceinline__ double pack_t(uint32_t lo, uint32_t hi) {
+  return __hiloint2double((int)hi, (int)lo);
+}
+
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t v, uint32_t lane0_in) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)lane0_in, (int)v, DPP_WAVE_SHR1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t dpp_shl1(uint32_t v, uint32_t lane63_in) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)lane63_in, (int)v, DPP_WAVE_SHL1, 0xF, 0xF, false);
+}
+
+template <int QS>
+__device__ __forceinline__ void rq_init(RegQueue<QS>& q) {
+#pragma unroll
+  for (int s = 0; s < QS; ++s) { q.tlo[s] = 0xffffffffu; q.thi[s] = 0x7fefffffu; q.key[s] = 0xffffffffu; q.proc[s] = -1; }
+  q.n = 0;
+}
+
+template <int QS>
+__device__ __forceinline__ bool rq_insert(RegQueue<QS>& q, double t, uint32_t key, int proc, int lane) {
+  if (q.n >= QS * 64) return false;
+  int pos = 0;
+#pragma unroll
+  for (int s = 0; s < QS; ++s) {
+    if (s * 64 >= q.n) break;  // wave-uniform: only sets that hold entries
+    const double et = pack_t(q.tlo[s], q.thi[s]);
+    const bool less = (s * 64 + lane < q.n) && (et < t || (et == t && q.key[s] < key));
+    pos += __popcll(__ballot(less));
+  }
+  const uint32_t tlo = (uint32_t)__double2loint(t), thi = (uint32_t)__double2hiint(t);
+  // shift entries >= pos up by one, high set first (each set's carry is the previous set's lane 63)
+#pragma unroll
+  for (int s = QS - 1; s >= 0; --s) {
+    if (s * 64 > q.n || (s + 1) * 64 <= pos) continue;  // set untouched by this insert
+    const uint32_t c_tlo = s ? (uint32_t)__builtin_amdgcn_readlane((int)q.tlo[s - 1], 63) : 0u;
+    const uint32_t c_thi = s ? (uint32_t)__builtin_amdgcn_readlane((int)q.thi[s - 1], 63) : 0u;
+    const uint32_t c_key = s ? (uint32_t)__builtin_amdgcn_readlane((int)q.key[s - 1], 63) : 0u;
+    const uint32_t c_prc = s ? (uint32_t)__builtin_amdgcn_readlane(q.proc[s - 1], 63) : 0u;
+    const uint32_t sh_tlo = dpp_shr1(q.tlo[s], c_tlo), sh_thi = dpp_shr1(q.thi[s], c_thi);
+    const uint32_t sh_key = dpp_shr1(q.key[s], c_key), sh_prc = dpp_shr1((uint32_t)q.proc[s], c_prc);
+    const int idx = s * 64 + lane;
+    if (idx > pos) { q.tlo[s] = sh_tlo; q.thi[s] = sh_thi; q.key[s] = sh_key; q.proc[s] = (int)sh_prc; }
+    else if (idx == pos) { q.tlo[s] = tlo; q.thi[s] = thi; q.key[s] = key; q.proc[s] = proc; }
+  }
+  q.n++;
+  return true;
+}
+
+template <int QS>
+__device__ __forceinline__ void rq_pop(RegQueue<QS>& q, double& t, int& proc) {
+  t = pack_t((uint32_t)__builtin_amdgcn_readfirstlane((int)q.tlo[0]), (uint32_t)__builtin_amdgcn_readfirstlane((int)q.thi[0]));
+  proc = __builtin_amdgcn_readfirstlane(q.proc[0]);
+#pragma unroll
+  for (int s = 0; s < QS; ++s) {
+    if (s * 64 >= q.n) break;  // remaining sets are empty
+    const uint32_t c_tlo = s + 1 < QS ? (uint32_t)__builtin_amdgcn_readfirstlane((int)q.tlo[s + 1]) : 0xffffffffu;
+    const uint32_t c_thi = s + 1 < QS ? (uint32_t)__builtin_amdgcn_readfirstlane((int)q.thi[s + 1]) : 0x7fefffffu;
+    const uint32_t c_key = s + 1 < QS ? (uint32_t)__builtin_amdgcn_readfirstlane((int)q.key[s + 1]) : 0xffffffffu;
+    const uint32_t c_prc = s + 1 < QS ? (uint32_t)__builtin_amdgcn_readfirstlane(q.proc[s + 1]) : 0xffffffffu;
+    q.tlo[s] = dpp_shl1(q.tlo[s], c_tlo);
+    q.thi[s] = dpp_shl1(q.thi[s], c_thi);
+    q.key[s] = dpp_shl1(q.key[s], c_key);
+    q.proc[s] = (int)dpp_shl1((uint32_t)q.proc[s], c_prc);
+  }
+  q.n--;
+}
+
+// Merge the events lane 0's handler appended to S.events (the inbox) into the register queue.
+template <int QS>
+__device__ __forceinline__ void rq_merge_inbox(RegQueue<QS>& q, Env& S, int lane) {
+  const int nin = __builtin_amdgcn_readfirstlane(S.h->n_events);
+  for (int i = 0; i < nin; ++i) {
+    const Event e = S.events[i];
+    if (!rq_insert(q, e.t, e.key, e.proc, lane) && lane == 0) S.h->flags |= FLAG_EVENT_OVERFLOW;
+  }
   if (lane == 0) {
-    controller_prologue(S, a.K, T);
-    schedule_stop(S, a.K);
+    if (q.n > S.h->max_events) S.h->max_events = q.n;
+    S.h->n_events = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int QS>
+__device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst& K, char* base, char* topo_lds,
+                                                int env, int lane) {
+  Env S(base, a.L, a.D);
+  // Keep the env header in registers for the whole window (written back once at the end).
+  Header* const h_mem = S.h;
+  Header h_reg = *h_mem;
+  S.h = &h_reg;
+  const TopoDev T = stage_topo(a.topos[S.h->topo], topo_lds, lane);
+  load_action(S, K, T, a.actions + (long)env * a.action_stride, lane, 64);
+  __syncthreads();
+  // pending events -> sorted register queue; S.events then serves as the handlers' inbox
+  RegQueue<QS> q;
+  rq_init(q);
+  rq_merge_inbox(q, S, lane);
+  if (lane == 0) {
+    controller_prologue(S, K, T);
+    schedule_stop(S, K);
   }
   __syncthreads();
+  rq_merge_inbox(q, S, lane);
+  const bool prof = a.prof != nullptr;
+  unsigned long long t_sel = 0, t_hdl = 0, t_mrg = 0, n_ev = 0;
+  const unsigned long long t_begin = prof ? __builtin_amdgcn_s_memtime() : 0;
   for (long it = 0;; ++it) {
-    const int idx = argmin_event_wave(S, lane);
-    if (idx < 0 || it > kMaxEventsPerStep) {
+    const unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    if (q.n <= 0 || it > kMaxEventsPerStep) {
       if (lane == 0) S.h->flags |= FLAG_BAD_STATE;
       break;
     }
-    const Event ev = S.events[idx];
-    __syncthreads();
-    if (lane == 0) {
-      remove_event(S, idx);
-      S.h->now = ev.t;
-      if (ev.proc != kStopProc) dispatch(S, a.K, T, ev.proc);
+    double et;
+    int ep;
+    rq_pop(q, et, ep);
+    const unsigned long long t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    if (ep == kStopProc) {
+      if (lane == 0) S.h->now = et;
+      break;
     }
-    __syncthreads();
-    if (ev.proc == kStopProc) break;
+    int ptype = 0;
+    if (lane == 0) {
+      S.h->now = et;
+      if (prof) ptype = S.procs[ep].type;
+      dispatch(S, K, T, ep);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const unsigned long long t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    rq_merge_inbox(q, S, lane);
+    if (prof) {
+      const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+      t_sel += t1 - t0;
+      t_hdl += t2 - t1;
+      t_mrg += t3 - t2;
+      n_ev++;
+      if (a.prof_types && lane == 0) {
+        a.prof_types[((long)env * 16 + ptype) * 2] += t2 - t1;
+        a.prof_types[((long)env * 16 + ptype) * 2 + 1] += 1;
+      }
+    }
+  }
+  if (prof && lane == 0) {
+    unsigned long long* pr = a.prof + (long)env * 4;
+    pr[0] += t_sel;
+    pr[1] += t_hdl;
+    pr[2] += t_mrg;
+    pr[3] += n_ev;
   }
   __syncthreads();
-  if (lane == 0) step_epilogue(S, a, env);
+  // write the queue back (sorted) as the persistent pending-event array
+  for (int s = 0; s < QS; ++s) {
+    const int idx = s * 64 + lane;
+    if (idx < q.n) {
+      Event e;
+      e.t = pack_t(q.tlo[s], q.thi[s]);
+      e.key = q.key[s];
+      e.proc = (int16_t)q.proc[s];
+      e.pad = 0;
+      S.events[idx] = e;
+    }
+  }
+  if (lane == 0) S.h->n_events = q.n;
+  __syncthreads();
+  if (lane == 0) {
+    step_epilogue(S, a, K, env);  // on episode end env_init rebuilds S.events / n_events itself
+    *h_mem = h_reg;
+  }
   __syncthreads();
 }
 
+template <int QSETS, bool LDS_STATE>
 __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int env = blockIdx.x;
   const int lane = threadIdx.x;
+  // [SimConst][topology tables][state blob (LDS mode)]
+  SimConst* Ks = reinterpret_cast<SimConst*>(smem);
+  if (lane == 0) *Ks = a.K;
+  char* topo_lds = smem + const_stage_bytes();
+  char* state_lds = topo_lds + a.topo_stage;
   char* g = a.states + (long)env * a.state_bytes;
-  if (a.use_lds) {
-    copy16(smem, g, a.state_bytes, lane);
+  if constexpr (LDS_STATE) {
+    copy16(state_lds, g, a.state_bytes, lane);
     __syncthreads();
-    device_step_env(a, smem, env, lane);
-    copy16(g, smem, a.state_bytes, lane);
+    device_step_env<QSETS>(a, *Ks, state_lds, topo_lds, env, lane);
+    copy16(g, state_lds, a.state_bytes, lane);
   } else {
-    device_step_env(a, g, env, lane);
+    __syncthreads();
+    device_step_env<QSETS>(a, *Ks, g, topo_lds, env, lane);
   }
 }
 
@@ -169,7 +365,7 @@ static void host_step_env(const SimArgs& a, int env) {
   controller_prologue(S, a.K, T);
   schedule_stop(S, a.K);
   run_until_stop_serial(S, a.K, T);
-  step_epilogue(S, a, env);
+  step_epilogue(S, a, a.K, env);
 }
 
 template <class F>
@@ -233,10 +429,21 @@ class SimContext {
       GSC_HIP_CHECK(hipGetDevice(&dev));
       int max_lds = 0;
       GSC_HIP_CHECK(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
-      use_lds_ = L_.total <= max_lds;
-      if (use_lds_ && L_.total > 65536)
-        GSC_HIP_CHECK(hipFuncSetAttribute((const void*)sim_step_kernel,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, L_.total));
+      int maxH = 1;
+      for (auto& t : topos_) maxH = t.H > maxH ? t.H : maxH;
+      topo_stage_ = topo_stage_bytes(D_, maxH);
+      const long fixed = const_stage_bytes() + topo_stage_;
+      GSC_CHECK(fixed <= max_lds, "topology tables do not fit in LDS");
+      use_lds_ = fixed + L_.total <= max_lds;
+      const long need = fixed + (use_lds_ ? L_.total : 0);
+      qsets_ = D_.event_cap <= 64 ? 1 : (D_.event_cap <= 128 ? 2 : (D_.event_cap <= 256 ? 4 : 8));
+      if (need > 65536) {
+        const void* fns[] = {(const void*)sim_step_kernel<1, true>, (const void*)sim_step_kernel<2, true>,
+                             (const void*)sim_step_kernel<4, true>, (const void*)sim_step_kernel<8, true>,
+                             (const void*)sim_step_kernel<1, false>, (const void*)sim_step_kernel<2, false>,
+                             (const void*)sim_step_kernel<4, false>, (const void*)sim_step_kernel<8, false>};
+        for (auto f : fns) GSC_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
+      }
     }
   }
   ~SimContext() {
@@ -261,12 +468,24 @@ class SimContext {
 
   void step(uintptr_t states, uintptr_t topo_next, uintptr_t seeds, uintptr_t actions, long action_stride,
             uintptr_t obs, uintptr_t next_obs, uintptr_t reward, uintptr_t done, uintptr_t stats,
-            uintptr_t ep_return, int E, uintptr_t stream) {
+            uintptr_t ep_return, int E, uintptr_t stream, uintptr_t prof) {
     SimArgs a = args(states, topo_next, seeds, actions, action_stride, obs, next_obs, reward, done, stats,
                      ep_return, E);
+    a.prof = ptr<unsigned long long>(prof);
+    a.prof_types = prof ? ptr<unsigned long long>(prof) + (long)E * 4 : nullptr;
     if (device_) {
-      const size_t lds = use_lds_ ? (size_t)L_.total : 0;
-      hipLaunchKernelGGL(sim_step_kernel, dim3(E), dim3(64), lds, stream_of(stream), a);
+      const size_t lds = const_stage_bytes() + topo_stage_ + (use_lds_ ? (size_t)L_.total : 0);
+      const hipStream_t st = stream_of(stream);
+#define GSC_LAUNCH_SIM(QS)                                                                      \
+  if (use_lds_) hipLaunchKernelGGL((sim_step_kernel<QS, true>), dim3(E), dim3(64), lds, st, a); \
+  else hipLaunchKernelGGL((sim_step_kernel<QS, false>), dim3(E), dim3(64), lds, st, a);
+      switch (qsets_) {
+        case 1: GSC_LAUNCH_SIM(1) break;
+        case 2: GSC_LAUNCH_SIM(2) break;
+        case 4: GSC_LAUNCH_SIM(4) break;
+        default: GSC_LAUNCH_SIM(8) break;
+      }
+#undef GSC_LAUNCH_SIM
       check_launch();
     } else {
       parallel_for(E, host_threads_, [&](int e) { host_step_env(a, e); });
@@ -296,6 +515,7 @@ class SimContext {
     a.ep_return = ptr<float>(ep_return);
     a.E = E;
     a.use_lds = use_lds_ ? 1 : 0;
+    a.topo_stage = topo_stage_;
     return a;
   }
 
@@ -367,6 +587,8 @@ class SimContext {
   bool device_;
   int host_threads_;
   bool use_lds_ = false;
+  long topo_stage_ = 0;
+  int qsets_ = 8;
   Dims D_{};
   Layout L_{};
   SimConst K_{};
@@ -381,7 +603,9 @@ void register_sim(py::module_& m) {
       .def_property_readonly("state_bytes", &SimContext::state_bytes)
       .def_property_readonly("use_lds", &SimContext::use_lds)
       .def("reset", &SimContext::reset)
-      .def("step", &SimContext::step);
+      .def("step", &SimContext::step, py::arg("states"), py::arg("topo_next"), py::arg("seeds"), py::arg("actions"),
+           py::arg("action_stride"), py::arg("obs"), py::arg("next_obs"), py::arg("reward"), py::arg("done"),
+           py::arg("stats"), py::arg("ep_return"), py::arg("E"), py::arg("stream"), py::arg("prof") = 0);
   m.attr("SIM_NUM_STATS") = kNumStats;
   m.attr("SIM_HEADER_BYTES") = (int)sizeof(Header);
 }

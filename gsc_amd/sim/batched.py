@@ -129,7 +129,9 @@ def _default_caps(topos: Sequence[Topology], cfg: dict) -> dict:
     ttl = max(cfg["ttl"])
     per_node = ttl / max(mean, 1e-3) * (1.0 if cfg["det_arrival"] else 2.5) + 8
     flows = int(min(4096, max(64, 2 * max_ing * per_node)))
-    return dict(flow_cap=flows, proc_cap=min(32000, 3 * flows + 32), event_cap=min(32000, 3 * flows + 32))
+    # the pending-event queue lives in VGPRs on the device (64 per set); observed peaks on the reference
+    # configs are 30-60 events, so 128 leaves 2x headroom (overflow is flagged, never silent)
+    return dict(flow_cap=flows, proc_cap=min(32000, 3 * flows + 32), event_cap=128 if max_ing <= 8 else 256)
 
 
 class BatchedSimulator:
@@ -206,6 +208,7 @@ class BatchedSimulator:
         self.stats = torch.zeros((self.E, self.native.SIM_NUM_STATS), dtype=torch.float32, device=dev)
         self.ep_return = torch.zeros(self.E, dtype=torch.float32, device=dev)
         self.topo_cur = self.topo_next.clone()
+        self.prof = None
 
     # ------------------------------------------------------------------------------------------
     def _stream(self) -> int:
@@ -224,6 +227,10 @@ class BatchedSimulator:
         self.topo_cur.copy_(self.topo_next)
         return self.obs
 
+    def enable_profiling(self, on: bool = True) -> None:
+        """Accumulate per-env cycle counters (event selection / handlers / total / events) in ``self.prof``."""
+        self.prof = torch.zeros(self.E * 4 + self.E * 32, dtype=torch.int64, device=self.device) if on else None
+
     def step(self, actions: torch.Tensor) -> SimStepOut:
         if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
             actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
@@ -231,7 +238,8 @@ class BatchedSimulator:
             raise ValueError(f"actions must be [E={self.E}, >= {self.action_dim}], got {tuple(actions.shape)}")
         self.ctx.step(self.states.data_ptr(), self.topo_next.data_ptr(), self.seeds.data_ptr(), actions.data_ptr(),
                       actions.shape[1], self.obs.data_ptr(), self.next_obs.data_ptr(), self.reward.data_ptr(),
-                      self.done.data_ptr(), self.stats.data_ptr(), self.ep_return.data_ptr(), self.E, self._stream())
+                      self.done.data_ptr(), self.stats.data_ptr(), self.ep_return.data_ptr(), self.E, self._stream(),
+                      self.prof.data_ptr() if (self.prof is not None and self.is_device) else 0)
         return SimStepOut(self.obs, self.next_obs, self.reward, self.done.bool(), self.stats, self.ep_return)
 
     def check_flags(self) -> int:

@@ -18,6 +18,7 @@ ap.add_argument("--envs", type=int, default=256)
 ap.add_argument("--steps", type=int, default=200)
 ap.add_argument("--device", default="cuda")
 ap.add_argument("--net", default="configs/networks/abilene/abilene-in4-rand-cap1-2.graphml")
+ap.add_argument("--profile", action="store_true")
 ap.add_argument("--simcfg", default="configs/config/simulator/sample_config.yaml")
 args = ap.parse_args()
 cfg = yaml.safe_load(open("configs/config/agent/sample_agent.yaml"))
@@ -34,6 +35,8 @@ for _ in range(5):
     sim.step(A)
 if args.device == "cuda":
     torch.cuda.synchronize()
+if args.profile:
+    sim.enable_profiling()
 t = time.perf_counter()
 S = D = 0.0
 for _ in range(args.steps):
@@ -44,3 +47,15 @@ dt = time.perf_counter() - t
 sim.check_flags()
 print(f"envs={args.envs} steps={args.steps} state_bytes={sim.state_bytes} lds={sim.ctx.use_lds} "
       f"env_steps_per_s={args.envs * args.steps / dt:.1f} ms_per_step={dt / args.steps * 1e3:.3f}")
+if args.profile:
+    pr = sim.prof.double().cpu()
+    p = pr[: args.envs * 4].view(-1, 4).sum(0)
+    ty = pr[args.envs * 4:].view(args.envs, 16, 2).sum(0)
+    names = ["free", "writer", "mmpp", "trace", "arrival", "handle", "decide", "forward", "process", "request",
+             "finish", "retlink"]
+    for i, nm in enumerate(names):
+        if ty[i, 1] > 0:
+            print(f"  {nm:8s} events/env-step={ty[i, 1] / (args.envs * args.steps):7.1f} "
+                  f"cycles/dispatch={ty[i, 0] / ty[i, 1]:7.0f} share={ty[i, 0] / ty[:, 0].sum():.2f}")
+    print(f"cycles/event: select={p[0] / p[3]:.0f} dispatch={p[1] / p[3]:.0f} merge={p[2] / p[3]:.0f} "
+          f"events/env-step={p[3] / (args.envs * args.steps):.0f}")
