@@ -67,6 +67,24 @@ class GraphSet:
                 lst[i, :len(order)] = order
                 cnt = np.bincount(key, minlength=self.n_pad)
                 ptr[i, 1:] = np.cumsum(cnt)
+        # CSR-ordered message arrays (channel-lane kernels): messages sorted by target node keep
+        # their source/target directly, and the source-sorted view stores positions in that order.
+        in_src = np.zeros((T, self.M), np.int32)
+        in_dst = np.zeros((T, self.M), np.int32)
+        out_q = np.zeros((T, self.M), np.int32)
+        out_dst = np.zeros((T, self.M), np.int32)
+        for i, (s, d) in enumerate(msgs):
+            m = len(s)
+            pos = np.empty(m, np.int64)
+            pos[in_msg[i, :m]] = np.arange(m)
+            in_src[i, :m] = s[in_msg[i, :m]]
+            in_dst[i, :m] = d[in_msg[i, :m]]
+            out_q[i, :m] = pos[out_msg[i, :m]]
+            out_dst[i, :m] = d[out_msg[i, :m]]
+        self.in_src = torch.from_numpy(in_src).to(dev)
+        self.in_dst = torch.from_numpy(in_dst).to(dev)
+        self.out_q = torch.from_numpy(out_q).to(dev)
+        self.out_dst = torch.from_numpy(out_dst).to(dev)
         self.in_ptr = torch.from_numpy(in_ptr).to(dev)
         self.in_msg = torch.from_numpy(in_msg).to(dev)
         self.out_ptr = torch.from_numpy(out_ptr).to(dev)

@@ -14,7 +14,9 @@ def _tables(graphs) -> dict:
         t = dict(src=graphs.src_i32.data_ptr(), dst=graphs.dst_i32.data_ptr(), in_ptr=graphs.in_ptr.data_ptr(),
                  in_msg=graphs.in_msg.data_ptr(), out_ptr=graphs.out_ptr.data_ptr(),
                  out_msg=graphs.out_msg.data_ptr(), deg=graphs.deg.data_ptr(), nnodes=graphs.n_nodes_i32.data_ptr(),
-                 nmsgs=graphs.num_msgs.data_ptr(), M=int(graphs.M), NM=int(graphs.max_nodes))
+                 nmsgs=graphs.num_msgs.data_ptr(), M=int(graphs.M), NM=int(graphs.max_nodes),
+                 in_src=graphs.in_src.data_ptr(), in_dst=graphs.in_dst.data_ptr(), out_q=graphs.out_q.data_ptr(),
+                 out_dst=graphs.out_dst.data_ptr())
         graphs._kernel_tables = t
     return t
 

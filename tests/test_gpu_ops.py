@@ -21,19 +21,34 @@ def _graphs(dev):
     return GraphSet(topos, 24, dev)
 
 
-@pytest.mark.parametrize("layers,iters", [(2, 2), (1, 1), (3, 1)])
-def test_gnn_fused_matches_reference(layers, iters):
+@pytest.mark.parametrize("path", [0, 1, 3], ids=["generic", "cl-fwd", "cl-fwd-bwd"])
+@pytest.mark.parametrize("layers,iters,hidden", [(2, 2, 22), (1, 1, 22), (3, 1, 22), (2, 2, 32), (2, 2, 40)])
+def test_gnn_fused_matches_reference(layers, iters, hidden, path):
+    """Channel-lane kernels (H <= 32, <= 2 parameter blocks) and the generic fused kernels, selected
+    via gnn_set_path; unsupported shapes fall back to the generic kernels."""
+    from gsc_amd.native import load
+    nat = load()
+    old = nat.gnn_get_path()
+    nat.gnn_set_path(path)
+    try:
+        _check_gnn(layers, iters, hidden)
+    finally:
+        nat.gnn_set_path(old)
+
+
+def _check_gnn(layers, iters, hidden):
     torch.manual_seed(0)
     gs = _graphs(DEV)
-    emb = GNNEmbedder(3, 22, layers, "mean", iters).to(DEV)
+    emb = GNNEmbedder(3, hidden, layers, "mean", iters).to(DEV)
     B = 777
     topo = torch.randint(0, 3, (B,), device=DEV)
     x = torch.rand(B, 24, 3, device=DEV) * gs.node_mask[topo].unsqueeze(-1)
     params = list(emb.parameters())
     ref = emb.forward_reference(x, topo, gs)
-    gref = torch.autograd.grad((ref * torch.linspace(-1, 1, 22, device=DEV)).sum(), params)
+    w = torch.linspace(-1, 1, hidden, device=DEV)
+    gref = torch.autograd.grad((ref * w).sum(), params)
     out = emb(x, topo, gs, use_native=True)
-    gout = torch.autograd.grad((out * torch.linspace(-1, 1, 22, device=DEV)).sum(), params)
+    gout = torch.autograd.grad((out * w).sum(), params)
     torch.testing.assert_close(out, ref, rtol=2e-5, atol=2e-5)
     for a, b in zip(gout, gref):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
