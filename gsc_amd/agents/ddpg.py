@@ -32,6 +32,7 @@ from gsc_amd.models import Actor, GraphSet, QNetwork
 from gsc_amd.ops import FlatParams, FusedAdamPolyak, explore_postprocess
 from gsc_amd.parallel.dist import DistInfo, allreduce_sum_, broadcast_tensors
 from gsc_amd.sim.batched import BatchedSimulator
+from gsc_amd.utils.tracing import trace_range
 from .replay import Batch, DeviceReplay
 
 
@@ -197,10 +198,12 @@ class BatchedTrainer:
 
     def step(self) -> None:
         warm = self.global_step < self.learning_starts
-        mu = self.learner.act(self.obs, self.topo)
-        act = explore_postprocess(mu, self.masks.index_select(0, self.topo), self.sim.n_pad, warm, self.rand_mu,
-                                  self.rand_sigma, seed=self.t.seed * 131 + self.dist.rank, step=self.global_step,
-                                  out=self.act_buf)
+        with trace_range("act"):
+            mu = self.learner.act(self.obs, self.topo)
+        with trace_range("explore"):
+            act = explore_postprocess(mu, self.masks.index_select(0, self.topo), self.sim.n_pad, warm, self.rand_mu,
+                                      self.rand_sigma, seed=self.t.seed * 131 + self.dist.rank,
+                                      step=self.global_step, out=self.act_buf)
         self._schedule_next()
         train = self.global_step >= self.learning_starts - 1 and len(self.replay) > 0
         if self.sim_stream is not None and train:
@@ -210,13 +213,16 @@ class BatchedTrainer:
             self.sim_stream.wait_stream(main)
             with torch.cuda.stream(self.sim_stream):
                 out = self.sim.step(act)
-            for _ in range(self.t.updates_per_step):
-                self.learner.update(self.replay.sample(self.batch_size))
+            with trace_range("learn"):
+                for _ in range(self.t.updates_per_step):
+                    self.learner.update(self.replay.sample(self.batch_size))
             main.wait_stream(self.sim_stream)
             train = False
         else:
-            out = self.sim.step(act)
-        self.replay.add(self.obs, self.topo, act, out.reward, out.next_obs, out.done)
+            with trace_range("sim"):
+                out = self.sim.step(act)
+        with trace_range("replay"):
+            self.replay.add(self.obs, self.topo, act, out.reward, out.next_obs, out.done)
         st = out.stats
         self.acc_succ += st[:, 0].sum()
         self.acc_drop += st[:, 1].sum()
@@ -228,8 +234,9 @@ class BatchedTrainer:
             self.episode += 1
             self.topo = self.sim.topo_next.to(torch.int64).clone()
         if train:
-            for _ in range(self.t.updates_per_step):
-                self.learner.update(self.replay.sample(self.batch_size))
+            with trace_range("learn"):
+                for _ in range(self.t.updates_per_step):
+                    self.learner.update(self.replay.sample(self.batch_size))
         self.global_step += 1
         if self.t.check_every and self.global_step % self.t.check_every == 0:
             self.sim.check_flags()

@@ -55,6 +55,7 @@ class GymEnv:
         self.simulator_factory = simulator_factory or make_simulator
         self._test_mode = test_mode
         self.simulator = None
+        self.current_network = None
         self.sim_seed = sim_seed
         self.simulator_wrapper = None
         self.current_simulator_state = None
@@ -87,6 +88,7 @@ class GymEnv:
         return bool(self.agent_helper is not None and self.agent_helper.test_mode is True)
 
     def _create_simulator(self, network):
+        self.current_network = network
         if self.agent_helper is not None:
             self.agent_helper.network_path = network
             self.agent_helper.result.env_config["network_file"] = network
@@ -102,11 +104,12 @@ class GymEnv:
             tqdm.write(f"current network: {os.path.basename(network)}")
             self.simulator = self._create_simulator(network)
             return self.simulator
-        if self.simulator is None and self.episode_count == 0:
-            network = files[0]
+        if self.simulator is None:
+            # first reset (or the first one after a resume at episode ``episode_count``)
+            network = files[(self.episode_count // sched["period"]) % len(files)]
             tqdm.write(f"current network: {os.path.basename(network)}")
             self.simulator = self._create_simulator(network)
-        if self.episode_count % sched["period"] == 0 and self.episode_count > 0:
+        elif self.episode_count % sched["period"] == 0 and self.episode_count > 0:
             network = files[(self.episode_count // sched["period"]) % len(files)]
             tqdm.write(f"current network: {os.path.basename(network)}")
             self.simulator = self._create_simulator(network)

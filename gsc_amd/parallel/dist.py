@@ -89,3 +89,12 @@ def allreduce_max_scalar(x: float, device) -> float:
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sync_string(s: str, src: int = 0) -> str:
+    """Rank ``src``'s value of a short string on every rank (run ids, seeds)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return s
+    obj = [s]
+    dist.broadcast_object_list(obj, src=src)
+    return obj[0]

@@ -118,6 +118,7 @@ class AgentHelper:
         self.schedule_path = schedule
         self.schedule = None
         self.seed = seed
+        self.datetime = DATETIME
         self.experiment_id = f"{DATETIME}_seed{seed}"
         self.result = ExperimentResult(self.experiment_id)
         self.weights = weights
@@ -204,7 +205,14 @@ def create_input_file(target_dir, num_ingress_nodes, algo):
         yaml.safe_dump({"num_ingress": num_ingress_nodes, "algorithm": algo}, f, default_flow_style=False)
 
 
-def setup_files(h: AgentHelper, results_root: str = "results") -> None:
+def write_yaml(path: str, data: dict) -> None:
+    os.makedirs(os.path.dirname(os.path.realpath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        yaml.safe_dump({k: (v.item() if hasattr(v, "item") else v) for k, v in data.items()}, f,
+                       default_flow_style=False)
+
+
+def setup_files(h: AgentHelper, results_root: str = "results", write_files: bool = True) -> None:
     base = get_base_path(h.agent_config_path, h.schedule_path, h.service_path, h.sim_config_path)
     h.result_base_path = os.path.join(results_root, base)
     h.graph_base_path = os.path.join("graph", base)
@@ -212,11 +220,14 @@ def setup_files(h: AgentHelper, results_root: str = "results") -> None:
     h.logfile = os.path.join(h.config_dir, "training.log")
     h.graph_path = os.path.join(h.graph_base_path, h.experiment_id)
     if h.test and not h.append_test:
-        h.config_dir = os.path.join(h.result_base_path, h.test, f"test-{DATETIME}_seed{h.seed}") + os.sep
+        h.config_dir = os.path.join(h.result_base_path, h.test, f"test-{h.datetime}_seed{h.seed}") + os.sep
         h.logfile = os.path.join(h.config_dir, "test.log")
         h.weights_path = os.path.join(h.result_base_path, h.test)
     h.result.log_file = h.logfile
     h.result_file = os.path.join(h.config_dir, "result.yaml")
+    if not write_files:  # non-zero ranks: same paths, no files
+        setup_logging(h.verbose, None)
+        return
     setup_logging(h.verbose, h.logfile)
     (h.agent_config_path, h.network_path, h.service_path, h.sim_config_path,
      h.schedule_path) = copy_input_files(h.config_dir, h.agent_config_path, h.network_path, h.service_path,
@@ -224,17 +235,19 @@ def setup_files(h: AgentHelper, results_root: str = "results") -> None:
 
 
 def setup(agent_config, network, service, sim_config, scheduler, seed, episodes, weights=None, verbose=False,
-          test=None, append_test=False, sim_seed=None, gen_scenario=None, results_root="results") -> AgentHelper:
-    """Reference ``setup`` (main.py:62-86)."""
-    h = AgentHelper(agent_config, network, service, sim_config, scheduler, seed, episodes, weights, verbose, DATETIME,
-                    test, append_test, sim_seed, gen_scenario)
+          test=None, append_test=False, sim_seed=None, gen_scenario=None, results_root="results",
+          datetime_str: Optional[str] = None, write_files: bool = True) -> AgentHelper:
+    """Reference ``setup`` (main.py:62-86).  ``datetime_str`` pins the run id (all DP ranks share one)."""
+    h = AgentHelper(agent_config, network, service, sim_config, scheduler, seed, episodes, weights, verbose,
+                    datetime_str or DATETIME, test, append_test, sim_seed, gen_scenario)
     h.schedule = load_schedule(scheduler)
-    setup_files(h, results_root)
+    setup_files(h, results_root, write_files)
     set_random_seed(seed)
     h.config = get_config(h.agent_config_path)
     h.episode_steps = h.config["episode_steps"]
     h.result.episodes = episodes
-    create_input_file(h.config_dir, num_ingress(network), h.config.get("agent_type"))
+    if write_files:
+        create_input_file(h.config_dir, num_ingress(network), h.config.get("agent_type"))
     return h
 
 

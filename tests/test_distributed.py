@@ -1,0 +1,126 @@
+"""Data-parallel correctness on CPU (gloo, 2 ranks).
+
+SURVEY §4: (a) replicas stay bit-identical across ranks after N updates, and (b) the all-reduced
+update equals the single-process update over the concatenated batch (fp32 tolerance).  The
+same code path runs over RCCL on GPUs (backend chosen by ``init_distributed``).
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import yaml
+
+from tests.conftest import ROOT, cfg_path
+
+ABILENE = cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml")
+B_PER_RANK = 6
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg():
+    cfg = yaml.safe_load(open(cfg_path("config", "agent", "sample_agent.yaml")))
+    cfg["actor_hidden_layer_nodes"] = [32]
+    cfg["critic_hidden_layer_nodes"] = [16]
+    return cfg
+
+
+def _learner(dist_info=None, seed=3):
+    from gsc_amd.agents import DDPGLearner
+    from gsc_amd.coordsim.reader import load_topology
+    from gsc_amd.models import GraphSet
+    gs = GraphSet([load_topology(ABILENE)], 24, "cpu")
+    return DDPGLearner(_cfg(), 3, 24 * 1 * 3 * 24, gs, 1, 3, "cpu", dist_info, amp_bf16=False, seed=seed), gs
+
+
+def _batches(n_updates):
+    from gsc_amd.agents import Batch
+    g = torch.Generator().manual_seed(11)
+    out = []
+    for _ in range(n_updates):
+        B = B_PER_RANK * WORLD
+        obs = torch.rand(B, 24, 3, generator=g)
+        obs[:, 11:] = 0
+        nxt = torch.rand(B, 24, 3, generator=g)
+        nxt[:, 11:] = 0
+        out.append(Batch(obs, torch.zeros(B, dtype=torch.int64), torch.rand(B, 1728, generator=g),
+                         torch.rand(B, generator=g) - 0.5, nxt, (torch.rand(B, generator=g) < 0.2).float()))
+    return out
+
+
+def _worker(rank, port, out_dir, n_updates):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from gsc_amd.agents import Batch
+    from gsc_amd.parallel.dist import init_distributed, shutdown
+    info = init_distributed("cpu")
+    # different init seeds per rank: the learner must broadcast rank 0's replicas
+    learner, _ = _learner(info, seed=3 if rank == 0 else 99)
+    for b in _batches(n_updates):
+        sl = slice(rank * B_PER_RANK, (rank + 1) * B_PER_RANK)
+        learner.update(Batch(*(t[sl] for t in b)))
+    torch.save({"actor": learner.actor_flat.flat.clone(), "critic": learner.critic_flat.flat.clone(),
+                "target_actor": learner.target_actor_flat.flat.clone()}, os.path.join(out_dir, f"r{rank}.pt"))
+    shutdown()
+
+
+def test_dp_allreduce_matches_single_process():
+    n_updates = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(_free_port(), d, n_updates), nprocs=WORLD, join=True, start_method="spawn")
+        r = [torch.load(os.path.join(d, f"r{i}.pt"), weights_only=True) for i in range(WORLD)]
+    for k in r[0]:
+        assert torch.equal(r[0][k], r[1][k]), f"{k} differs across ranks"
+    ref, _ = _learner(None, seed=3)
+    for b in _batches(n_updates):
+        ref.update(b)
+    torch.testing.assert_close(r[0]["critic"], ref.critic_flat.flat, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(r[0]["actor"], ref.actor_flat.flat, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(r[0]["target_actor"], ref.target_actor_flat.flat, rtol=1e-5, atol=1e-6)
+
+
+def _trainer_worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from gsc_amd.agents import BatchedTrainer, TrainerConfig
+    from gsc_amd.parallel.dist import init_distributed, shutdown
+    from gsc_amd.sim.batched import load_batched_from_paths
+    info = init_distributed("cpu")
+    cfg = _cfg()
+    os.chdir(ROOT)
+    sim = load_batched_from_paths([ABILENE], cfg_path("service_functions", "abc.yaml"),
+                                  cfg_path("config", "simulator", "sample_config.yaml"), cfg, 4, device="cpu",
+                                  seed=1000 + rank, host_threads=1)
+    tr = BatchedTrainer(cfg, sim, TrainerConfig(num_envs=4, batch_size=16, learning_starts=2, seed=5 + rank,
+                                                check_every=0), info)
+    for _ in range(5):
+        tr.step()
+    m = tr.metrics()
+    torch.save({"actor": tr.learner.actor_flat.flat.clone(), "critic": tr.learner.critic_flat.flat.clone(),
+                "succ": torch.tensor(m["succ"]), "updates": torch.tensor(tr.learner.updates)},
+               os.path.join(out_dir, f"t{rank}.pt"))
+    shutdown()
+
+
+def test_dp_batched_trainer_replicas_identical():
+    """Ranks step different envs (different seeds) yet hold identical parameters after every update;
+    metrics are all-reduced (both ranks report the same whole-job counts)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_trainer_worker, args=(_free_port(), d), nprocs=WORLD, join=True, start_method="spawn")
+        r = [torch.load(os.path.join(d, f"t{i}.pt"), weights_only=True) for i in range(WORLD)]
+    assert int(r[0]["updates"]) == 4
+    assert torch.equal(r[0]["actor"], r[1]["actor"])
+    assert torch.equal(r[0]["critic"], r[1]["critic"])
+    assert float(r[0]["succ"]) == float(r[1]["succ"]) > 0
