@@ -557,6 +557,8 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
     return;
   }
   a.waves = 4;
+  while (a.waves > 1 && sizeof(float) * (((a.n_params + 3) & ~3) + (size_t)a.waves * fwd_per_wave(a)) > 80 * 1024)
+    a.waves--;
   const size_t lds = sizeof(float) * (((a.n_params + 3) & ~3) + (size_t)a.waves * fwd_per_wave(a));
   GSC_CHECK(lds <= 160 * 1024, "GNN forward working set exceeds LDS");
   const int blocks_needed = (B + a.waves - 1) / a.waves;
@@ -605,12 +607,28 @@ void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo
   check_launch();
 }
 
+// Whether the fused kernels' per-graph working sets fit LDS (one wave per block) for these sizes;
+// larger graphs (e.g. 200-node topologies) run the PyTorch reference path instead.
+bool gnn_fused_fits(int M, int NM, int P, int Fin, int H, std::vector<int> layer_of) {
+  GnnArgs a{};
+  a.M = M; a.NM = NM; a.P = P; a.Fin = Fin; a.H = H; a.L = (int)layer_of.size(); a.waves = 1;
+  if (a.L < 1 || a.L > kGnnMaxLayers) return false;
+  int maxb = 0;
+  for (int i = 0; i < a.L; ++i) { a.layer_of[i] = layer_of[i]; maxb = layer_of[i] > maxb ? layer_of[i] : maxb; }
+  a.n_params = block_offset(maxb, Fin, H) + block_size(maxb == 0 ? Fin : H, H);
+  const size_t pbytes = sizeof(float) * ((a.n_params + 3) & ~3);
+  const size_t fwd = pbytes + sizeof(float) * fwd_per_wave(a);
+  const size_t bwd = pbytes + sizeof(float) * bwd_layout(a).per_wave;
+  return fwd <= 160 * 1024 && bwd <= 160 * 1024;
+}
+
 int gnn_num_params(int Fin, int H, int max_block) { return block_offset(max_block, Fin, H) + block_size(max_block == 0 ? Fin : H, H); }
 
 void register_gnn(py::module_& m) {
   m.def("gnn_forward", &gnn_forward);
   m.def("gnn_backward", &gnn_backward);
   m.def("gnn_num_params", &gnn_num_params);
+  m.def("gnn_fused_fits", &gnn_fused_fits);
   m.def("gnn_set_path", &gnn_set_path, "bit0: channel-lane forward, bit1: channel-lane backward");
   m.def("gnn_get_path", &gnn_path);
 }

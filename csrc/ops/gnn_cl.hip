@@ -522,7 +522,11 @@ __global__ __launch_bounds__(256) void gnn_cl_bwd_kernel(ClArgs a, ClBwdLayout b
 template <int HP>
 static void cl_launch_fwd(ClArgs a, hipStream_t st, int cus) {
   a.waves = 4;
-  const size_t lds = sizeof(float) * ((size_t)a.n_blocks * cl_pblock<HP>() + (size_t)a.waves * cl_fwd_per_wave<HP>(a));
+  auto bytes = [&]() {
+    return sizeof(float) * ((size_t)a.n_blocks * cl_pblock<HP>() + (size_t)a.waves * cl_fwd_per_wave<HP>(a));
+  };
+  while (a.waves > 1 && bytes() > 80 * 1024) a.waves--;
+  const size_t lds = bytes();
   GSC_CHECK(lds <= 160 * 1024, "GNN forward working set exceeds LDS");
   if (lds > 65536)
     GSC_HIP_CHECK(hipFuncSetAttribute((const void*)gnn_cl_fwd_kernel<HP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

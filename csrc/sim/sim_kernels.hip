@@ -242,7 +242,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   Header* const h_mem = S.h;
   Header h_reg = *h_mem;
   S.h = &h_reg;
-  const TopoDev T = stage_topo(a.topos[S.h->topo], topo_lds, lane);
+  const TopoDev T = a.topo_stage ? stage_topo(a.topos[S.h->topo], topo_lds, lane) : a.topos[S.h->topo];
   load_action(S, K, T, a.actions + (long)env * a.action_stride, lane, 64);
   __syncthreads();
   // pending events -> sorted register queue; S.events then serves as the handlers' inbox
@@ -432,8 +432,10 @@ class SimContext {
       int maxH = 1;
       for (auto& t : topos_) maxH = t.H > maxH ? t.H : maxH;
       topo_stage_ = topo_stage_bytes(D_, maxH);
+      // Large topologies (N^2 * hops path tables beyond the LDS budget, e.g. 200 nodes): the tables
+      // stay in HBM and are served from L2 — only SimConst (+ the state blob, if it fits) is staged.
+      if (const_stage_bytes() + topo_stage_ + 1024 > max_lds) topo_stage_ = 0;
       const long fixed = const_stage_bytes() + topo_stage_;
-      GSC_CHECK(fixed <= max_lds, "topology tables do not fit in LDS");
       use_lds_ = fixed + L_.total <= max_lds;
       const long need = fixed + (use_lds_ ? L_.total : 0);
       qsets_ = D_.event_cap <= 64 ? 1 : (D_.event_cap <= 128 ? 2 : (D_.event_cap <= 256 ? 4 : 8));

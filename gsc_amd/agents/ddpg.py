@@ -143,6 +143,7 @@ class TrainerConfig:
     learning_starts: Optional[int] = None   # iterations; default: nb_steps_warmup_critic
     replay_capacity: Optional[int] = None   # default: mem_limit * num_envs (capped)
     replay_cap_max: int = 2_000_000
+    replay_bytes_max: Optional[float] = None  # default: 25 % of HBM (4 GB on CPU)
     seed: int = 0
     check_every: int = 50
     overlap_sim: bool = True                # run the simulator kernel on its own stream, concurrent with updates
@@ -163,6 +164,11 @@ class BatchedTrainer:
         self.learner = DDPGLearner(cfg, sim.n_obs, sim.action_dim, self.graphs, sim.C, sim.F, self.device,
                                    self.dist, seed=tcfg.seed)
         cap = tcfg.replay_capacity or min(int(cfg.get("mem_limit", 10000)) * self.E, tcfg.replay_cap_max)
+        # byte budget: large action spaces (50/200-node topologies, A = N^2 C F) bound the ring size
+        per = 4 * (2 * sim.n_pad * sim.n_obs + sim.action_dim + 4)
+        budget = tcfg.replay_bytes_max or (0.25 * torch.cuda.get_device_properties(self.device).total_memory
+                                           if self.device.type == "cuda" else 4e9)
+        cap = int(min(cap, budget // per))
         self.replay = DeviceReplay(max(cap, self.E), sim.n_pad, sim.n_obs, sim.action_dim, self.device,
                                    seed=tcfg.seed + 7919 * self.dist.rank)
         self.batch_size = tcfg.batch_size or 100 * self.E

@@ -117,8 +117,10 @@ class GNNEmbedder(nn.Module):
         if use_native is None:
             use_native = x.is_cuda
         if use_native:
-            from gsc_amd.ops.gnn import gnn_embed
-            return gnn_embed(self, x, topo, graphs)
+            from gsc_amd.ops.gnn import gnn_embed, gnn_fits
+            if gnn_fits(self, graphs, x.shape[1], x.shape[2]):
+                return gnn_embed(self, x, topo, graphs)
+            # graphs whose per-graph working set exceeds LDS (e.g. 200 nodes): PyTorch path
         return self.forward_reference(x, topo, graphs)
 
     def forward_reference(self, x, topo, graphs: GraphSet):

@@ -90,6 +90,16 @@ class _GnnEmbed(torch.autograd.Function):
         return (None, None, None, None, *out)
 
 
+def gnn_fits(embedder, graphs, P: int, Fin: int) -> bool:
+    """Fused kernels handle these graph sizes (per-graph working set fits one CU's LDS)."""
+    key = ("_gnn_fits", embedder.hidden_dim, tuple(_layer_of(embedder)), P, Fin)
+    cache = graphs.__dict__.setdefault("_fits_cache", {})
+    if key not in cache:
+        cache[key] = bool(load_native().gnn_fused_fits(int(graphs.M), int(graphs.max_nodes), int(P), int(Fin),
+                                                       int(embedder.hidden_dim), _layer_of(embedder)))
+    return cache[key]
+
+
 def gnn_embed(embedder, x: torch.Tensor, topo: torch.Tensor, graphs) -> torch.Tensor:
     params = embedder.flat_parameters()
     return _GnnEmbed.apply(x, topo, graphs, (embedder.hidden_dim, _layer_of(embedder)), *params)

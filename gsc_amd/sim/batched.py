@@ -240,7 +240,10 @@ class BatchedSimulator:
                       actions.shape[1], self.obs.data_ptr(), self.next_obs.data_ptr(), self.reward.data_ptr(),
                       self.done.data_ptr(), self.stats.data_ptr(), self.ep_return.data_ptr(), self.E, self._stream(),
                       self.prof.data_ptr() if (self.prof is not None and self.is_device) else 0)
-        return SimStepOut(self.obs, self.next_obs, self.reward, self.done.bool(), self.stats, self.ep_return)
+        done = self.done.bool()
+        # envs that finished were reset onto their scheduled topology
+        torch.where(done, self.topo_next, self.topo_cur, out=self.topo_cur)
+        return SimStepOut(self.obs, self.next_obs, self.reward, done, self.stats, self.ep_return)
 
     def check_flags(self) -> int:
         flags = int(self.stats[:, 12].max().item())

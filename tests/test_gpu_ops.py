@@ -36,13 +36,28 @@ def test_gnn_fused_matches_reference(layers, iters, hidden, path):
         nat.gnn_set_path(old)
 
 
-def _check_gnn(layers, iters, hidden):
+@pytest.mark.parametrize("path", [0, 1, 3], ids=["generic", "cl-fwd", "cl-fwd-bwd"])
+def test_gnn_fused_50_nodes(path):
+    """50-node synthetic topology (n_pad 50, 250 messages) next to Abilene."""
+    from gsc_amd.native import load
+    nat = load()
+    old = nat.gnn_get_path()
+    nat.gnn_set_path(path)
+    try:
+        gs = GraphSet([load_topology(cfg_path("networks", "synthetic", "syn50-in8-cap1-3.graphml")),
+                       load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml"))], 50, DEV)
+        _check_gnn(2, 2, 22, gs, 50)
+    finally:
+        nat.gnn_set_path(old)
+
+
+def _check_gnn(layers, iters, hidden, gs=None, P=24):
     torch.manual_seed(0)
-    gs = _graphs(DEV)
+    gs = gs if gs is not None else _graphs(DEV)
     emb = GNNEmbedder(3, hidden, layers, "mean", iters).to(DEV)
     B = 777
-    topo = torch.randint(0, 3, (B,), device=DEV)
-    x = torch.rand(B, 24, 3, device=DEV) * gs.node_mask[topo].unsqueeze(-1)
+    topo = torch.randint(0, gs.num_topologies, (B,), device=DEV)
+    x = torch.rand(B, P, 3, device=DEV) * gs.node_mask[topo].unsqueeze(-1)
     params = list(emb.parameters())
     ref = emb.forward_reference(x, topo, gs)
     w = torch.linspace(-1, 1, hidden, device=DEV)

@@ -42,3 +42,31 @@ def test_device_matches_host(simcfg):
         assert torch.equal(oh.reward, od.reward.cpu())
         assert torch.equal(oh.done, od.done.cpu())
     dev.check_flags()
+
+
+SYN50 = cfg_path("networks", "synthetic", "syn50-in8-cap1-3.graphml")
+SYN200 = [cfg_path("networks", "synthetic", f"syn200-in16-cap1-3-s{i}.graphml") for i in range(4)]
+SVC3 = cfg_path("service_functions", "abc-3sfc.yaml")
+
+
+@pytest.mark.parametrize("case", ["syn50-trace", "syn200"])
+def test_device_matches_host_large(case):
+    """50-node (3 SFCs + trace; topology tables staged in LDS) and 200-node (tables in HBM) topologies."""
+    if case == "syn50-trace":
+        nets, simcfg, agent = [SYN50], cfg_path("config", "simulator", "rand-arrival12_trace_syn50.yaml"), "agent_syn50"
+    else:
+        nets, simcfg, agent = SYN200, cfg_path("config", "simulator", "sample_config.yaml"), "agent_syn200"
+    cfg = yaml.safe_load(open(cfg_path("config", "agent", agent + ".yaml")))
+    cfg["episode_steps"] = 6
+    E = 16
+    host = load_batched_from_paths(nets, SVC3, simcfg, cfg, E, device="cpu", seed=5, topo_init=np.arange(E) % len(nets))
+    dev = load_batched_from_paths(nets, SVC3, simcfg, cfg, E, device="cuda", seed=5, topo_init=np.arange(E) % len(nets))
+    assert torch.equal(host.reset().clone(), dev.reset().cpu())
+    rng = np.random.default_rng(2)
+    for k in range(8):
+        a = torch.from_numpy(rng.random((E, host.action_dim), dtype=np.float32))
+        oh, od = host.step(a), dev.step(a.cuda())
+        torch.cuda.synchronize()
+        assert torch.equal(oh.stats, od.stats.cpu()), f"step {k}"
+        assert torch.equal(oh.obs, od.obs.cpu()), f"step {k}"
+    dev.check_flags()
