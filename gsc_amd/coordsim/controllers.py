@@ -72,8 +72,16 @@ class DurationController(BaseController):
         self.episode = 0
         self.duration = params.run_duration
 
+    def _predict(self):
+        if getattr(self.params, "prediction", False):
+            if getattr(self, "predictor", None) is None:
+                from .predictor import TrafficPredictor
+                self.predictor = TrafficPredictor(self.params)
+            self.predictor.predict_traffic(self.env.now)
+
     def get_init_state(self):
         self.env.step()
+        self._predict()
         self.parse_network()
         self.network_metrics()
         return self._state()
@@ -90,6 +98,7 @@ class DurationController(BaseController):
             p.network.nodes[node_id]["available_sf"] = avail
         p.schedule = action.scheduling
         self.env.run(until=self.duration * p.run_times)
+        self._predict()
         self.parse_network()
         self.network_metrics()
         return self._state()

@@ -60,7 +60,9 @@ class Simulator(SimulatorInterface):
         self.config = reader.get_config(config_file)
         self.network, self.ing_nodes, self.eg_nodes = reader.network_builder(network_file, self.config)
         self.metrics = Metrics(self.network, self.sf_list)
-        self.prediction = False
+        # reference forces prediction off (simulator.py:47); ``future_traffic: true`` enables the
+        # list-based predictor (coordsim/predictor.py)
+        self.prediction = bool(self.config.get("future_traffic", False))
         self.params = SimulatorParams(logger, self.network, self.ing_nodes, self.eg_nodes, self.sfc_list,
                                       self.sf_list, self.config, self.metrics, prediction=self.prediction)
         self.writer = ResultWriter(test_mode, test_dir, bool(self.config.get("write_schedule", False)),
