@@ -40,6 +40,7 @@ from gsc_amd.parallel.dist import DistInfo
 from gsc_amd.utils import checkpoint as ckpt
 from gsc_amd.utils.experiment import MetricsLogger, ResultsWriter
 from gsc_amd.utils.tracing import SPSCounter, trace_range
+from .base import RLSPAgent
 from .ddpg import BatchedTrainer, DDPGLearner, TrainerConfig
 from .replay import GraphReplayBuffer
 
@@ -53,7 +54,7 @@ def default_device() -> torch.device:
     return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
 
-class SimpleDDPG:
+class SimpleDDPG(RLSPAgent):
     def __init__(self, agent_helper, backend: str = "auto", num_envs: Optional[int] = None, device=None,
                  dist_info: Optional[DistInfo] = None, checkpoint_every: int = 0, results_writers: bool = True,
                  trainer_overrides: Optional[dict] = None):
