@@ -44,6 +44,25 @@ struct GnnArgs {
   float* partials;         // [grid, n_params]
   int B, P, Fin, H, L, M, NM, n_params, waves;
   int layer_of[kGnnMaxLayers];
+  unsigned long long* prof;  // optional per-phase cycle counters (gnn_set_profile)
+};
+
+// Per-phase cycle accounting for the profiling instantiation (wave-uniform, s_memtime based).
+template <bool PROF>
+struct PhaseClock {
+  unsigned long long last = 0, acc[12] = {};
+  __device__ __forceinline__ void start() { if (PROF) last = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void mark(int k) {
+    if (PROF) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc[k] += t - last;
+      last = t;
+    }
+  }
+  __device__ __forceinline__ void flush(unsigned long long* out, int lane) {
+    if (PROF && out && lane == 0)
+      for (int k = 0; k < 12; ++k) atomicAdd(out + k, acc[k]);
+  }
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -271,7 +290,9 @@ __host__ __device__ inline BwdLayout bwd_layout(const GnnArgs& a) {
   return b;
 }
 
+template <bool PROF>
 __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
+  PhaseClock<PROF> clk;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < a.n_params; i += blockDim.x) lds[i] = a.params[i];
@@ -287,9 +308,11 @@ __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
   float* da = W + bl.da;
   Topo T;
   bind_topo(T, reinterpret_cast<int*>(W + bl.topo), a);
+  clk.start();
   for (int gi = blockIdx.x * a.waves + wave; gi < a.B; gi += gridDim.x * a.waves) {
     load_topo(T, a, a.topo[gi], lane);
     const int n = T.n, m = T.m;
+    clk.mark(0);
     // ---- forward recompute ----
     const float* xg = a.x + (long)gi * a.P * a.Fin;
     for (int i = lane; i < n * a.Fin; i += 64) W[bl.hin[0] + i] = xg[i];
@@ -303,6 +326,7 @@ __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
         wave_sync();
       }
     }
+    clk.mark(1);
     // ---- d emb -> dy of the last conv ----
     const float inv_n = 1.f / (float)n;
     for (int idx = lane; idx < n * H; idx += 64) {
@@ -330,6 +354,7 @@ __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
         for (int v = 0; v < n; ++v) s += dy[v * H + c];
         acc[o_bias + c] += s;
       }
+      clk.mark(2);
       // d alpha_q = (dy[i] / deg_i) . x_l[j]
       for (int q = lane; q < m; q += 64) {
         const int j = T.src[q], i = T.dst[q];
@@ -341,6 +366,7 @@ __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
         da[q] = s / T.deg[i];
       }
       wave_sync();
+      clk.mark(3);
       // softmax backward: de_q = alpha_q (da_q - sum_{q' -> i} alpha_q' da_q')
       for (int v = lane; v < n; v += 64) {
         float sad = 0.f;
@@ -351,6 +377,7 @@ __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
         }
       }
       wave_sync();
+      clk.mark(4);
       // d att_c = sum_q de_q * lrelu(z_qc)
       for (int c = lane; c < H; c += 64) {
         float s = 0.f;
@@ -361,6 +388,7 @@ __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
         }
         acc[o_att + c] += s;
       }
+      clk.mark(5);
       // dz_qc = de_q att_c lrelu'(z_qc);  dxl[j] = sum_{q: src=j} alpha_q dy[dst]/deg + dz;  dxr[i] = sum_{q: dst=i} dz
       for (int idx = lane; idx < n * H; idx += 64) {
         const int v = fdiv(idx, invH), c = idx - v * H;
@@ -383,6 +411,7 @@ __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
         dxr[idx] = sr;
       }
       wave_sync();
+      clk.mark(6);
       const float invFi = 1.f / (float)Fi;
       for (int idx = lane; idx < H * Fi; idx += 64) {
         const int c = fdiv(idx, invFi), k = idx - c * Fi;
@@ -395,12 +424,14 @@ __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
         acc[o_Wl + idx] += sl;
         acc[o_Wr + idx] += sr;
       }
+      clk.mark(7);
       for (int c = lane; c < H; c += 64) {
         float sl = 0.f, sr = 0.f;
         for (int v = 0; v < n; ++v) { sl += dxl[v * H + c]; sr += dxr[v * H + c]; }
         acc[o_bl + c] += sl;
         acc[o_br + c] += sr;
       }
+      clk.mark(8);
       if (l > 0) {
         wave_sync();
         for (int idx = lane; idx < n * Fi; idx += 64) {
@@ -417,8 +448,10 @@ __global__ __launch_bounds__(256) void gnn_bwd_kernel(GnnArgs a, BwdLayout bl) {
         }
       }
       wave_sync();
+      clk.mark(9);
     }
   }
+  clk.flush(a.prof, lane);
   __syncthreads();
   // reduce the waves' accumulators into this workgroup's partial row
   const float* acc0 = lds + ((a.n_params + 3) & ~3) + bl.acc;
@@ -484,13 +517,15 @@ static ClArgsMirror to_cl(const GnnArgs& a, py::dict t) {
   return c;
 }
 
-// Forward: the channel-lane kernel (118 us vs ~150 us per 25.6k-graph call on MI355X).
-// Backward: the generic kernel stays the default (948 us vs 1179 us for the channel-lane backward,
-// which needs ~290 VGPRs for its register-resident gradients -> 1 wave/SIMD); GSC_GNN_CL_BWD=1 opts in.
+// Channel-lane kernels are the default for both directions (25.6k Abilene graphs on MI355X:
+// forward 155 us vs 200 us generic, backward 640 us vs 945 us generic).  GSC_GNN_GENERIC=1 selects
+// the generic kernels, GSC_GNN_CL_FWD_ONLY=1 only the channel-lane forward.
+static unsigned long long* g_gnn_prof = nullptr;  // device buffer of 12 counters, or null
+void gnn_set_profile(uintptr_t p) { g_gnn_prof = reinterpret_cast<unsigned long long*>(p); }
 static int g_gnn_path = -1;  // bit0: channel-lane forward, bit1: channel-lane backward
 static int gnn_path() {
   if (g_gnn_path < 0)
-    g_gnn_path = getenv("GSC_GNN_GENERIC") ? 0 : (getenv("GSC_GNN_CL_BWD") ? 3 : 1);
+    g_gnn_path = getenv("GSC_GNN_GENERIC") ? 0 : (getenv("GSC_GNN_CL_FWD_ONLY") ? 1 : 3);
   return g_gnn_path;
 }
 void gnn_set_path(int bits) { g_gnn_path = bits & 3; }
@@ -598,8 +633,14 @@ void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo
   int grid = blocks_needed < num_cus() * per_cu ? blocks_needed : num_cus() * per_cu;
   if (grid > max_rows) grid = max_rows;
   if (grid < 1) grid = 1;
-  set_lds((const void*)gnn_bwd_kernel, lds);
-  hipLaunchKernelGGL(gnn_bwd_kernel, dim3(grid), dim3(64 * a.waves), lds, stream_of(stream), a, bl);
+  a.prof = g_gnn_prof;
+  if (a.prof) {
+    set_lds((const void*)gnn_bwd_kernel<true>, lds);
+    hipLaunchKernelGGL(gnn_bwd_kernel<true>, dim3(grid), dim3(64 * a.waves), lds, stream_of(stream), a, bl);
+  } else {
+    set_lds((const void*)gnn_bwd_kernel<false>, lds);
+    hipLaunchKernelGGL(gnn_bwd_kernel<false>, dim3(grid), dim3(64 * a.waves), lds, stream_of(stream), a, bl);
+  }
   check_launch();
   const int cols = a.n_params;
   hipLaunchKernelGGL(column_sum_kernel, dim3((cols + 31) / 32), dim3(256), 0, stream_of(stream),
@@ -629,6 +670,7 @@ void register_gnn(py::module_& m) {
   m.def("gnn_backward", &gnn_backward);
   m.def("gnn_num_params", &gnn_num_params);
   m.def("gnn_fused_fits", &gnn_fused_fits);
+  m.def("gnn_set_profile", &gnn_set_profile, "device int64[12] phase-cycle counters for the generic backward (0 = off)");
   m.def("gnn_set_path", &gnn_set_path, "bit0: channel-lane forward, bit1: channel-lane backward");
   m.def("gnn_get_path", &gnn_path);
 }

@@ -432,8 +432,9 @@ __device__ __forceinline__ void cl_grad_flush(const ClGrad<FIP>& G, float* row, 
   }
 }
 
-template <int HP, int NB>
-__global__ __launch_bounds__(256) void gnn_cl_bwd_kernel(ClArgs a, ClBwdLayout bl) {
+template <int HP, int NB, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void gnn_cl_bwd_kernel(ClArgs a,
+                                                                                                ClBwdLayout bl) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   cl_stage_params<HP>(a, lds);
@@ -549,15 +550,19 @@ static int cl_launch_bwd(ClArgs a, hipStream_t st, int cus, int max_rows) {
     a.waves--;
   }
   GSC_CHECK(lds <= 160 * 1024, "GNN backward working set exceeds LDS");
-  const void* fn = a.n_blocks == 1 ? (const void*)gnn_cl_bwd_kernel<HP, 1> : (const void*)gnn_cl_bwd_kernel<HP, 2>;
+  // Register budget: 2 waves/SIMD (<= 256 VGPRs; a few spills for NB=2) measured 640 us vs 1179 us at
+  // the unconstrained 287 VGPRs (1 wave/SIMD) for 25.6k Abilene graphs.  GSC_CL_WPE=1 restores the latter.
+  static const int wpe = getenv("GSC_CL_WPE") ? atoi(getenv("GSC_CL_WPE")) : 2;
+  const void* fn = a.n_blocks == 1 ? (wpe == 2 ? (const void*)gnn_cl_bwd_kernel<HP, 1, 2> : (const void*)gnn_cl_bwd_kernel<HP, 1, 1>)
+                                   : (wpe == 2 ? (const void*)gnn_cl_bwd_kernel<HP, 2, 2> : (const void*)gnn_cl_bwd_kernel<HP, 2, 1>);
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int per_cu = (int)((160 * 1024) / lds);
   const int need = (a.B + a.waves - 1) / a.waves;
   int grid = need < cus * (per_cu > 0 ? per_cu : 1) ? need : cus * (per_cu > 0 ? per_cu : 1);
   if (grid > max_rows) grid = max_rows;
   if (grid < 1) grid = 1;
-  if (a.n_blocks == 1) hipLaunchKernelGGL((gnn_cl_bwd_kernel<HP, 1>), dim3(grid), dim3(64 * a.waves), lds, st, a, bl);
-  else hipLaunchKernelGGL((gnn_cl_bwd_kernel<HP, 2>), dim3(grid), dim3(64 * a.waves), lds, st, a, bl);
+  hipLaunchKernelGGL(reinterpret_cast<void (*)(ClArgs, ClBwdLayout)>(const_cast<void*>(fn)), dim3(grid),
+                     dim3(64 * a.waves), lds, st, a, bl);
   check_launch();
   return grid;
 }

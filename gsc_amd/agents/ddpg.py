@@ -85,7 +85,8 @@ class DDPGLearner:
         g, masks = self.graphs, self.masks
         inv_world = 1.0 / self.dist.world_size
         with torch.no_grad(), self._autocast():
-            a2 = self.target_actor(b.next_obs, b.topo, g, masks).float().clamp(-1, 1)
+            # stays in the autocast dtype: the target critic consumes it as a bf16 GEMM operand
+            a2 = self.target_actor(b.next_obs, b.topo, g, masks).clamp(-1, 1)
             q2 = self.target_critic(b.next_obs, b.topo, g, masks, a2).float().view(-1)
             y = b.rewards + (1 - b.dones) * self.gamma * q2
         with self._autocast():
@@ -165,12 +166,14 @@ class BatchedTrainer:
                                    self.dist, seed=tcfg.seed)
         cap = tcfg.replay_capacity or min(int(cfg.get("mem_limit", 10000)) * self.E, tcfg.replay_cap_max)
         # byte budget: large action spaces (50/200-node topologies, A = N^2 C F) bound the ring size
-        per = 4 * (2 * sim.n_pad * sim.n_obs + sim.action_dim + 4)
+        adt = torch.bfloat16 if self.learner.amp else torch.float32
+        per = 4 * (2 * sim.n_pad * sim.n_obs + 4) + torch.empty((), dtype=adt).element_size() * sim.action_dim
         budget = tcfg.replay_bytes_max or (0.25 * torch.cuda.get_device_properties(self.device).total_memory
                                            if self.device.type == "cuda" else 4e9)
         cap = int(min(cap, budget // per))
+        # on the GPU actions are stored in bf16: the critic consumes them as bf16 GEMM operands
         self.replay = DeviceReplay(max(cap, self.E), sim.n_pad, sim.n_obs, sim.action_dim, self.device,
-                                   seed=tcfg.seed + 7919 * self.dist.rank)
+                                   action_dtype=adt, seed=tcfg.seed + 7919 * self.dist.rank)
         self.batch_size = tcfg.batch_size or 100 * self.E
         self.learning_starts = (tcfg.learning_starts if tcfg.learning_starts is not None
                                 else int(cfg.get("nb_steps_warmup_critic", 200)))

@@ -20,7 +20,7 @@ import torch
 class Batch(NamedTuple):
     obs: torch.Tensor        # [B, n_pad, F]
     topo: torch.Tensor       # [B] int64
-    actions: torch.Tensor    # [B, A] float32
+    actions: torch.Tensor    # [B, A] (bf16 on the GPU, float32 on CPU)
     rewards: torch.Tensor    # [B]
     next_obs: torch.Tensor   # [B, n_pad, F]
     dones: torch.Tensor      # [B]
@@ -73,7 +73,7 @@ class DeviceReplay:
                 raise RuntimeError("cannot sample from an empty replay buffer")
             idx = torch.randint(0, self.pos, (batch_size,), device=self.device, generator=self.gen)
         return Batch(self.obs.index_select(0, idx), self.topo.index_select(0, idx),
-                     self.actions.index_select(0, idx).float(), self.rewards.index_select(0, idx),
+                     self.actions.index_select(0, idx), self.rewards.index_select(0, idx),
                      self.next_obs.index_select(0, idx), self.dones.index_select(0, idx))
 
     def state_dict(self) -> dict:

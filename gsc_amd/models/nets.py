@@ -57,10 +57,21 @@ class MaskedInputMLP(nn.Module):
             h = h + F.linear(extra, W[:, D + A:])
         return h
 
-    def forward(self, dense, topo, masks, extra=None):
+    def forward(self, dense, topo, masks, extra=None, out_mask=None):
+        """``out_mask`` [out_dim]: multiply the output by a constant 0/1 vector, folded into the last
+        layer's weight rows and bias (same values as masking the ``[B, out]`` output, no extra pass)."""
         h = self.first_layer(dense, topo, masks, extra)
-        for layer in self.layers[1:]:
-            h = layer(F.relu(h))
+        last = len(self.layers) - 1
+        for i, layer in enumerate(self.layers):
+            if i == 0:
+                continue
+            h = F.relu(h)
+            if i == last and out_mask is not None:
+                h = F.linear(h, layer.weight * out_mask.unsqueeze(1), layer.bias * out_mask)
+            else:
+                h = layer(h)
+        if last == 0 and out_mask is not None:
+            h = h * out_mask
         return h
 
     def forward_full(self, x):
@@ -89,6 +100,8 @@ class Actor(nn.Module):
 
     def forward(self, x, topo, graphs: GraphSet, masks: torch.Tensor):
         emb = self.embedder(x, topo, graphs)
+        if masks.shape[0] == 1:  # one topology: fold the output mask into the last layer
+            return self.mlp(emb, topo, masks, out_mask=masks[0])
         out = self.mlp(emb, topo, masks)
         return out * select_rows(masks, topo)
 

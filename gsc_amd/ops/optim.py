@@ -39,13 +39,30 @@ class FlatParams:
         return self.grad[: self.numel]
 
     def set_grads(self, grads: Iterable[Optional[torch.Tensor]]) -> torch.Tensor:
-        """Write per-parameter gradients (``None`` = zero) into the flat gradient buffer."""
-        for p, o, g in zip(self.params, self.offsets, grads):
-            dst = self.grad[o:o + p.numel()]
+        """Write per-parameter gradients (``None`` = zero) into the flat gradient buffer.
+
+        Runs of gradients that are consecutive slices of one buffer laid out like the parameters
+        (e.g. the fused GNN backward's single gradient vector) are copied with one copy."""
+        grads = list(grads)
+        n = len(self.params)
+        i = 0
+        while i < n:
+            g, o = grads[i], self.offsets[i]
             if g is None:
-                dst.zero_()
-            else:
-                dst.copy_(g.reshape(-1))
+                self.grad[o:o + self.params[i].numel()].zero_()
+                i += 1
+                continue
+            j = i + 1
+            if g.is_contiguous():
+                es, sp = g.element_size(), g.untyped_storage().data_ptr()
+                while (j < n and grads[j] is not None and grads[j].is_contiguous() and grads[j].dtype == g.dtype
+                       and grads[j].untyped_storage().data_ptr() == sp
+                       and grads[j].data_ptr() == g.data_ptr() + (self.offsets[j] - o) * es):
+                    j += 1
+            length = self.offsets[j - 1] + self.params[j - 1].numel() - o
+            src = g.reshape(-1) if j == i + 1 else torch.as_strided(g, (length,), (1,), g.storage_offset())
+            self.grad[o:o + length].copy_(src)
+            i = j
         return self.grad
 
     def load_flat_(self, src: torch.Tensor) -> None:
