@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--device", default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true", help="run the simulator on the learner's stream")
+    ap.add_argument("--sim-cus", type=int, default=0,
+                    help="CUs reserved for the simulator stream (contiguous CU-mask bits); 0 = shared CUs")
     args = ap.parse_args()
 
     import torch
@@ -64,7 +66,7 @@ def main():
                                   seed=args.seed * 1000 + info.rank)
     tcfg = TrainerConfig(num_envs=args.envs, batch_size=args.batch_size, updates_per_step=args.updates_per_step,
                          learning_starts=1, seed=args.seed + 17 * info.rank, check_every=0,
-                         overlap_sim=not args.no_overlap)
+                         overlap_sim=not args.no_overlap, sim_cus=args.sim_cus)
     trainer = BatchedTrainer(cfg, sim, tcfg, info)
 
     def sync():
@@ -118,6 +120,7 @@ def main():
                 "learner_batch_per_gpu": trainer.batch_size,
                 "updates_per_step": args.updates_per_step,
                 "sim_learner_overlap": not args.no_overlap,
+                "sim_cus": args.sim_cus,
                 "topology": os.path.basename(args.network),
                 "device": torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu",
             },

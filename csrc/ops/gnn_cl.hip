@@ -533,7 +533,8 @@ static void cl_launch_fwd(ClArgs a, hipStream_t st, int cus) {
     GSC_HIP_CHECK(hipFuncSetAttribute((const void*)gnn_cl_fwd_kernel<HP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int per_cu = (int)((160 * 1024) / lds);
   const int need = (a.B + a.waves - 1) / a.waves;
-  int grid = need < cus * (per_cu > 0 ? per_cu : 1) ? need : cus * (per_cu > 0 ? per_cu : 1);
+  const int cap = cus * (per_cu > 0 ? per_cu : 1);
+  int grid = need < cap ? need : cap;
   hipLaunchKernelGGL(gnn_cl_fwd_kernel<HP>, dim3(grid > 0 ? grid : 1), dim3(64 * a.waves), lds, st, a);
   check_launch();
 }
@@ -558,7 +559,8 @@ static int cl_launch_bwd(ClArgs a, hipStream_t st, int cus, int max_rows) {
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int per_cu = (int)((160 * 1024) / lds);
   const int need = (a.B + a.waves - 1) / a.waves;
-  int grid = need < cus * (per_cu > 0 ? per_cu : 1) ? need : cus * (per_cu > 0 ? per_cu : 1);
+  const int cap = cus * (per_cu > 0 ? per_cu : 1);
+  int grid = need < cap ? need : cap;
   if (grid > max_rows) grid = max_rows;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(reinterpret_cast<void (*)(ClArgs, ClBwdLayout)>(const_cast<void*>(fn)), dim3(grid),

@@ -23,6 +23,7 @@ struct AdamArgs {
   float* target;  // may be null
   long n;
   float lr, b1, b2, eps, bc1, bc2_sqrt, tau, grad_scale, weight_decay;
+  const long long* step;  // optional device step counter (HIP-graph replay); overrides bc1/bc2_sqrt
 };
 
 __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamArgs& a) {
@@ -35,6 +36,11 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
 }
 
 __global__ __launch_bounds__(256) void adam_polyak_kernel(AdamArgs a) {
+  if (a.step) {  // bias corrections from the device-resident step (same formulas as the host path)
+    const double t = (double)*a.step;
+    a.bc1 = (float)(1.0 - pow((double)a.b1, t));
+    a.bc2_sqrt = (float)sqrt(1.0 - pow((double)a.b2, t));
+  }
   const long n4 = a.n >> 2;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -70,7 +76,8 @@ __global__ __launch_bounds__(256) void adam_polyak_kernel(AdamArgs a) {
 }
 
 void adam_polyak(uintptr_t p, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t target, long n, float lr, float b1,
-                 float b2, float eps, long step, float tau, float grad_scale, float weight_decay, uintptr_t stream) {
+                 float b2, float eps, long step, float tau, float grad_scale, float weight_decay, uintptr_t stream,
+                 uintptr_t step_ptr) {
   GSC_CHECK((p & 15) == 0 && (g & 15) == 0 && (m & 15) == 0 && (v & 15) == 0 && (target & 15) == 0,
             "adam_polyak buffers must be 16-byte aligned");
   AdamArgs a;
@@ -89,6 +96,7 @@ void adam_polyak(uintptr_t p, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t t
   a.tau = tau;
   a.grad_scale = grad_scale;
   a.weight_decay = weight_decay;
+  a.step = step_ptr ? ptr<const long long>(step_ptr) : nullptr;
   const long n4 = (n + 3) / 4;
   long grid = (n4 + 255) / 256;
   if (grid > 2048) grid = 2048;
@@ -111,7 +119,9 @@ void polyak(uintptr_t target, uintptr_t p, long n, float tau, uintptr_t stream) 
 }
 
 void register_optim(py::module_& m) {
-  m.def("adam_polyak", &adam_polyak);
+  m.def("adam_polyak", &adam_polyak, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("target"),
+        py::arg("n"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("step"), py::arg("tau"),
+        py::arg("grad_scale"), py::arg("weight_decay"), py::arg("stream"), py::arg("step_ptr") = 0);
   m.def("polyak", &polyak);
 }
 

@@ -67,10 +67,15 @@ class DDPGLearner:
         self.amp = (self.device.type == "cuda") if amp_bf16 is None else bool(amp_bf16)
         self.updates = 0
         self.last: Dict[str, torch.Tensor] = {}
+        self._graphs = None
+        self._graph_warm = 0
+        self._a = None
 
     def _autocast(self):
         if self.amp:
-            return torch.autocast(device_type=self.device.type, dtype=torch.bfloat16)
+            # no cast cache: weights are re-read after every optimizer step, and HIP-graph capture
+            # must not keep cached casts alive across replays
+            return torch.autocast(device_type=self.device.type, dtype=torch.bfloat16, cache_enabled=False)
         return torch.autocast(device_type=self.device.type, enabled=False)
 
     @torch.no_grad()
@@ -81,11 +86,12 @@ class DDPGLearner:
     def _allreduce(self, flat: FlatParams):
         return allreduce_sum_(flat.grad, async_op=True)
 
-    def update(self, b: Batch) -> None:
+    # -- update stages (eager or captured into HIP graphs) ---------------------------------------
+    def _stage_critic(self, b: Batch) -> None:
+        """TD target + critic loss -> critic gradients in ``critic_flat.grad``."""
         g, masks = self.graphs, self.masks
-        inv_world = 1.0 / self.dist.world_size
         with torch.no_grad(), self._autocast():
-            # stays in the autocast dtype: the target critic consumes it as a bf16 GEMM operand
+            # the clamped target action stays bf16: the target critic consumes it as a GEMM operand
             a2 = self.target_actor(b.next_obs, b.topo, g, masks).clamp(-1, 1)
             q2 = self.target_critic(b.next_obs, b.topo, g, masks, a2).float().view(-1)
             y = b.rewards + (1 - b.dones) * self.gamma * q2
@@ -94,27 +100,100 @@ class DDPGLearner:
             lq = F.mse_loss(q, y)
         grads = torch.autograd.grad(lq, self.critic_flat.params)
         self.critic_flat.set_grads(grads)
-        h_c = self._allreduce(self.critic_flat)
-        # actor forward overlaps the critic-gradient all-reduce (it does not read critic weights)
+        self._lq, self._qv = lq.detach(), q.detach().mean()
+
+    def _stage_actor_fwd(self, b: Batch) -> None:
         with self._autocast():
-            a = self.actor(b.obs, b.topo, g, masks)
-        if h_c is not None:
-            h_c.wait()
+            self._a = self.actor(b.obs, b.topo, self.graphs, self.masks)
+
+    def _stage_actor_grad(self, b: Batch, inv_world: float) -> None:
+        """Critic Adam/Polyak, then the actor loss through the frozen (updated) critic -> actor gradients."""
         self.critic_opt.step(grad_scale=inv_world)
         for p in self.critic_flat.params:
             p.requires_grad_(False)
         with self._autocast():
-            la = -self.critic(b.obs, b.topo, g, masks, a).float().mean()
+            la = -self.critic(b.obs, b.topo, self.graphs, self.masks, self._a).float().mean()
         grads = torch.autograd.grad(la, self.actor_flat.params)
         for p in self.critic_flat.params:
             p.requires_grad_(True)
         self.actor_flat.set_grads(grads)
+        self._la = la.detach()
+        self._a = None
+
+    def _stage_actor_opt(self, inv_world: float) -> None:
+        self.actor_opt.step(grad_scale=inv_world)
+
+    def update(self, b: Batch) -> None:
+        """One DDPG update, eager.  The critic-gradient all-reduce overlaps the actor forward."""
+        inv_world = 1.0 / self.dist.world_size
+        self._stage_critic(b)
+        h_c = self._allreduce(self.critic_flat)
+        self._stage_actor_fwd(b)     # does not read critic weights
+        if h_c is not None:
+            h_c.wait()
+        self._stage_actor_grad(b, inv_world)
         h_a = self._allreduce(self.actor_flat)
         if h_a is not None:
             h_a.wait()
-        self.actor_opt.step(grad_scale=inv_world)
+        self._stage_actor_opt(inv_world)
         self.updates += 1
-        self.last = {"qf1_loss": lq.detach(), "actor_loss": la.detach(), "qf1_values": q.detach().mean()}
+        self.last = {"qf1_loss": self._lq, "actor_loss": self._la, "qf1_values": self._qv}
+
+    # -- HIP-graph replay ----------------------------------------------------------------------
+    def update_graphed(self, b: Batch, warmup: int = 2) -> None:
+        """Same update, replayed from captured HIP graphs (``b`` must be the same static buffers on
+        every call).  One process: one graph for the whole update.  Data parallel: three graphs with
+        the two gradient all-reduces issued eagerly between them (collectives stay out of capture).
+        The first ``warmup`` calls run eagerly (they are real updates) on a side stream."""
+        inv_world = 1.0 / self.dist.world_size
+        if self._graphs is None:
+            if self._graph_warm < warmup:
+                s = torch.cuda.Stream(self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(s):
+                    self.update(b)
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                self._graph_warm += 1
+                return
+            self._capture(b, inv_world)
+        if len(self._graphs) == 1:
+            self._graphs[0].replay()
+        else:
+            g1, g2, g3 = self._graphs
+            g1.replay()
+            h = self._allreduce(self.critic_flat)
+            if h is not None:
+                h.wait()
+            g2.replay()
+            h = self._allreduce(self.actor_flat)
+            if h is not None:
+                h.wait()
+            g3.replay()
+        self.updates += 1
+        self.last = {"qf1_loss": self._lq, "actor_loss": self._la, "qf1_values": self._qv}
+
+    def _capture(self, b: Batch, inv_world: float) -> None:
+        pool = torch.cuda.graph_pool_handle()
+        graphs = []
+        if self.dist.world_size == 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                self._stage_critic(b)
+                self._stage_actor_fwd(b)
+                self._stage_actor_grad(b, inv_world)
+                self._stage_actor_opt(inv_world)
+            graphs.append(g)
+        else:
+            stages = [lambda: self._stage_critic(b),
+                      lambda: (self._stage_actor_fwd(b), self._stage_actor_grad(b, inv_world)),
+                      lambda: self._stage_actor_opt(inv_world)]
+            for fn in stages:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    fn()
+                graphs.append(g)
+        self._graphs = graphs
+        # capture recorded but did not execute the update: the caller's replay performs it
 
     # checkpointing --------------------------------------------------------------------------
     def state_dict(self) -> dict:
@@ -148,6 +227,9 @@ class TrainerConfig:
     seed: int = 0
     check_every: int = 50
     overlap_sim: bool = True                # run the simulator kernel on its own stream, concurrent with updates
+    sim_cus: int = 0                        # >0: simulator stream owns this many CUs (contiguous CU-mask bits,
+                                            # = sim_cus/8 per XCD), the learner the rest; 0: shared CUs
+    cuda_graphs: bool = True                # replay the DDPG update from captured HIP graphs (GPU only)
 
 
 class BatchedTrainer:
@@ -194,8 +276,22 @@ class BatchedTrainer:
         self.acc_return = torch.zeros((), dtype=torch.float64, device=self.device)
         self.acc_episodes = torch.zeros((), dtype=torch.float64, device=self.device)
         self.episode_returns: List[float] = []
-        self.sim_stream = (torch.cuda.Stream(self.device) if self.device.type == "cuda" and tcfg.overlap_sim
-                           else None)
+        self.graphed = bool(tcfg.cuda_graphs and self.device.type == "cuda")
+        self._batch = None
+        self.sim_stream = self.learn_stream = None
+        if self.device.type == "cuda" and tcfg.overlap_sim:
+            if tcfg.sim_cus > 0:
+                # disjoint CU sets: the latency-bound simulator waves and the LDS-bound learner kernels
+                # stop competing for the same CUs (scripts/cu_partition.py, profiles/)
+                nat = sim.native
+                n = nat.cu_count()
+                k = max(8, min(int(tcfg.sim_cus), n - 8))
+                self.sim_stream = torch.cuda.ExternalStream(nat.create_cu_masked_stream(list(range(k))),
+                                                            device=self.device)
+                self.learn_stream = torch.cuda.ExternalStream(nat.create_cu_masked_stream(list(range(k, n))),
+                                                              device=self.device)
+            else:
+                self.sim_stream = torch.cuda.Stream(self.device)
 
     def _schedule_next(self) -> None:
         """Network scheduler: topology used by the episode that starts after this step."""
@@ -206,6 +302,15 @@ class BatchedTrainer:
             self.sim.set_topologies(self.schedule[idx])
 
     def step(self) -> None:
+        if self.learn_stream is not None:
+            self.learn_stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.learn_stream):
+                self._step()
+            torch.cuda.current_stream(self.device).wait_stream(self.learn_stream)
+        else:
+            self._step()
+
+    def _step(self) -> None:
         warm = self.global_step < self.learning_starts
         with trace_range("act"):
             mu = self.learner.act(self.obs, self.topo)
@@ -223,8 +328,7 @@ class BatchedTrainer:
             with torch.cuda.stream(self.sim_stream):
                 out = self.sim.step(act)
             with trace_range("learn"):
-                for _ in range(self.t.updates_per_step):
-                    self.learner.update(self.replay.sample(self.batch_size))
+                self._learn()
             main.wait_stream(self.sim_stream)
             train = False
         else:
@@ -244,11 +348,20 @@ class BatchedTrainer:
             self.topo = self.sim.topo_next.to(torch.int64).clone()
         if train:
             with trace_range("learn"):
-                for _ in range(self.t.updates_per_step):
-                    self.learner.update(self.replay.sample(self.batch_size))
+                self._learn()
         self.global_step += 1
         if self.t.check_every and self.global_step % self.t.check_every == 0:
             self.sim.check_flags()
+
+    def _learn(self) -> None:
+        for _ in range(self.t.updates_per_step):
+            if self.graphed:
+                if self._batch is None:
+                    self._batch = self.replay.empty_batch(self.batch_size)
+                self.replay.sample(self.batch_size, out=self._batch)
+                self.learner.update_graphed(self._batch)
+            else:
+                self.learner.update(self.replay.sample(self.batch_size))
 
     def metrics(self, reset: bool = True) -> dict:
         vals = torch.stack([self.acc_succ, self.acc_drop, self.acc_return, self.acc_episodes])

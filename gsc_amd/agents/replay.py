@@ -64,7 +64,8 @@ class DeviceReplay:
         self.pos = new % self.capacity
 
     @torch.no_grad()
-    def sample(self, batch_size: int) -> Batch:
+    def sample(self, batch_size: int, out: Optional[Batch] = None) -> Batch:
+        """Uniform sample; with ``out`` the rows are gathered into those (static) buffers."""
         if self.full:
             idx = (torch.randint(1, self.capacity, (batch_size,), device=self.device, generator=self.gen)
                    + self.pos) % self.capacity
@@ -72,9 +73,19 @@ class DeviceReplay:
             if self.pos == 0:
                 raise RuntimeError("cannot sample from an empty replay buffer")
             idx = torch.randint(0, self.pos, (batch_size,), device=self.device, generator=self.gen)
-        return Batch(self.obs.index_select(0, idx), self.topo.index_select(0, idx),
-                     self.actions.index_select(0, idx), self.rewards.index_select(0, idx),
-                     self.next_obs.index_select(0, idx), self.dones.index_select(0, idx))
+        if out is None:
+            return Batch(self.obs.index_select(0, idx), self.topo.index_select(0, idx),
+                         self.actions.index_select(0, idx), self.rewards.index_select(0, idx),
+                         self.next_obs.index_select(0, idx), self.dones.index_select(0, idx))
+        for src, dst in zip((self.obs, self.topo, self.actions, self.rewards, self.next_obs, self.dones), out):
+            torch.index_select(src, 0, idx, out=dst)
+        return out
+
+    def empty_batch(self, batch_size: int) -> Batch:
+        """Static batch buffers (for :meth:`sample` ``out=`` and HIP-graph replay)."""
+        mk = lambda t: torch.empty((batch_size,) + tuple(t.shape[1:]), dtype=t.dtype, device=self.device)
+        return Batch(mk(self.obs), mk(self.topo), mk(self.actions), mk(self.rewards), mk(self.next_obs),
+                     mk(self.dones))
 
     def state_dict(self) -> dict:
         n = len(self)

@@ -79,7 +79,13 @@ class FusedAdamPolyak:
         self.target, self.tau = target, float(tau)
         self.m = torch.zeros_like(flat.flat)
         self.v = torch.zeros_like(flat.flat)
-        self.step_count = 0
+        # the step counter lives on the device so a captured HIP graph advances it on every replay
+        self.step_t = torch.zeros((), dtype=torch.int64, device=flat.flat.device)
+        self._host_step = 0
+
+    @property
+    def step_count(self) -> int:
+        return int(self.step_t.item()) if self.step_t.is_cuda else self._host_step
 
     def state_dict(self) -> dict:
         return {"m": self.m, "v": self.v, "step": self.step_count, "lr": self.lr, "betas": self.betas,
@@ -88,21 +94,25 @@ class FusedAdamPolyak:
     def load_state_dict(self, sd: dict) -> None:
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
-        self.step_count = int(sd["step"])
+        self._host_step = int(sd["step"])
+        self.step_t.fill_(int(sd["step"]))
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0) -> None:
-        self.step_count += 1
         p, g = self.fp.flat, self.fp.grad
         t = self.target.flat if self.target is not None else None
         if p.is_cuda:
             from gsc_amd.native import load
+            self.step_t.add_(1)
             load().adam_polyak(p.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                                t.data_ptr() if t is not None else 0, p.numel(), self.lr, self.betas[0],
-                               self.betas[1], self.eps, self.step_count, self.tau if t is not None else 0.0,
-                               float(grad_scale), self.wd, torch.cuda.current_stream(p.device).cuda_stream)
+                               self.betas[1], self.eps, 1, self.tau if t is not None else 0.0,
+                               float(grad_scale), self.wd, torch.cuda.current_stream(p.device).cuda_stream,
+                               step_ptr=self.step_t.data_ptr())
             return
-        adam_polyak_reference(p, g * grad_scale, self.m, self.v, t, self.step_count, self.lr, self.betas, self.eps,
+        self._host_step += 1
+        self.step_t.add_(1)
+        adam_polyak_reference(p, g * grad_scale, self.m, self.v, t, self._host_step, self.lr, self.betas, self.eps,
                               self.tau, self.wd)
 
 

@@ -87,8 +87,11 @@ def test_adam_polyak_matches_reference():
         opt = FusedAdamPolyak.__new__(FusedAdamPolyak)
         opt.fp, opt.lr, opt.betas, opt.eps, opt.wd, opt.tau = fp, 1e-3, (0.9, 0.999), 1e-8, 0.0, 1e-2
         opt.target = type("T", (), {"flat": tgt})()
-        opt.m, opt.v, opt.step_count = m, v, step - 1
+        opt.m, opt.v = m, v
+        opt.step_t = torch.full((), step - 1, dtype=torch.int64, device=DEV)  # device step counter
+        opt._host_step = step - 1
         opt.step()
+        assert opt.step_count == step
     torch.testing.assert_close(p, p2, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(tgt, t2, rtol=1e-6, atol=1e-6)
 
