@@ -42,8 +42,9 @@ def main():
     ap.add_argument("--device", default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true", help="run the simulator on the learner's stream")
-    ap.add_argument("--sim-cus", type=int, default=0,
-                    help="CUs reserved for the simulator stream (contiguous CU-mask bits); 0 = shared CUs")
+    ap.add_argument("--sim-cus", type=int, default=-1,
+                    help="CUs reserved for the simulator stream (contiguous CU-mask bits); 0 = shared CUs, "
+                         "-1 = auto (one round of env workgroups)")
     args = ap.parse_args()
 
     import torch
@@ -120,7 +121,7 @@ def main():
                 "learner_batch_per_gpu": trainer.batch_size,
                 "updates_per_step": args.updates_per_step,
                 "sim_learner_overlap": not args.no_overlap,
-                "sim_cus": args.sim_cus,
+                "sim_cus": getattr(trainer, "sim_cus", 0),
                 "topology": os.path.basename(args.network),
                 "device": torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu",
             },

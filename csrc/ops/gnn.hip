@@ -568,6 +568,10 @@ static GnnArgs make_args(py::dict t, uintptr_t params, uintptr_t x, uintptr_t to
   return a;
 }
 
+// CUs the launching stream may use: the device's count, or the budget of a CU-masked learner
+// stream (gnn_set_cu_budget) so persistent grids are sized to one full round on that partition.
+static int g_cu_budget = 0;
+void gnn_set_cu_budget(int n) { g_cu_budget = n > 0 ? n : 0; }
 static int num_cus() {
   static int cus = 0;
   if (!cus) {
@@ -575,7 +579,7 @@ static int num_cus() {
     GSC_HIP_CHECK(hipGetDevice(&dev));
     GSC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  return cus;
+  return g_cu_budget > 0 && g_cu_budget < cus ? g_cu_budget : cus;
 }
 
 static void set_lds(const void* fn, size_t lds) {
@@ -670,6 +674,7 @@ void register_gnn(py::module_& m) {
   m.def("gnn_backward", &gnn_backward);
   m.def("gnn_num_params", &gnn_num_params);
   m.def("gnn_fused_fits", &gnn_fused_fits);
+  m.def("gnn_set_cu_budget", &gnn_set_cu_budget, "CUs available to GNN launches (0 = whole device)");
   m.def("gnn_set_profile", &gnn_set_profile, "device int64[12] phase-cycle counters for the generic backward (0 = off)");
   m.def("gnn_set_path", &gnn_set_path, "bit0: channel-lane forward, bit1: channel-lane backward");
   m.def("gnn_get_path", &gnn_path);

@@ -454,6 +454,8 @@ class SimContext {
 
   long state_bytes() const { return L_.total; }
   bool use_lds() const { return use_lds_; }
+  // LDS bytes one env's workgroup needs on the device (SimConst + topology tables + state blob)
+  long lds_per_env() const { return const_stage_bytes() + topo_stage_ + (use_lds_ ? L_.total : 0); }
 
   void reset(uintptr_t states, uintptr_t topo_init, uintptr_t seeds, uintptr_t obs, int E, uintptr_t stream) {
     SimArgs a = args(states, topo_init, seeds, 0, 0, obs, 0, 0, 0, 0, 0, E);
@@ -604,6 +606,7 @@ void register_sim(py::module_& m) {
            py::arg("device"), py::arg("host_threads") = 8)
       .def_property_readonly("state_bytes", &SimContext::state_bytes)
       .def_property_readonly("use_lds", &SimContext::use_lds)
+      .def_property_readonly("lds_per_env", &SimContext::lds_per_env)
       .def("reset", &SimContext::reset)
       .def("step", &SimContext::step, py::arg("states"), py::arg("topo_next"), py::arg("seeds"), py::arg("actions"),
            py::arg("action_stride"), py::arg("obs"), py::arg("next_obs"), py::arg("reward"), py::arg("done"),
