@@ -70,6 +70,7 @@ class DDPGLearner:
         self._graphs = None
         self._graph_warm = 0
         self._a = None
+        self.compose_actor_critic = True
 
     def _autocast(self):
         if self.amp:
@@ -102,9 +103,16 @@ class DDPGLearner:
         self.critic_flat.set_grads(grads)
         self._lq, self._qv = lq.detach(), q.detach().mean()
 
+    def _composed(self) -> bool:
+        # one topology and at least one actor hidden layer: critic(obs, actor(obs)) re-associated
+        return self.compose_actor_critic and self.masks.shape[0] == 1 and len(self.actor.mlp.layers) > 1
+
     def _stage_actor_fwd(self, b: Batch) -> None:
         with self._autocast():
-            self._a = self.actor(b.obs, b.topo, self.graphs, self.masks)
+            if self._composed():
+                self._a = self.actor.hidden(b.obs, b.topo, self.graphs, self.masks)
+            else:
+                self._a = self.actor(b.obs, b.topo, self.graphs, self.masks)
 
     def _stage_actor_grad(self, b: Batch, inv_world: float) -> None:
         """Critic Adam/Polyak, then the actor loss through the frozen (updated) critic -> actor gradients."""
@@ -112,7 +120,11 @@ class DDPGLearner:
         for p in self.critic_flat.params:
             p.requires_grad_(False)
         with self._autocast():
-            la = -self.critic(b.obs, b.topo, self.graphs, self.masks, self._a).float().mean()
+            if self._composed():
+                q = self.critic.forward_on_actor(b.obs, b.topo, self.graphs, self.masks, self.actor, self._a)
+            else:
+                q = self.critic(b.obs, b.topo, self.graphs, self.masks, self._a)
+            la = -q.float().mean()
         grads = torch.autograd.grad(la, self.actor_flat.params)
         for p in self.critic_flat.params:
             p.requires_grad_(True)

@@ -74,6 +74,13 @@ class MaskedInputMLP(nn.Module):
             h = h * out_mask
         return h
 
+    def hidden(self, dense, topo, masks, extra=None):
+        """Input of the last layer (post-ReLU activation of the last hidden layer)."""
+        h = self.first_layer(dense, topo, masks, extra)
+        for layer in self.layers[1:-1]:
+            h = layer(F.relu(h))
+        return F.relu(h)
+
     def forward_full(self, x):
         """Unfolded reference: ``x`` is the explicit concatenation (used by tests)."""
         h = x
@@ -105,6 +112,10 @@ class Actor(nn.Module):
         out = self.mlp(emb, topo, masks)
         return out * select_rows(masks, topo)
 
+    def hidden(self, x, topo, graphs: GraphSet, masks: torch.Tensor):
+        """Last hidden activation ``z`` with ``forward(x) = (z W^T + b) * mask`` (W, b = last layer)."""
+        return self.mlp.hidden(self.embedder(x, topo, graphs), topo, masks)
+
     def scale_action(self, a):
         return 2.0 * ((a - self.low) / (self.high - self.low)) - 1.0
 
@@ -124,6 +135,33 @@ class QNetwork(nn.Module):
     def forward(self, x, topo, graphs: GraphSet, masks: torch.Tensor, action: torch.Tensor):
         emb = self.embedder(x, topo, graphs)
         return self.mlp(emb, topo, masks, action)
+
+
+    def forward_on_actor(self, x, topo, graphs: GraphSet, masks: torch.Tensor, actor: "Actor", z: torch.Tensor):
+        """``forward(x, ..., actor(x))`` for one topology without materialising the ``[B, A]`` action.
+
+        With one topology the actor output is ``a = z W2m^T + b2m`` (``W2m``, ``b2m``: last layer with
+        the constant mask folded in), so the critic's action projection re-associates:
+        ``a Wa^T = z (Wa W2m)^T + Wa b2m``.  Same function (up to rounding order); the ``[B, A]``
+        actor output and its two large GEMMs (plus their backward) are replaced by an ``[H1, A] x
+        [A, h]`` product and a ``[B, h] x [h, H1]`` GEMM.  Gradients reach the actor through
+        ``W2m``, ``b2m`` and ``z`` exactly as through ``a``."""
+        assert masks.shape[0] == 1, "composed critic/actor path needs a single topology"
+        mlp = self.mlp
+        D, A = mlp.dense_dim, mlp.mask_dim
+        W1 = mlp.first.weight
+        Wa = W1[:, D + A:]                                   # [h1, A]
+        last = actor.mlp.layers[-1]
+        m = masks[0]
+        W2m = last.weight * m.unsqueeze(1)                   # [A, z]
+        b2m = last.bias * m                                  # [A]
+        Mc = Wa @ W2m                                        # [h1, z]
+        cb = Wa @ b2m                                        # [h1]
+        emb = self.embedder(x, topo, graphs)
+        h = mlp.first_layer(emb, topo, masks) + F.linear(z, Mc, cb)
+        for layer in mlp.layers[1:]:
+            h = layer(F.relu(h))
+        return h
 
 
 def count_params(m: nn.Module) -> int:

@@ -109,3 +109,28 @@ def test_mask_folding_equals_concatenation():
     folded = a.mlp(emb, tid, masks.double())
     full = a.mlp.forward_full(torch.cat([emb, masks.double()[tid]], 1))
     torch.testing.assert_close(folded, full)
+
+
+def test_composed_actor_critic_equals_materialised():
+    """critic(x, actor(x)) via the re-associated action projection == the materialised path
+    (values and gradients w.r.t. actor and critic parameters), one topology."""
+    torch.manual_seed(0)
+    cfg = _cfg()
+    cfg["actor_hidden_layer_nodes"] = [32]
+    cfg["critic_hidden_layer_nodes"] = [16]
+    gs = GraphSet([load_topology(ABILENE)], 24, "cpu")
+    masks = gs.action_masks(1, 3)
+    actor, critic = Actor(cfg, 3, 1728), QNetwork(cfg, 3, 1728)
+    x = torch.rand(6, 24, 3) * gs.node_mask[torch.zeros(6, dtype=torch.long)].unsqueeze(-1)
+    topo = torch.zeros(6, dtype=torch.long)
+    params = list(actor.parameters()) + list(critic.parameters())
+    q1 = critic(x, topo, gs, masks, actor(x, topo, gs, masks))
+    g1 = torch.autograd.grad(q1.sum(), params, allow_unused=True)
+    q2 = critic.forward_on_actor(x, topo, gs, masks, actor, actor.hidden(x, topo, gs, masks))
+    g2 = torch.autograd.grad(q2.sum(), params, allow_unused=True)
+    torch.testing.assert_close(q1, q2, rtol=1e-5, atol=1e-5)
+    for a, b in zip(g1, g2):
+        if a is None:
+            assert b is None or torch.count_nonzero(b) == 0
+        else:
+            torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
