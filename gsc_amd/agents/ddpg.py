@@ -19,6 +19,7 @@ act (actor forward) -> exploration + post-processing kernel -> simulator kernel 
 from __future__ import annotations
 
 import copy
+import os
 import math
 import time
 from dataclasses import dataclass, field
@@ -70,7 +71,8 @@ class DDPGLearner:
         self._graphs = None
         self._graph_warm = 0
         self._a = None
-        self.compose_actor_critic = True
+        # GSC_COMPOSE=0 forces the materialised critic(obs, actor(obs)) path (A/B checks)
+        self.compose_actor_critic = os.environ.get("GSC_COMPOSE", "1") != "0"
 
     def _autocast(self):
         if self.amp:
@@ -105,7 +107,8 @@ class DDPGLearner:
 
     def _composed(self) -> bool:
         # one topology and at least one actor hidden layer: critic(obs, actor(obs)) re-associated
-        return self.compose_actor_critic and self.masks.shape[0] == 1 and len(self.actor.mlp.layers) > 1
+        return (self.compose_actor_critic and self.masks.shape[0] == 1 and len(self.actor.mlp.layers) > 1
+                and not self.actor.squash)
 
     def _stage_actor_fwd(self, b: Batch) -> None:
         with self._autocast():
@@ -406,10 +409,18 @@ class BatchedTrainer:
             out[k] = float(v)
         return out
 
-    def state_dict(self) -> dict:
-        return {"learner": self.learner.state_dict(), "global_step": self.global_step, "episode": self.episode,
-                "sim_states": self.sim.states.cpu(), "obs": self.obs.cpu(), "topo": self.topo.cpu(),
-                "replay": self.replay.state_dict(), "rng": self.replay.gen.get_state()}
+    def replay_bytes(self) -> int:
+        r = self.replay
+        return sum(t[:len(r)].numel() * t.element_size() for t in (r.obs, r.next_obs, r.topo, r.actions, r.rewards,
+                                                                  r.dones))
+
+    def state_dict(self, include_replay: bool = True) -> dict:
+        sd = {"learner": self.learner.state_dict(), "global_step": self.global_step, "episode": self.episode,
+              "sim_states": self.sim.states.cpu(), "obs": self.obs.cpu(), "topo": self.topo.cpu(),
+              "rng": self.replay.gen.get_state()}
+        if include_replay:
+            sd["replay"] = self.replay.state_dict()
+        return sd
 
     def load_state_dict(self, sd: dict) -> None:
         self.learner.load_state_dict(sd["learner"])
@@ -418,5 +429,9 @@ class BatchedTrainer:
         self.sim.states.copy_(sd["sim_states"].to(self.device))
         self.obs.copy_(sd["obs"].to(self.device))
         self.topo = sd["topo"].to(self.device)
-        self.replay.load_state_dict(sd["replay"])
+        if "replay" in sd:
+            self.replay.load_state_dict(sd["replay"])
+        else:  # checkpoint without the replay ring: resume refills it (learning restarts after warm-up)
+            self.replay.pos, self.replay.full = 0, False
+            self.learning_starts = self.global_step + 1
         self.replay.gen.set_state(sd["rng"])

@@ -69,6 +69,8 @@ class SimpleDDPG(RLSPAgent):
         self.backend = backend
         self.episode_steps = int(self.cfg["episode_steps"])
         self.checkpoint_every = int(checkpoint_every)
+        self.checkpoint_replay = "auto"          # auto | yes | no
+        self.checkpoint_replay_max = 1 << 30     # bytes (auto)
         sched = h.schedule
         self.train_files: List[str] = list(sched["training_network_files"])
         self.period = int(sched.get("period", 0) or 0)
@@ -273,7 +275,14 @@ class SimpleDDPG(RLSPAgent):
         base = {"backend": self.backend, "global_step": self.global_step, "episode": self.episode,
                 "best_return": float(self.best_return)}
         if self.backend == "batched":
-            base["trainer"] = self.trainer.state_dict()
+            # the replay ring is checkpointed when it is small enough (exact resume); a multi-GB ring
+            # (millions of transitions) is skipped unless checkpoint_replay="yes" — resume then refills it
+            pol = self.checkpoint_replay
+            rb = self.trainer.replay_bytes()
+            keep = pol == "yes" or (pol == "auto" and rb <= self.checkpoint_replay_max)
+            if not keep:
+                logger.info(f"checkpoint without the replay ring ({rb / 2**30:.1f} GiB)")
+            base["trainer"] = self.trainer.state_dict(include_replay=keep)
         else:
             n = len(self.rb)
             base["learner"] = self.learner.state_dict()

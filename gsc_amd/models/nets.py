@@ -104,9 +104,18 @@ class Actor(nn.Module):
         self.action_dim = action_dim
         self.mlp = MaskedInputMLP(H, action_dim, 0, list(cfg["actor_hidden_layer_nodes"]), action_dim)
         self.low, self.high = float(low), float(high)
+        # reference: no output squashing (Q6); new optional key ``actor_output_activation: sigmoid``
+        # bounds the policy to the [0, 1] action box (keeps the critic from being queried far outside
+        # the replayed actions, where its linear extrapolation drives the actor loss to -inf)
+        act = cfg.get("actor_output_activation", "none") or "none"
+        if act not in ("none", "sigmoid"):
+            raise ValueError(f"actor_output_activation must be none|sigmoid, got {act}")
+        self.squash = act == "sigmoid"
 
     def forward(self, x, topo, graphs: GraphSet, masks: torch.Tensor):
         emb = self.embedder(x, topo, graphs)
+        if self.squash:
+            return torch.sigmoid(self.mlp(emb, topo, masks)) * select_rows(masks, topo)
         if masks.shape[0] == 1:  # one topology: fold the output mask into the last layer
             return self.mlp(emb, topo, masks, out_mask=masks[0])
         out = self.mlp(emb, topo, masks)

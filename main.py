@@ -93,8 +93,11 @@ def select_best_agent(result_dir: str, last_n: int = 10):
 @click.option("--checkpoint-every", type=int, default=0, help="Write checkpoint.pt every N episodes (0: at the end).")
 @click.option("--results-root", default="results")
 @click.option("--no-test", is_flag=True, help="Skip the greedy test episode after training.")
+@click.option("--checkpoint-replay", type=click.Choice(["auto", "yes", "no"]), default="auto",
+              help="Include the replay ring in checkpoint.pt (auto: if <= 1 GiB).")
 def cli(agent_config, network, service, sim_config, scheduler, episodes, seed, test, weights, append_test, verbose,
-        best, sim_seed, gen_scenario, backend, envs, device, checkpoint_every, results_root, no_test):
+        best, sim_seed, gen_scenario, backend, envs, device, checkpoint_every, results_root, no_test,
+        checkpoint_replay):
     """GSC training and testing (GATv2 + DDPG on coord-sim), MI355X-native."""
     import torch
 
@@ -121,6 +124,7 @@ def cli(agent_config, network, service, sim_config, scheduler, episodes, seed, t
                  datetime_str=stamp, write_files=info.is_main)
     agent = SimpleDDPG(h, backend=backend, num_envs=envs, device=dev_type if dev_type == "cpu" else None,
                        dist_info=info, checkpoint_every=checkpoint_every)
+    agent.checkpoint_replay = checkpoint_replay
     log = xp.logger
     if test and not append_test:
         actor_file = os.path.join(h.weights_path, "trained_actor.pt")
