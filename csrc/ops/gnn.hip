@@ -497,6 +497,10 @@ struct ClArgsMirror {
   int layer_of[kGnnMaxLayers];
 };
 bool gnn_cl_supported(int Fin, int H, int L, int n_blocks);
+bool gnn_nl_supported(int Fin, int H, int NP, int L);
+void gnn_nl_forward(const float* params, int n_blocks, const float* x, const int32_t* topo, const int32_t* in_src,
+                    const int32_t* in_ptr, const float* deg, const int32_t* nnodes, float* emb, int B, int P, int Fin,
+                    int H, int L, int M, int NP, const int* layer_of, uintptr_t stream, int cus);
 void gnn_cl_forward(const void* args, uintptr_t stream, int cus);
 int gnn_cl_backward(const void* args, uintptr_t stream, int cus, int max_rows);
 
@@ -522,13 +526,13 @@ static ClArgsMirror to_cl(const GnnArgs& a, py::dict t) {
 // the generic kernels, GSC_GNN_CL_FWD_ONLY=1 only the channel-lane forward.
 static unsigned long long* g_gnn_prof = nullptr;  // device buffer of 12 counters, or null
 void gnn_set_profile(uintptr_t p) { g_gnn_prof = reinterpret_cast<unsigned long long*>(p); }
-static int g_gnn_path = -1;  // bit0: channel-lane forward, bit1: channel-lane backward
+static int g_gnn_path = -1;  // bit0: channel-lane forward, bit1: channel-lane backward, bit2: node-lane forward
 static int gnn_path() {
   if (g_gnn_path < 0)
     g_gnn_path = getenv("GSC_GNN_GENERIC") ? 0 : (getenv("GSC_GNN_CL_FWD_ONLY") ? 1 : 3);
   return g_gnn_path;
 }
-void gnn_set_path(int bits) { g_gnn_path = bits & 3; }
+void gnn_set_path(int bits) { g_gnn_path = bits & 7; }
 static bool use_cl(const GnnArgs& a, bool backward = false) {
   const bool off = !(gnn_path() & (backward ? 2 : 1));
   int maxb = 0;
@@ -590,6 +594,13 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
                  int H, std::vector<int> layer_of, uintptr_t stream) {
   GnnArgs a = make_args(tables, params, x, topo, B, P, Fin, H, layer_of);
   a.emb = ptr<float>(emb);
+  if ((gnn_path() & 4) && gnn_nl_supported(Fin, H, a.NM, a.L)) {
+    int maxb = 0;
+    for (int i = 0; i < a.L; ++i) maxb = a.layer_of[i] > maxb ? a.layer_of[i] : maxb;
+    gnn_nl_forward(a.params, maxb + 1, a.x, a.topo, ptr<const int32_t>(tables["in_src"].cast<uintptr_t>()), a.in_ptr,
+                   a.deg, a.nnodes, a.emb, B, P, Fin, H, a.L, a.M, a.NM, a.layer_of, stream, num_cus());
+    return;
+  }
   if (use_cl(a)) {
     const ClArgsMirror c = to_cl(a, tables);
     gnn_cl_forward(&c, stream, num_cus());

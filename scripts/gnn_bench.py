@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=25600)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--path", type=int, default=None, help="0 generic, 1 cl fwd, 3 cl fwd+bwd")
+    ap.add_argument("--path", type=int, default=None, help="bits: 1 cl fwd, 2 cl bwd, 4 node-lane fwd (0 = generic)")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--hidden", type=int, default=22)
     a = ap.parse_args()

@@ -21,7 +21,7 @@ def _graphs(dev):
     return GraphSet(topos, 24, dev)
 
 
-@pytest.mark.parametrize("path", [0, 1, 3], ids=["generic", "cl-fwd", "cl-fwd-bwd"])
+@pytest.mark.parametrize("path", [0, 1, 3, 7], ids=["generic", "cl-fwd", "cl-fwd-bwd", "nl-fwd"])
 @pytest.mark.parametrize("layers,iters,hidden", [(2, 2, 22), (1, 1, 22), (3, 1, 22), (2, 2, 32), (2, 2, 40)])
 def test_gnn_fused_matches_reference(layers, iters, hidden, path):
     """Channel-lane kernels (H <= 32, <= 2 parameter blocks) and the generic fused kernels, selected
@@ -36,7 +36,7 @@ def test_gnn_fused_matches_reference(layers, iters, hidden, path):
         nat.gnn_set_path(old)
 
 
-@pytest.mark.parametrize("path", [0, 1, 3], ids=["generic", "cl-fwd", "cl-fwd-bwd"])
+@pytest.mark.parametrize("path", [0, 1, 3, 7], ids=["generic", "cl-fwd", "cl-fwd-bwd", "nl-fwd"])
 def test_gnn_fused_50_nodes(path):
     """50-node synthetic topology (n_pad 50, 250 messages) next to Abilene."""
     from gsc_amd.native import load
