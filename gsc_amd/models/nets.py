@@ -18,6 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from gsc_amd.ops.linear import linear
 from .gnn import GNNEmbedder
 from .graphs import GraphSet
 
@@ -50,11 +51,11 @@ class MaskedInputMLP(nn.Module):
     def first_layer(self, dense, topo, masks, extra=None):
         W = self.first.weight
         D, A = self.dense_dim, self.mask_dim
-        h = F.linear(dense, W[:, :D], self.first.bias)
+        h = linear(dense, W[:, :D], self.first.bias)
         topo_bias = F.linear(masks, W[:, D:D + A])           # [T, h1]
         h = h + select_rows(topo_bias, topo)
         if extra is not None:
-            h = h + F.linear(extra, W[:, D + A:])
+            h = h + linear(extra, W[:, D + A:])
         return h
 
     def forward(self, dense, topo, masks, extra=None, out_mask=None):
@@ -67,9 +68,9 @@ class MaskedInputMLP(nn.Module):
                 continue
             h = F.relu(h)
             if i == last and out_mask is not None:
-                h = F.linear(h, layer.weight * out_mask.unsqueeze(1), layer.bias * out_mask)
+                h = linear(h, layer.weight * out_mask.unsqueeze(1), layer.bias * out_mask)
             else:
-                h = layer(h)
+                h = linear(h, layer.weight, layer.bias)
         if last == 0 and out_mask is not None:
             h = h * out_mask
         return h
@@ -78,7 +79,7 @@ class MaskedInputMLP(nn.Module):
         """Input of the last layer (post-ReLU activation of the last hidden layer)."""
         h = self.first_layer(dense, topo, masks, extra)
         for layer in self.layers[1:-1]:
-            h = layer(F.relu(h))
+            h = linear(F.relu(h), layer.weight, layer.bias)
         return F.relu(h)
 
     def forward_full(self, x):
@@ -167,9 +168,9 @@ class QNetwork(nn.Module):
         Mc = Wa @ W2m                                        # [h1, z]
         cb = Wa @ b2m                                        # [h1]
         emb = self.embedder(x, topo, graphs)
-        h = mlp.first_layer(emb, topo, masks) + F.linear(z, Mc, cb)
+        h = mlp.first_layer(emb, topo, masks) + linear(z, Mc, cb)
         for layer in mlp.layers[1:]:
-            h = layer(F.relu(h))
+            h = linear(F.relu(h), layer.weight, layer.bias)
         return h
 
 

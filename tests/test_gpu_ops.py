@@ -115,3 +115,21 @@ def test_explore_postprocess_device():
     out = explore_postprocess(mu, mask, P, False, 0.0, 0.0, seed=5, step=7)
     ref = normalize_slices_reference((0.5 * (2 * mu - 1 + 1)).clamp(0, 1).view(E, -1, P).cpu().double(), 0.1, 2)
     torch.testing.assert_close(out.cpu(), ref.float().view(E, A), rtol=1e-6, atol=1e-6)
+
+
+def test_splitk_linear_matches_linear():
+    """Split-K weight gradient == plain GEMM gradient (fp32 reference, bf16 autocast tolerance)."""
+    from gsc_amd.ops.linear import linear
+    torch.manual_seed(0)
+    x = torch.randn(25600, 1728, device=DEV, requires_grad=True)
+    w = torch.randn(64, 1728, device=DEV, requires_grad=True)
+    b = torch.randn(64, device=DEV, requires_grad=True)
+    g = torch.randn(25600, 64, device=DEV)
+    ref = torch.autograd.grad((torch.nn.functional.linear(x, w, b) * g).sum(), (x, w, b))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = linear(x, w, b)
+    assert out.dtype == torch.bfloat16
+    got = torch.autograd.grad((out.float() * g).sum(), (x, w, b))
+    for r, o in zip(ref, got):
+        assert o.dtype == r.dtype
+        assert (o - r).abs().max() <= 2e-2 * r.abs().max()
