@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--device", default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true", help="run the simulator on the learner's stream")
+    ap.add_argument("--check-replicas", action="store_true",
+                    help="after timing, verify that every rank holds bit-identical parameters")
     ap.add_argument("--sim-cus", type=int, default=-1,
                     help="CUs reserved for the simulator stream (contiguous CU-mask bits); 0 = shared CUs, "
                          "-1 = auto (one round of env workgroups)")
@@ -57,8 +59,9 @@ def main():
     device_type = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
     info = init_distributed(device_type)
     if device_type == "cuda":
-        torch.cuda.set_device(info.local_rank)
-        device = torch.device("cuda", info.local_rank)
+        dev_index = info.local_rank % torch.cuda.device_count()
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
     os.chdir(ROOT)
@@ -89,6 +92,18 @@ def main():
     sim.check_flags()
     m = trainer.metrics(reset=True)
 
+    if args.check_replicas and info.enabled:
+        import torch.distributed as dist
+        L = trainer.learner
+        sig = torch.stack([t.double().sum() for t in (L.actor_flat.flat, L.critic_flat.flat, L.target_actor_flat.flat,
+                                                      L.target_critic_flat.flat)])
+        sigs = [torch.zeros_like(sig) for _ in range(info.world_size)]
+        dist.all_gather(sigs, sig)
+        same = all(torch.equal(sigs[0], x) for x in sigs)
+        if info.is_main:
+            print(json.dumps({"replicas_identical": bool(same), "updates": L.updates,
+                              "graphed": bool(L._graphs is not None)}), flush=True)
+        assert same, "parameter replicas diverged across ranks"
     dt_t = torch.tensor([dt], dtype=torch.float64, device=device)
     if info.enabled:
         import torch.distributed as dist

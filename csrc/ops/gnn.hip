@@ -495,6 +495,7 @@ struct ClArgsMirror {
   float* partials;
   int B, P, Fin, H, L, M, NM, n_params, n_blocks, waves;
   int layer_of[kGnnMaxLayers];
+  unsigned long long* prof;
 };
 bool gnn_cl_supported(int Fin, int H, int L, int n_blocks);
 bool gnn_nl_supported(int Fin, int H, int NP, int L);
@@ -504,6 +505,8 @@ void gnn_nl_forward(const float* params, int n_blocks, const float* x, const int
 void gnn_cl_forward(const void* args, uintptr_t stream, int cus);
 int gnn_cl_backward(const void* args, uintptr_t stream, int cus, int max_rows);
 
+static unsigned long long* g_gnn_prof = nullptr;  // device buffer of 12 counters, or null
+void gnn_set_profile(uintptr_t p) { g_gnn_prof = reinterpret_cast<unsigned long long*>(p); }
 static ClArgsMirror to_cl(const GnnArgs& a, py::dict t) {
   ClArgsMirror c{};
   c.params = a.params; c.x = a.x; c.topo = a.topo;
@@ -518,14 +521,13 @@ static ClArgsMirror to_cl(const GnnArgs& a, py::dict t) {
   for (int i = 0; i < a.L; ++i) { c.layer_of[i] = a.layer_of[i]; maxb = a.layer_of[i] > maxb ? a.layer_of[i] : maxb; }
   c.n_blocks = maxb + 1;
   c.waves = 4;
+  c.prof = g_gnn_prof;
   return c;
 }
 
 // Channel-lane kernels are the default for both directions (25.6k Abilene graphs on MI355X:
 // forward 155 us vs 200 us generic, backward 640 us vs 945 us generic).  GSC_GNN_GENERIC=1 selects
 // the generic kernels, GSC_GNN_CL_FWD_ONLY=1 only the channel-lane forward.
-static unsigned long long* g_gnn_prof = nullptr;  // device buffer of 12 counters, or null
-void gnn_set_profile(uintptr_t p) { g_gnn_prof = reinterpret_cast<unsigned long long*>(p); }
 static int g_gnn_path = -1;  // bit0: channel-lane forward, bit1: channel-lane backward, bit2: node-lane forward
 static int gnn_path() {
   if (g_gnn_path < 0)

@@ -21,6 +21,24 @@ namespace gsc {
 constexpr int kClMaxLayers = 16;
 constexpr float kClSlope = 0.2f;
 
+// Optional per-phase cycle counters of the backward (s_memtime; gnn_cl_set_profile).
+struct ClClock {
+  unsigned long long last, acc[12];
+  bool on;
+  __device__ __forceinline__ void start(bool enable) {
+    on = enable;
+    for (int k = 0; k < 12; ++k) acc[k] = 0;
+    if (on) last = __builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void mark(int k) {
+    if (on) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      acc[k] += t - last;
+      last = t;
+    }
+  }
+};
+
 struct ClArgs {
   const float* params;     // unpadded module layout (Wl, bl, Wr, br, att, bias per block)
   const float* x;          // [B, P, Fin]
@@ -39,6 +57,7 @@ struct ClArgs {
   float* partials;         // [grid, n_params] (unpadded layout)
   int B, P, Fin, H, L, M, NM, n_params, n_blocks, waves;
   int layer_of[kClMaxLayers];
+  unsigned long long* prof;  // 12 phase counters or null
 };
 
 __device__ __forceinline__ void cl_wave_sync() {
@@ -312,7 +331,8 @@ __device__ __forceinline__ void cl_grad_zero(ClGrad<FIP>& g) {
 template <int HP, int FIP>
 __device__ __forceinline__ void cl_conv_bwd(const float* Pb, ClGrad<FIP>& G, const ClTopo& T, const float* hin,
                                             const float* xl, const float* xr, const float* al, const float* dy,
-                                            float* dxl, float* dxr, float* da, float* dh, bool need_dh, int lane) {
+                                            float* dxl, float* dxr, float* da, float* dh, bool need_dh, int lane,
+                                            ClClock& ck) {
   const int half = lane >> 5, c = lane & 31;
   const int cc = c < HP ? c : 0;
   const float* WlP = Pb;
@@ -335,6 +355,7 @@ __device__ __forceinline__ void cl_conv_bwd(const float* Pb, ClGrad<FIP>& G, con
     da[q] = s / T.deg[i];
   }
   cl_wave_sync();
+  ck.mark(3);
   // softmax backward: de_q = alpha_q (da_q - sum_{q' -> i} alpha_q' da_q')   (contiguous per node)
   for (int v = lane; v < n; v += 64) {
     const int q0 = T.iptr[v], q1 = T.iptr[v + 1];
@@ -343,12 +364,14 @@ __device__ __forceinline__ void cl_conv_bwd(const float* Pb, ClGrad<FIP>& G, con
     for (int q = q0; q < q1; ++q) da[q] = al[q] * (da[q] - sad);
   }
   cl_wave_sync();
+  ck.mark(4);
   // d att_c = sum_q de_q lrelu(z_qc)   (lane = channel, halves split the messages)
   for (int q = half; q < m; q += 2) {
     float z = xl[T.isrc[q] * HP + cc] + xr[T.idst[q] * HP + cc];
     z = z > 0.f ? z : kClSlope * z;
     G.att = fmaf(da[q], z, G.att);
   }
+  ck.mark(5);
   // dxl[v] = sum_{q: src=v} alpha_q dy[dst]/deg[dst] + dz_q ;  dxr[v] = sum_{q: dst=v} dz_q
   const float attc = vec[64 + c];
   for (int v = half; v < n; v += 2) {
@@ -371,6 +394,7 @@ __device__ __forceinline__ void cl_conv_bwd(const float* Pb, ClGrad<FIP>& G, con
     }
   }
   cl_wave_sync();
+  ck.mark(6);
   // weight gradients straight into the VGPR accumulators
   for (int v = half; v < n; v += 2) {
     const float el = dxl[v * HP + cc], er = dxr[v * HP + cc];
@@ -386,6 +410,7 @@ __device__ __forceinline__ void cl_conv_bwd(const float* Pb, ClGrad<FIP>& G, con
       G.wr[4 * k4 + 2] = fmaf(er, h4.z, G.wr[4 * k4 + 2]); G.wr[4 * k4 + 3] = fmaf(er, h4.w, G.wr[4 * k4 + 3]);
     }
   }
+  ck.mark(7);
   if (need_dh) {
     // dh[v,k] = sum_c dxl[v,c] Wl[c,k] + dxr[v,c] Wr[c,k]: lane k holds weight columns in VGPRs,
     // dxl/dxr rows arrive as 16-byte broadcasts
@@ -410,6 +435,7 @@ __device__ __forceinline__ void cl_conv_bwd(const float* Pb, ClGrad<FIP>& G, con
     }
   }
   cl_wave_sync();
+  ck.mark(8);
 }
 
 template <int FIP>
@@ -450,6 +476,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   ClTopo T;
   cl_bind_topo(T, reinterpret_cast<int*>(W + bl.topo), a);
   float* dy = W + bl.dy;
+  ClClock ck;
+  ck.start(a.prof != nullptr);
   for (int g = blockIdx.x * a.waves + wave; g < a.B; g += gridDim.x * a.waves) {
     cl_load_topo(T, a, a.topo[g], lane);
     const int n = T.n;
@@ -468,6 +496,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (l == 0) cl_conv<HP, FIN_P>(Pb, T, W + bl.hin[0], W + bl.xl[0], W + bl.xr[0], W + bl.al[0], y, relu, lane);
       else cl_conv<HP, HP>(Pb, T, W + bl.hin[l], W + bl.xl[l], W + bl.xr[l], W + bl.al[l], y, relu, lane);
     }
+    ck.mark(1);
     // d emb -> dy of the last conv (mean pool), ReLU mask when the embedder has a single conv
     const float ge = c < a.H ? a.demb[(long)g * a.H + c] / (float)n : 0.f;
     for (int v = half; v < n; v += 2) {
@@ -480,17 +509,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const float* Pb = lds + a.layer_of[l] * cl_pblock<HP>();
       if (l == 0) {
         cl_conv_bwd<HP, FIN_P>(Pb, GE, T, W + bl.hin[0], W + bl.xl[0], W + bl.xr[0], W + bl.al[0], dy, W + bl.dxl,
-                               W + bl.dxr, W + bl.da, dy, false, lane);
+                               W + bl.dxr, W + bl.da, dy, false, lane, ck);
       } else {
         cl_conv_bwd<HP, HP>(Pb, GP, T, W + bl.hin[l], W + bl.xl[l], W + bl.xr[l], W + bl.al[l], dy, W + bl.dxl,
-                            W + bl.dxr, W + bl.da, dy, true, lane);
+                            W + bl.dxr, W + bl.da, dy, true, lane, ck);
         const float* post = W + bl.hin[l];  // post-ReLU output of conv l-1
         for (int v = half; v < n; v += 2)
           if (c < HP && !(post[v * HP + c] > 0.f)) dy[v * HP + c] = 0.f;
         cl_wave_sync();
+        ck.mark(9);
       }
     }
   }
+  if (ck.on && lane == 0)
+    for (int k = 0; k < 12; ++k) atomicAdd(a.prof + k, ck.acc[k]);
   // per-wave accumulators -> LDS (reusing each wave's scratch) -> block sum -> partial row
   __syncthreads();
   float* accw = W;  // n_blocks * pblock floats fit inside the per-wave scratch (checked on the host)

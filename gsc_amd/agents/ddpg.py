@@ -188,11 +188,12 @@ class DDPGLearner:
         self.last = {"qf1_loss": self._lq, "actor_loss": self._la, "qf1_values": self._qv}
 
     def _capture(self, b: Batch, inv_world: float) -> None:
+        # thread-local capture: the RCCL watchdog thread keeps querying its events while we capture
         pool = torch.cuda.graph_pool_handle()
         graphs = []
         if self.dist.world_size == 1:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 self._stage_critic(b)
                 self._stage_actor_fwd(b)
                 self._stage_actor_grad(b, inv_world)
@@ -204,7 +205,7 @@ class DDPGLearner:
                       lambda: self._stage_actor_opt(inv_world)]
             for fn in stages:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
+                with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                     fn()
                 graphs.append(g)
         self._graphs = graphs

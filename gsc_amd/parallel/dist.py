@@ -44,14 +44,17 @@ def init_distributed(device_type: str = "cuda", timeout_s: int = 600) -> DistInf
         return DistInfo(0, 1, local, "none")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
-    backend = "nccl" if device_type == "cuda" else "gloo"
+    # GSC_DIST_BACKEND=gloo rehearses the multi-rank GPU path with several ranks on one GPU
+    # (RCCL refuses two ranks per device); the default on GPUs is RCCL ("nccl")
+    backend = os.environ.get("GSC_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if device_type == "cuda":
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
         # RCCL async error handling: a hung peer surfaces as an exception instead of a silent hang
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if not dist.is_initialized():
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
-        if device_type == "cuda":
+        if device_type == "cuda" and backend == "nccl":
             kw["device_id"] = torch.device("cuda", local)
         try:
             dist.init_process_group(**kw)

@@ -13,8 +13,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PHASES = ["topo", "fwd-recompute", "bias", "d-alpha", "softmax-bwd", "d-att", "dxl/dxr", "dW", "d-bl/br", "dh",
-          "-", "-"]
+PHASES = ["topo", "fwd-recompute", "bias", "d-alpha", "softmax-bwd", "d-att", "dxl/dxr", "dW", "d-bl/br|dh(cl)",
+          "dh|relu-mask(cl)", "-", "-"]
 
 
 def main():
@@ -71,7 +71,7 @@ def main():
         nat.gnn_set_profile(0)
         p = prof.cpu().tolist()
         tot = sum(p)
-        print("generic backward phase cycles per graph (s_memtime ticks, summed over waves):")
+        print("backward phase cycles per graph (s_memtime ticks, summed over waves; cl: bias+d-alpha in 'd-alpha'):")
         for k, v in enumerate(p):
             if v:
                 print(f"  {PHASES[k]:>14}: {v / B:10.1f}  ({100 * v / tot:5.1f} %)")
