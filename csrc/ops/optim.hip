@@ -24,6 +24,7 @@ struct AdamArgs {
   long n;
   float lr, b1, b2, eps, bc1, bc2_sqrt, tau, grad_scale, weight_decay;
   const long long* step;  // optional device step counter (HIP-graph replay); overrides bc1/bc2_sqrt
+  const int* skip;        // optional device flag: non-zero -> leave p, m, v, target untouched (bad grads)
 };
 
 __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamArgs& a) {
@@ -36,6 +37,7 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
 }
 
 __global__ __launch_bounds__(256) void adam_polyak_kernel(AdamArgs a) {
+  if (a.skip && *a.skip) return;
   if (a.step) {  // bias corrections from the device-resident step (same formulas as the host path)
     const double t = (double)*a.step;
     a.bc1 = (float)(1.0 - pow((double)a.b1, t));
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(256) void adam_polyak_kernel(AdamArgs a) {
 
 void adam_polyak(uintptr_t p, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t target, long n, float lr, float b1,
                  float b2, float eps, long step, float tau, float grad_scale, float weight_decay, uintptr_t stream,
-                 uintptr_t step_ptr) {
+                 uintptr_t step_ptr, uintptr_t skip_ptr) {
   GSC_CHECK((p & 15) == 0 && (g & 15) == 0 && (m & 15) == 0 && (v & 15) == 0 && (target & 15) == 0,
             "adam_polyak buffers must be 16-byte aligned");
   AdamArgs a;
@@ -97,6 +99,7 @@ void adam_polyak(uintptr_t p, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t t
   a.grad_scale = grad_scale;
   a.weight_decay = weight_decay;
   a.step = step_ptr ? ptr<const long long>(step_ptr) : nullptr;
+  a.skip = skip_ptr ? ptr<const int>(skip_ptr) : nullptr;
   const long n4 = (n + 3) / 4;
   long grid = (n4 + 255) / 256;
   if (grid > 2048) grid = 2048;
@@ -118,10 +121,33 @@ void polyak(uintptr_t target, uintptr_t p, long n, float tau, uintptr_t stream) 
   check_launch();
 }
 
+// flag[0] = any non-finite value in g[0..n); flag[1] += flag[0] (skipped-update counter).
+// One block per 64K elements, atomicOr into the flag; a second tiny launch bumps the counter.
+__global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ g, long n, int* flag) {
+  int bad = 0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    bad |= !isfinite(g[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+__global__ void nonfinite_count_kernel(int* flag) { flag[1] += flag[0] ? 1 : 0; }
+
+void grad_guard(uintptr_t g, long n, uintptr_t flag, uintptr_t stream) {
+  hipStream_t st = stream_of(stream);
+  GSC_HIP_CHECK(hipMemsetAsync(ptr<int>(flag), 0, sizeof(int), st));
+  long grid = (n + 255) / 256;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)(grid > 0 ? grid : 1)), dim3(256), 0, st, ptr<const float>(g), n,
+                     ptr<int>(flag));
+  hipLaunchKernelGGL(nonfinite_count_kernel, dim3(1), dim3(1), 0, st, ptr<int>(flag));
+  check_launch();
+}
+
 void register_optim(py::module_& m) {
+  m.def("grad_guard", &grad_guard, "flag[0] = any non-finite gradient; flag[1] counts flagged steps");
   m.def("adam_polyak", &adam_polyak, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("target"),
         py::arg("n"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("step"), py::arg("tau"),
-        py::arg("grad_scale"), py::arg("weight_decay"), py::arg("stream"), py::arg("step_ptr") = 0);
+        py::arg("grad_scale"), py::arg("weight_decay"), py::arg("stream"), py::arg("step_ptr") = 0,
+        py::arg("skip_ptr") = 0);
   m.def("polyak", &polyak);
 }
 

@@ -18,6 +18,15 @@ def load(auto_build: bool = None):
         return _mod
     if auto_build is None:
         auto_build = os.environ.get("GSC_AUTO_BUILD", "1") == "1"
+    so = os.environ.get("GSC_NATIVE_SO")
+    if so:  # an alternative build of the same module (e.g. the host-sanitizer build, scripts/asan_check.sh)
+        import importlib.util
+        import sys
+        spec = importlib.util.spec_from_file_location("gsc_amd._native", so)
+        _mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(_mod)
+        sys.modules["gsc_amd._native"] = _mod
+        return _mod
     try:
         _mod = importlib.import_module("gsc_amd._native")
     except ImportError:

@@ -21,8 +21,17 @@ ARCH = os.environ.get("GSC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
-def ext_path() -> str:
+def ext_path(sanitize: bool = False) -> str:
+    if sanitize:
+        return os.path.join(ROOT, "build", "asan", "_native" + sysconfig.get_config_var("EXT_SUFFIX"))
     return os.path.join(ROOT, "gsc_amd", "_native" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+# Host-only AddressSanitizer + UBSan build: every -fsanitize= goes after -Xarch_host,
+# so device code objects are unchanged (GPU ASan / XNACK are not available on this pool).
+SAN_COMPILE = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+               "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-g"]
+SAN_LINK = ["-fsanitize=address", "-fsanitize=undefined", "-shared-libsan", "-fno-gpu-sanitize"]
 
 
 def _includes():
@@ -46,31 +55,32 @@ def _headers():
     return glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
 
 
-def _obj(src: str) -> str:
+def _obj(src: str, sanitize: bool = False) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
-    return os.path.join(BUILD, rel + ".o")
+    return os.path.join(BUILD + ("_asan" if sanitize else ""), rel + ".o")
 
 
-def _compile(src: str, newest_header: float) -> str:
-    obj = _obj(src)
+def _compile(src: str, newest_header: float, sanitize: bool = False) -> str:
+    obj = _obj(src, sanitize)
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), newest_header):
         return obj
-    cmd = [HIPCC, "-c", src, "-o", obj] + _flags(src) + _includes()
+    cmd = [HIPCC, "-c", src, "-o", obj] + _flags(src) + _includes() + (SAN_COMPILE if sanitize else [])
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(verbose: bool = True, jobs: int = 8) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose: bool = True, jobs: int = 8, sanitize: bool = False) -> str:
+    os.makedirs(BUILD + ("_asan" if sanitize else ""), exist_ok=True)
     srcs = _sources()
     newest_header = max([os.path.getmtime(h) for h in _headers()] + [0.0])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, newest_header), srcs))
-    out = ext_path()
+        objs = list(ex.map(lambda s: _compile(s, newest_header, sanitize), srcs))
+    out = ext_path(sanitize)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + objs + (SAN_LINK if sanitize else [])
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -80,4 +90,4 @@ def build(verbose: bool = True, jobs: int = 8) -> str:
 
 
 if __name__ == "__main__":
-    build()
+    build(sanitize="--sanitize" in sys.argv)

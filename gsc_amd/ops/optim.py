@@ -82,6 +82,14 @@ class FusedAdamPolyak:
         # the step counter lives on the device so a captured HIP graph advances it on every replay
         self.step_t = torch.zeros((), dtype=torch.int64, device=flat.flat.device)
         self._host_step = 0
+        # non-finite gradient guard: [flag, skipped-count]; a flagged step leaves params/moments/target
+        # untouched (device-side decision, no host sync, works inside captured HIP graphs)
+        self.guard = torch.zeros(2, dtype=torch.int32, device=flat.flat.device)
+        self.guard_enabled = True
+
+    @property
+    def skipped_steps(self) -> int:
+        return int(self.guard[1].item())
 
     @property
     def step_count(self) -> int:
@@ -103,12 +111,23 @@ class FusedAdamPolyak:
         t = self.target.flat if self.target is not None else None
         if p.is_cuda:
             from gsc_amd.native import load
-            self.step_t.add_(1)
-            load().adam_polyak(p.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
-                               t.data_ptr() if t is not None else 0, p.numel(), self.lr, self.betas[0],
-                               self.betas[1], self.eps, 1, self.tau if t is not None else 0.0,
-                               float(grad_scale), self.wd, torch.cuda.current_stream(p.device).cuda_stream,
-                               step_ptr=self.step_t.data_ptr())
+            nat = load()
+            stream = torch.cuda.current_stream(p.device).cuda_stream
+            skip = 0
+            if self.guard_enabled:
+                nat.grad_guard(g.data_ptr(), self.fp.numel, self.guard.data_ptr(), stream)
+                skip = self.guard.data_ptr()
+                # a skipped step does not advance Adam's bias-correction counter
+                self.step_t.add_(1 - self.guard[0].to(torch.int64))
+            else:
+                self.step_t.add_(1)
+            nat.adam_polyak(p.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                            t.data_ptr() if t is not None else 0, p.numel(), self.lr, self.betas[0],
+                            self.betas[1], self.eps, 1, self.tau if t is not None else 0.0,
+                            float(grad_scale), self.wd, stream, step_ptr=self.step_t.data_ptr(), skip_ptr=skip)
+            return
+        if self.guard_enabled and not bool(torch.isfinite(g).all()):
+            self.guard[1] += 1
             return
         self._host_step += 1
         self.step_t.add_(1)
