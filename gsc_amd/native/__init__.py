@@ -20,10 +20,10 @@ def load(auto_build: bool = None):
         auto_build = os.environ.get("GSC_AUTO_BUILD", "1") == "1"
     so = os.environ.get("GSC_NATIVE_SO")
     if so:  # an alternative build of the same module (e.g. the host-sanitizer build, scripts/asan_check.sh)
-        import importlib.util
+        import importlib.util as ilu
         import sys
-        spec = importlib.util.spec_from_file_location("gsc_amd._native", so)
-        _mod = importlib.util.module_from_spec(spec)
+        spec = ilu.spec_from_file_location("gsc_amd._native", so)
+        _mod = ilu.module_from_spec(spec)
         spec.loader.exec_module(_mod)
         sys.modules["gsc_amd._native"] = _mod
         return _mod
