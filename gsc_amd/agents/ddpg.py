@@ -308,9 +308,15 @@ class BatchedTrainer:
                 self.sim_cus = k
                 self.sim_stream = torch.cuda.ExternalStream(nat.create_cu_masked_stream(list(range(k))),
                                                             device=self.device)
-                self.learn_stream = torch.cuda.ExternalStream(nat.create_cu_masked_stream(list(range(k, n))),
-                                                              device=self.device)
-                nat.gnn_set_cu_budget(n - k)  # size the GNN kernels' persistent grids for the learner partition
+                mode = os.environ.get("GSC_LEARNER_MASK", "1")
+                if mode == "0":
+                    # learner unmasked: its kernels also fill the simulator's CUs once the sim step ends
+                    self.learn_stream = torch.cuda.Stream(self.device)
+                else:
+                    self.learn_stream = torch.cuda.ExternalStream(
+                        nat.create_cu_masked_stream(list(range(k, n))), device=self.device)
+                budget = int(os.environ.get("GSC_GNN_CU_BUDGET", str(n - k)))
+                nat.gnn_set_cu_budget(budget)  # size the GNN kernels' persistent grids for the learner partition
             else:
                 self.sim_stream = torch.cuda.Stream(self.device)
 

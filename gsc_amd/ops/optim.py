@@ -8,6 +8,7 @@ single data-parallel all-reduce of its gradient.  Semantics match ``torch.optim.
 """
 from __future__ import annotations
 
+import os
 from typing import Iterable, List, Optional
 
 import torch
@@ -85,7 +86,7 @@ class FusedAdamPolyak:
         # non-finite gradient guard: [flag, skipped-count]; a flagged step leaves params/moments/target
         # untouched (device-side decision, no host sync, works inside captured HIP graphs)
         self.guard = torch.zeros(2, dtype=torch.int32, device=flat.flat.device)
-        self.guard_enabled = True
+        self.guard_enabled = os.environ.get("GSC_GRAD_GUARD", "1") != "0"
 
     @property
     def skipped_steps(self) -> int:
