@@ -26,19 +26,40 @@ sys.path.insert(0, ROOT)
 
 BASELINE_ENV_STEPS_PER_S = 57.4  # reference env-only throughput, Abilene + abc, 1 CPU core
 
+PRESETS = {
+    "abilene": dict(network=["configs/networks/abilene/abilene-in4-rand-cap1-2.graphml"],
+                    service="configs/service_functions/abc.yaml",
+                    sim_config="configs/config/simulator/sample_config.yaml",
+                    agent_config="configs/config/agent/sample_agent.yaml", envs=256, batch=None, period=0,
+                    model="GSC GATv2-DDPG (GNN 22x2L2I, actor [256] 893,628 params, critic [64] 223,997 params)"),
+    "syn50": dict(network=["configs/networks/synthetic/syn50-in8-cap1-3.graphml"],
+                  service="configs/service_functions/abc-3sfc.yaml",
+                  sim_config="configs/config/simulator/rand-arrival12_trace_syn50.yaml",
+                  agent_config="configs/config/agent/agent_syn50.yaml", envs=256, batch=None, period=0,
+                  model="GSC GATv2-DDPG, 50-node synthetic topology, 3 SFCs, trace traffic (A = 22,500)"),
+    "syn200": dict(network=[f"configs/networks/synthetic/syn200-in16-cap1-3-s{i}.graphml" for i in range(3)],
+                   service="configs/service_functions/abc-3sfc.yaml",
+                   sim_config="configs/config/simulator/sample_config.yaml",
+                   agent_config="configs/config/agent/agent_syn200.yaml", envs=64, batch=1024, period=2,
+                   model="GSC GATv2-DDPG, 200-node synthetic topologies switched every 2 episodes, 3 SFCs (A = 360,000)"),
+}
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--envs", type=int, default=256, help="environments per GPU")
+    ap.add_argument("--envs", type=int, default=None, help="environments per GPU (preset default: 256)")
     ap.add_argument("--batch-size", type=int, default=None, help="learner batch (default 100 * envs)")
     ap.add_argument("--updates-per-step", type=int, default=1)
-    ap.add_argument("--network", default="configs/networks/abilene/abilene-in4-rand-cap1-2.graphml")
-    ap.add_argument("--service", default="configs/service_functions/abc.yaml")
-    ap.add_argument("--sim-config", default="configs/config/simulator/sample_config.yaml")
-    ap.add_argument("--agent-config", default="configs/config/agent/sample_agent.yaml")
+    ap.add_argument("--preset", choices=sorted(PRESETS), default="abilene",
+                    help="abilene: BASELINE configs 2/3 (headline); syn50: config 4 (50-node + 3 SFCs + trace); "
+                         "syn200: config 5 (200-node topologies switched by the network scheduler)")
+    ap.add_argument("--network", default=None, help="override the preset's network(s) (comma-separated)")
+    ap.add_argument("--service", default=None)
+    ap.add_argument("--sim-config", default=None)
+    ap.add_argument("--agent-config", default=None)
     ap.add_argument("--device", default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-overlap", action="store_true", help="run the simulator on the learner's stream")
@@ -56,6 +77,15 @@ def main():
     from gsc_amd.parallel.dist import barrier, init_distributed, shutdown
     from gsc_amd.sim.batched import load_batched_from_paths
 
+    pre = PRESETS[args.preset]
+    networks = args.network.split(",") if args.network else pre["network"]
+    service = args.service or pre["service"]
+    sim_config = args.sim_config or pre["sim_config"]
+    agent_config = args.agent_config or pre["agent_config"]
+    if args.envs is None:
+        args.envs = pre["envs"]
+    if args.batch_size is None:
+        args.batch_size = pre["batch"]
     device_type = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
     info = init_distributed(device_type)
     if device_type == "cuda":
@@ -65,13 +95,14 @@ def main():
     else:
         device = torch.device("cpu")
     os.chdir(ROOT)
-    cfg = yaml.safe_load(open(args.agent_config))
-    sim = load_batched_from_paths([args.network], args.service, args.sim_config, cfg, args.envs, device=device,
+    cfg = yaml.safe_load(open(agent_config))
+    sim = load_batched_from_paths(networks, service, sim_config, cfg, args.envs, device=device,
                                   seed=args.seed * 1000 + info.rank)
     tcfg = TrainerConfig(num_envs=args.envs, batch_size=args.batch_size, updates_per_step=args.updates_per_step,
                          learning_starts=1, seed=args.seed + 17 * info.rank, check_every=0,
                          overlap_sim=not args.no_overlap, sim_cus=args.sim_cus)
-    trainer = BatchedTrainer(cfg, sim, tcfg, info)
+    trainer = BatchedTrainer(cfg, sim, tcfg, info, network_schedule=list(range(len(networks))),
+                             period=pre["period"])
 
     def sync():
         if device.type == "cuda":
@@ -113,7 +144,9 @@ def main():
     value = total_envs * args.steps / dt
     if info.is_main:
         rec = {
-            "metric": "env-steps/sec (whole node) + flow success ratio, Abilene SFC",
+            "metric": "env-steps/sec (whole node) + flow success ratio, Abilene SFC" if args.preset == "abilene"
+            else f"env-steps/sec (whole node) + flow success ratio, {args.preset} (BASELINE config "
+                 f"{'4' if args.preset == 'syn50' else '5'})",
             "value": round(value, 1),
             "unit": "env-steps/s",
             "n_gpus": info.world_size,
@@ -122,12 +155,15 @@ def main():
             "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_ENV_STEPS_PER_S, 1),
+            # BASELINE.md quotes the reference only on Abilene; the synthetic presets have no baseline
+            "vs_baseline": round(value / BASELINE_ENV_STEPS_PER_S, 1) if args.preset == "abilene" else None,
             "dtype": "bf16" if device.type == "cuda" else "fp32",
-            "data": "synthetic (coord-sim sample_config traffic on Abilene-in4-rand-cap1-2, abc SFC), random-init weights",
+            "data": (f"synthetic (coord-sim {os.path.basename(sim_config)} traffic on "
+                     f"{', '.join(os.path.basename(n) for n in networks)}, {os.path.basename(service)}), "
+                     "random-init weights"),
             "success_ratio": round(m["success_ratio"], 4),
             "config": {
-                "model": "GSC GATv2-DDPG (GNN 22x2L2I, actor [256] 893,628 params, critic [64] 223,997 params)",
+                "model": pre["model"],
                 "global_batch": trainer.batch_size * info.world_size,
                 "seq_len": sim.episode_steps,
                 "parallelism": f"dp{info.world_size}",
@@ -137,7 +173,7 @@ def main():
                 "updates_per_step": args.updates_per_step,
                 "sim_learner_overlap": not args.no_overlap,
                 "sim_cus": getattr(trainer, "sim_cus", 0),
-                "topology": os.path.basename(args.network),
+                "topology": ",".join(os.path.basename(n) for n in networks),
                 "device": torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu",
             },
         }

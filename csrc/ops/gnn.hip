@@ -528,13 +528,15 @@ static ClArgsMirror to_cl(const GnnArgs& a, py::dict t) {
 // Channel-lane kernels are the default for both directions (25.6k Abilene graphs on MI355X:
 // forward 155 us vs 200 us generic, backward 640 us vs 945 us generic).  GSC_GNN_GENERIC=1 selects
 // the generic kernels, GSC_GNN_CL_FWD_ONLY=1 only the channel-lane forward.
-static int g_gnn_path = -1;  // bit0: channel-lane forward, bit1: channel-lane backward, bit2: node-lane forward
+// bit0: channel-lane forward, bit1: channel-lane backward, bit2: node-lane forward (forced),
+// bit3: automatic node-lane forward for large graphs
+static int g_gnn_path = -1;
 static int gnn_path() {
   if (g_gnn_path < 0)
-    g_gnn_path = getenv("GSC_GNN_GENERIC") ? 0 : (getenv("GSC_GNN_CL_FWD_ONLY") ? 1 : 3);
+    g_gnn_path = getenv("GSC_GNN_GENERIC") ? 0 : (getenv("GSC_GNN_CL_FWD_ONLY") ? 1 : 3 | 8);
   return g_gnn_path;
 }
-void gnn_set_path(int bits) { g_gnn_path = bits & 7; }
+void gnn_set_path(int bits) { g_gnn_path = bits & 15; }
 static bool use_cl(const GnnArgs& a, bool backward = false) {
   const bool off = !(gnn_path() & (backward ? 2 : 1));
   int maxb = 0;
@@ -596,7 +598,10 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
                  int H, std::vector<int> layer_of, uintptr_t stream) {
   GnnArgs a = make_args(tables, params, x, topo, B, P, Fin, H, layer_of);
   a.emb = ptr<float>(emb);
-  if ((gnn_path() & 4) && gnn_nl_supported(Fin, H, a.NM, a.L)) {
+  // node-lane forward: forced by path bit 2, and chosen automatically for graphs with >= 32 node
+  // slots (50-node synthetic: 833 us vs 1737 us channel-lane per 25.6k graphs; Abilene: a tie)
+  const bool nl_auto = g_gnn_path < 0 || (g_gnn_path & 8);
+  if (((gnn_path() & 4) || (nl_auto && a.NM >= 32 && (gnn_path() & 1))) && gnn_nl_supported(Fin, H, a.NM, a.L)) {
     int maxb = 0;
     for (int i = 0; i < a.L; ++i) maxb = a.layer_of[i] > maxb ? a.layer_of[i] : maxb;
     gnn_nl_forward(a.params, maxb + 1, a.x, a.topo, ptr<const int32_t>(tables["in_src"].cast<uintptr_t>()), a.in_ptr,

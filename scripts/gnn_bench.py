@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--path", type=int, default=None, help="bits: 1 cl fwd, 2 cl bwd, 4 node-lane fwd (0 = generic)")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--hidden", type=int, default=22)
+    ap.add_argument("--network", default="configs/networks/abilene/abilene-in4-rand-cap1-2.graphml")
+    ap.add_argument("--n-pad", type=int, default=24)
     a = ap.parse_args()
     import torch
     from gsc_amd.coordsim.reader import load_topology
@@ -33,12 +35,11 @@ def main():
     if a.path is not None:
         nat.gnn_set_path(a.path)
     dev = "cuda"
-    gs = GraphSet([load_topology(os.path.join(ROOT, "configs/networks/abilene/abilene-in4-rand-cap1-2.graphml"))],
-                  24, dev)
+    gs = GraphSet([load_topology(os.path.join(ROOT, a.network))], a.n_pad, dev)
     emb = GNNEmbedder(3, a.hidden, 2, "mean", 2).to(dev)
     B = a.batch
     topo = torch.zeros(B, dtype=torch.int64, device=dev)
-    x = torch.rand(B, 24, 3, device=dev) * gs.node_mask[topo].unsqueeze(-1)
+    x = torch.rand(B, a.n_pad, 3, device=dev) * gs.node_mask[topo].unsqueeze(-1)
     w = torch.randn(a.hidden, device=dev)
     params = list(emb.parameters())
 
