@@ -7,6 +7,7 @@
 //   target = tau * p + (1 - tau) * target                     (after the step, as in the reference)
 // The target update is fused because targets are only read by the *next* update.
 // 16-byte vectorised, grid-stride; HBM-bound (20 B read + 16 B written per parameter).
+#include <hip/hip_bf16.h>
 #include <pybind11/pybind11.h>
 
 #include "../common.h"
@@ -25,7 +26,14 @@ struct AdamArgs {
   float lr, b1, b2, eps, bc1, bc2_sqrt, tau, grad_scale, weight_decay;
   const long long* step;  // optional device step counter (HIP-graph replay); overrides bc1/bc2_sqrt
   const int* skip;        // optional device flag: non-zero -> leave p, m, v, target untouched (bad grads)
+  __hip_bfloat16* p16;    // optional bf16 shadow of p (round-to-nearest-even, = autocast's cast)
+  __hip_bfloat16* t16;    // optional bf16 shadow of target
 };
+
+__device__ __forceinline__ void store_bf16x4(__hip_bfloat16* dst, long i4, const float4& v) {
+  __hip_bfloat16 h[4] = {__float2bfloat16(v.x), __float2bfloat16(v.y), __float2bfloat16(v.z), __float2bfloat16(v.w)};
+  *reinterpret_cast<uint2*>(dst + 4 * i4) = *reinterpret_cast<const uint2*>(h);
+}
 
 __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamArgs& a) {
   g *= a.grad_scale;
@@ -57,6 +65,7 @@ __global__ __launch_bounds__(256) void adam_polyak_kernel(AdamArgs a) {
     reinterpret_cast<float4*>(a.p)[i] = p;
     reinterpret_cast<float4*>(a.m)[i] = m;
     reinterpret_cast<float4*>(a.v)[i] = v;
+    if (a.p16) store_bf16x4(a.p16, i, p);
     if (a.target) {
       float4 t = reinterpret_cast<float4*>(a.target)[i];
       t.x = a.tau * p.x + (1.f - a.tau) * t.x;
@@ -64,6 +73,7 @@ __global__ __launch_bounds__(256) void adam_polyak_kernel(AdamArgs a) {
       t.z = a.tau * p.z + (1.f - a.tau) * t.z;
       t.w = a.tau * p.w + (1.f - a.tau) * t.w;
       reinterpret_cast<float4*>(a.target)[i] = t;
+      if (a.t16) store_bf16x4(a.t16, i, t);
     }
   }
   // tail
@@ -73,13 +83,17 @@ __global__ __launch_bounds__(256) void adam_polyak_kernel(AdamArgs a) {
     a.p[i] = p;
     a.m[i] = m;
     a.v[i] = v;
-    if (a.target) a.target[i] = a.tau * p + (1.f - a.tau) * a.target[i];
+    if (a.p16) a.p16[i] = __float2bfloat16(p);
+    if (a.target) {
+      a.target[i] = a.tau * p + (1.f - a.tau) * a.target[i];
+      if (a.t16) a.t16[i] = __float2bfloat16(a.target[i]);
+    }
   }
 }
 
 void adam_polyak(uintptr_t p, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t target, long n, float lr, float b1,
                  float b2, float eps, long step, float tau, float grad_scale, float weight_decay, uintptr_t stream,
-                 uintptr_t step_ptr, uintptr_t skip_ptr) {
+                 uintptr_t step_ptr, uintptr_t skip_ptr, uintptr_t p16, uintptr_t t16) {
   GSC_CHECK((p & 15) == 0 && (g & 15) == 0 && (m & 15) == 0 && (v & 15) == 0 && (target & 15) == 0,
             "adam_polyak buffers must be 16-byte aligned");
   AdamArgs a;
@@ -100,6 +114,9 @@ void adam_polyak(uintptr_t p, uintptr_t g, uintptr_t m, uintptr_t v, uintptr_t t
   a.weight_decay = weight_decay;
   a.step = step_ptr ? ptr<const long long>(step_ptr) : nullptr;
   a.skip = skip_ptr ? ptr<const int>(skip_ptr) : nullptr;
+  GSC_CHECK((p16 & 7) == 0 && (t16 & 7) == 0, "bf16 shadows must be 8-byte aligned");
+  a.p16 = p16 ? ptr<__hip_bfloat16>(p16) : nullptr;
+  a.t16 = t16 ? ptr<__hip_bfloat16>(t16) : nullptr;
   const long n4 = (n + 3) / 4;
   long grid = (n4 + 255) / 256;
   if (grid > 2048) grid = 2048;
@@ -147,7 +164,7 @@ void register_optim(py::module_& m) {
   m.def("adam_polyak", &adam_polyak, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("target"),
         py::arg("n"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("step"), py::arg("tau"),
         py::arg("grad_scale"), py::arg("weight_decay"), py::arg("stream"), py::arg("step_ptr") = 0,
-        py::arg("skip_ptr") = 0);
+        py::arg("skip_ptr") = 0, py::arg("p16") = 0, py::arg("t16") = 0);
   m.def("polyak", &polyak);
 }
 

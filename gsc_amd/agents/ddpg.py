@@ -66,6 +66,11 @@ class DDPGLearner:
         self.actor_opt = FusedAdamPolyak(self.actor_flat, lr=lr, target=self.target_actor_flat, tau=tau)
         self.masks = graphs.action_masks(C, F_)
         self.amp = (self.device.type == "cuda") if amp_bf16 is None else bool(amp_bf16)
+        if self.amp and self.device.type == "cuda":
+            # bf16 shadows of all four networks, refreshed by the fused Adam/Polyak kernels
+            for fp in (self.actor_flat, self.critic_flat, self.target_actor_flat, self.target_critic_flat):
+                fp.enable_shadow()
+            self.masks._bf16 = self.masks.to(torch.bfloat16)
         self.updates = 0
         self.last: Dict[str, torch.Tensor] = {}
         self._graphs = None
@@ -80,6 +85,11 @@ class DDPGLearner:
             # must not keep cached casts alive across replays
             return torch.autocast(device_type=self.device.type, dtype=torch.bfloat16, cache_enabled=False)
         return torch.autocast(device_type=self.device.type, enabled=False)
+
+    def refresh_shadows(self) -> None:
+        """Re-derive the bf16 shadows after parameters were written outside the optimizer."""
+        for fp in (self.actor_flat, self.critic_flat, self.target_actor_flat, self.target_critic_flat):
+            fp.refresh_shadow()
 
     @torch.no_grad()
     def act(self, obs: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:

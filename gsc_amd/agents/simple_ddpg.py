@@ -270,6 +270,7 @@ class SimpleDDPG(RLSPAgent):
             raise ValueError(f"{path}: not an actor file")
         self.actor.load_state_dict(d["state_dict"])
         self.learner.target_actor.load_state_dict(d["state_dict"])
+        self.learner.refresh_shadows()
 
     def state_dict(self) -> dict:
         base = {"backend": self.backend, "global_step": self.global_step, "episode": self.episode,
@@ -320,6 +321,7 @@ class SimpleDDPG(RLSPAgent):
         from gsc_amd.parallel.dist import broadcast_tensors
         L = self.learner
         broadcast_tensors([L.actor_flat.flat, L.critic_flat.flat, L.target_actor_flat.flat, L.target_critic_flat.flat])
+        L.refresh_shadows()
 
     def save_checkpoint(self, path: str) -> None:
         ckpt.save_checkpoint(path, self.state_dict(), meta={"experiment_id": self.agent_helper.experiment_id,

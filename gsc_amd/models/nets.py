@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from gsc_amd.ops.linear import linear
+from gsc_amd.ops.linear import composed_projection, linear, shadow
 from .gnn import GNNEmbedder
 from .graphs import GraphSet
 
@@ -50,15 +50,20 @@ class MaskedInputMLP(nn.Module):
 
     def first_layer(self, dense, topo, masks, extra=None):
         W = self.first.weight
+        W16 = shadow(W)
+        sl = lambda a, b: (W[:, a:b], W16[:, a:b] if W16 is not None else None)
         D, A = self.dense_dim, self.mask_dim
-        h = linear(dense, W[:, :D], self.first.bias)
-        topo_bias = F.linear(masks, W[:, D:D + A])           # [T, h1]
+        w, w16 = sl(0, D)
+        h = linear(dense, w, self.first.bias, w16=w16)
+        w, w16 = sl(D, D + A)
+        topo_bias = linear(masks, w, w16=w16)                # [T, h1]
         h = h + select_rows(topo_bias, topo)
         if extra is not None:
-            h = h + linear(extra, W[:, D + A:])
+            w, w16 = sl(D + A, W.shape[1])
+            h = h + linear(extra, w, w16=w16)
         return h
 
-    def forward(self, dense, topo, masks, extra=None, out_mask=None):
+    def forward(self, dense, topo, masks, extra=None, out_mask=None, out_mask16=None):
         """``out_mask`` [out_dim]: multiply the output by a constant 0/1 vector, folded into the last
         layer's weight rows and bias (same values as masking the ``[B, out]`` output, no extra pass)."""
         h = self.first_layer(dense, topo, masks, extra)
@@ -68,7 +73,7 @@ class MaskedInputMLP(nn.Module):
                 continue
             h = F.relu(h)
             if i == last and out_mask is not None:
-                h = linear(h, layer.weight * out_mask.unsqueeze(1), layer.bias * out_mask)
+                h = linear(h, layer.weight, layer.bias, row_mask=out_mask, row_mask16=out_mask16)
             else:
                 h = linear(h, layer.weight, layer.bias)
         if last == 0 and out_mask is not None:
@@ -118,7 +123,8 @@ class Actor(nn.Module):
         if self.squash:
             return torch.sigmoid(self.mlp(emb, topo, masks)) * select_rows(masks, topo)
         if masks.shape[0] == 1:  # one topology: fold the output mask into the last layer
-            return self.mlp(emb, topo, masks, out_mask=masks[0])
+            m16 = shadow(masks)
+            return self.mlp(emb, topo, masks, out_mask=masks[0], out_mask16=m16[0] if m16 is not None else None)
         out = self.mlp(emb, topo, masks)
         return out * select_rows(masks, topo)
 
@@ -161,12 +167,13 @@ class QNetwork(nn.Module):
         D, A = mlp.dense_dim, mlp.mask_dim
         W1 = mlp.first.weight
         Wa = W1[:, D + A:]                                   # [h1, A]
+        W16 = shadow(W1)
+        if W16 is not None:
+            Wa._bf16 = W16[:, D + A:]
         last = actor.mlp.layers[-1]
-        m = masks[0]
-        W2m = last.weight * m.unsqueeze(1)                   # [A, z]
-        b2m = last.bias * m                                  # [A]
-        Mc = Wa @ W2m                                        # [h1, z]
-        cb = Wa @ b2m                                        # [h1]
+        m16 = shadow(masks)
+        Mc, cb = composed_projection(Wa, last.weight, last.bias, masks[0],
+                                     m16[0] if m16 is not None else None)   # [h1, z], [h1]
         emb = self.embedder(x, topo, graphs)
         h = mlp.first_layer(emb, topo, masks) + linear(z, Mc, cb)
         for layer in mlp.layers[1:]:

@@ -32,6 +32,21 @@ class FlatParams:
             self.flat[o:o + p.numel()].copy_(p.detach().reshape(-1))
             p.data = self.flat[o:o + p.numel()].view_as(p)
         self.grad = torch.zeros_like(self.flat)
+        self.flat16 = None
+
+    def enable_shadow(self) -> None:
+        """Keep a bf16 copy of the parameters (``param._bf16`` views) for the bf16 GEMMs.
+
+        The fused Adam/Polyak kernel refreshes it in the same pass that writes the fp32 values, with
+        the same round-to-nearest-even cast autocast would apply — so forwards need no cast kernels
+        and produce bit-identical results."""
+        self.flat16 = self.flat.to(torch.bfloat16)
+        for p, o in zip(self.params, self.offsets):
+            p._bf16 = self.flat16[o:o + p.numel()].view_as(p)
+
+    def refresh_shadow(self) -> None:
+        if self.flat16 is not None:
+            self.flat16.copy_(self.flat)
 
     def view(self) -> torch.Tensor:
         return self.flat[: self.numel]
@@ -68,6 +83,7 @@ class FlatParams:
 
     def load_flat_(self, src: torch.Tensor) -> None:
         self.flat[: self.numel].copy_(src[: self.numel])
+        self.refresh_shadow()
 
 
 class FusedAdamPolyak:
@@ -125,7 +141,10 @@ class FusedAdamPolyak:
             nat.adam_polyak(p.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                             t.data_ptr() if t is not None else 0, p.numel(), self.lr, self.betas[0],
                             self.betas[1], self.eps, 1, self.tau if t is not None else 0.0,
-                            float(grad_scale), self.wd, stream, step_ptr=self.step_t.data_ptr(), skip_ptr=skip)
+                            float(grad_scale), self.wd, stream, step_ptr=self.step_t.data_ptr(), skip_ptr=skip,
+                            p16=self.fp.flat16.data_ptr() if self.fp.flat16 is not None else 0,
+                            t16=(self.target.flat16.data_ptr()
+                                 if t is not None and getattr(self.target, "flat16", None) is not None else 0))
             return
         if self.guard_enabled and not bool(torch.isfinite(g).all()):
             self.guard[1] += 1

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--rows", type=int, default=40)
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--trace", default=None, help="write a chrome trace here")
+    ap.add_argument("--by-count", action="store_true", help="sort framework ops by call count")
     a = ap.parse_args()
     import torch
     import yaml
@@ -35,7 +36,7 @@ def main():
                                   "configs/service_functions/abc.yaml", "configs/config/simulator/sample_config.yaml",
                                   cfg, a.envs, device="cuda")
     tr = BatchedTrainer(cfg, sim, TrainerConfig(num_envs=a.envs, learning_starts=1, check_every=0,
-                                                overlap_sim=not a.no_overlap))
+                                                overlap_sim=not a.no_overlap, cuda_graphs=False))
     for _ in range(a.warmup):
         tr.step()
     torch.cuda.synchronize()
@@ -48,7 +49,7 @@ def main():
                    max_shapes_column_width=70))
     # framework ops with full input shapes, by self device time per step
     rows = [e for e in ka if e.key.startswith("aten::") and e.self_device_time_total > 0]
-    rows.sort(key=lambda e: -e.self_device_time_total)
+    rows.sort(key=lambda e: -e.count if a.by_count else -e.self_device_time_total)
     print(f"{'us/step':>9} {'calls/step':>10}  op  shapes")
     for e in rows[:a.rows]:
         print(f"{e.self_device_time_total / a.steps:9.1f} {e.count / a.steps:10.1f}  {e.key}  {e.input_shapes}")

@@ -46,3 +46,31 @@ def test_graphed_update_matches_eager():
         torch.testing.assert_close(getattr(graphed, name).flat, getattr(eager, name).flat, rtol=1e-5, atol=1e-6)
     assert graphed.actor_opt.step_count == eager.actor_opt.step_count == 6
     torch.testing.assert_close(graphed.last["qf1_loss"], eager.last["qf1_loss"], rtol=1e-5, atol=1e-6)
+
+
+def test_bf16_shadows_match_autocast_casts():
+    """Updates using the bf16 parameter shadows == updates where autocast casts the fp32 weights."""
+    dev = "cuda"
+    cfg = yaml.safe_load(open(cfg_path("config", "agent", "sample_agent.yaml")))
+    gs = GraphSet([load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml"))], 24, dev)
+    a = DDPGLearner(cfg, 3, 1728, gs, 1, 3, dev, seed=9)
+    b = DDPGLearner(cfg, 3, 1728, gs, 1, 3, dev, seed=9)
+    for fp in (b.actor_flat, b.critic_flat, b.target_actor_flat, b.target_critic_flat):
+        fp.flat16 = None
+        for p in fp.params:
+            del p._bf16
+    del b.masks._bf16
+    for bt in _batches(3, 9000, dev):
+        a.update(bt)
+        b.update(bt)
+    torch.cuda.synchronize()
+    # identical except the actor's output bias, whose gradient the shadow path's composed projection
+    # accumulates in fp32 where autocast's bf16 matmul rounds it (|diff| ~ 1e-6 after 3 Adam steps)
+    for name in ("actor_flat", "critic_flat", "target_critic_flat"):
+        torch.testing.assert_close(getattr(a, name).flat, getattr(b, name).flat, rtol=1e-5, atol=2e-5)
+    n_b2 = a.actor.mlp.layers[-1].bias.numel()
+    torch.testing.assert_close(a.actor_flat.flat[:a.actor_flat.numel - n_b2],
+                               b.actor_flat.flat[:b.actor_flat.numel - n_b2], rtol=1e-5, atol=1e-6)
+    # the shadow tracks the fp32 parameters exactly (round-to-nearest-even)
+    assert torch.equal(a.actor_flat.flat16, a.actor_flat.flat.to(torch.bfloat16))
+    assert torch.equal(a.target_critic_flat.flat16, a.target_critic_flat.flat.to(torch.bfloat16))
