@@ -147,12 +147,12 @@ def main():
             "metric": "env-steps/sec (whole node) + flow success ratio, Abilene SFC" if args.preset == "abilene"
             else f"env-steps/sec (whole node) + flow success ratio, {args.preset} (BASELINE config "
                  f"{'4' if args.preset == 'syn50' else '5'})",
-            "value": round(value, 1),
+            "value": float(f"{value:.6g}"),
             "unit": "env-steps/s",
             "n_gpus": info.world_size,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "ms_per_step": float(f"{dt / args.steps * 1e3:.6g}"),
             "higher_is_better": True,
             "scaling": "weak",
             # BASELINE.md quotes the reference only on Abilene; the synthetic presets have no baseline

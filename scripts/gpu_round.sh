@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
 STEPS=${STEPS:-30}
-timeout -k 10 600 python -m pytest $R/tests -m gpu -x -q > $OUT/gpu_tests.log 2>&1 &&
+timeout -k 10 600 python -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1 &&
 timeout -k 10 300 python -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
 timeout -k 10 400 python $R/bench.py --steps $STEPS --warmup 5 > $OUT/bench.log 2>&1 &&
 cd /tmp && export TMPDIR=/tmp &&
