@@ -496,6 +496,9 @@ struct ClArgsMirror {
   int B, P, Fin, H, L, M, NM, n_params, n_blocks, waves;
   int layer_of[kGnnMaxLayers];
   unsigned long long* prof;
+  const void* s_dst;
+  const void* s_src;
+  int MP;
 };
 bool gnn_cl_supported(int Fin, int H, int L, int n_blocks);
 bool gnn_nl_supported(int Fin, int H, int NP, int L);
@@ -504,6 +507,9 @@ void gnn_nl_forward(const float* params, int n_blocks, const float* x, const int
                     int H, int L, int M, int NP, const int* layer_of, uintptr_t stream, int cus);
 void gnn_cl_forward(const void* args, uintptr_t stream, int cus);
 int gnn_cl_backward(const void* args, uintptr_t stream, int cus, int max_rows);
+bool gnn_mf_supported(int Fin, int H, int NM, int L, int n_blocks, const int* layer_of);
+void gnn_mf_forward(const void* args, uintptr_t stream, int cus);
+int gnn_mf_backward(const void* args, uintptr_t stream, int cus, int max_rows);
 
 static unsigned long long* g_gnn_prof = nullptr;  // device buffer of 12 counters, or null
 void gnn_set_profile(uintptr_t p) { g_gnn_prof = reinterpret_cast<unsigned long long*>(p); }
@@ -522,26 +528,43 @@ static ClArgsMirror to_cl(const GnnArgs& a, py::dict t) {
   c.n_blocks = maxb + 1;
   c.waves = 4;
   c.prof = g_gnn_prof;
+  if (t.contains("s_dst")) {
+    c.s_dst = reinterpret_cast<const void*>(t["s_dst"].cast<uintptr_t>());
+    c.s_src = reinterpret_cast<const void*>(t["s_src"].cast<uintptr_t>());
+    c.MP = t["MP"].cast<int>();
+  }
   return c;
 }
 
-// Channel-lane kernels are the default for both directions (25.6k Abilene graphs on MI355X:
-// forward 155 us vs 200 us generic, backward 640 us vs 945 us generic).  GSC_GNN_GENERIC=1 selects
-// the generic kernels, GSC_GNN_CL_FWD_ONLY=1 only the channel-lane forward.
-// bit0: channel-lane forward, bit1: channel-lane backward, bit2: node-lane forward (forced),
-// bit3: automatic node-lane forward for large graphs
+// Path bits: bit0 channel-lane forward, bit1 channel-lane backward, bit2 node-lane forward (forced),
+// bit3 automatic node-lane forward for large graphs, bit4 MFMA forward, bit5 MFMA backward.
+// Default: MFMA kernels (gnn_mf.hip) where they apply, else channel-lane, else generic.
+// 25.6k Abilene graphs on MI355X: channel-lane forward 143 us / backward 924 us (generic 200 / 945).
+// GSC_GNN_GENERIC=1 selects the generic kernels, GSC_GNN_CL=1 the channel-lane ones (no MFMA),
+// GSC_GNN_CL_FWD_ONLY=1 only the channel-lane forward.
 static int g_gnn_path = -1;
 static int gnn_path() {
   if (g_gnn_path < 0)
-    g_gnn_path = getenv("GSC_GNN_GENERIC") ? 0 : (getenv("GSC_GNN_CL_FWD_ONLY") ? 1 : 3 | 8);
+    g_gnn_path = getenv("GSC_GNN_GENERIC") ? 0
+                 : getenv("GSC_GNN_CL_FWD_ONLY") ? 1
+                 : getenv("GSC_GNN_CL") ? (3 | 8)
+                 : (3 | 8 | 16 | 32);
   return g_gnn_path;
 }
-void gnn_set_path(int bits) { g_gnn_path = bits & 15; }
-static bool use_cl(const GnnArgs& a, bool backward = false) {
-  const bool off = !(gnn_path() & (backward ? 2 : 1));
+void gnn_set_path(int bits) { g_gnn_path = bits & 63; }
+static int max_block(const GnnArgs& a) {
   int maxb = 0;
   for (int i = 0; i < a.L; ++i) maxb = a.layer_of[i] > maxb ? a.layer_of[i] : maxb;
-  return !off && gnn_cl_supported(a.Fin, a.H, a.L, maxb + 1);
+  return maxb;
+}
+static bool use_cl(const GnnArgs& a, bool backward = false) {
+  const bool off = !(gnn_path() & (backward ? 2 : 1));
+  return !off && gnn_cl_supported(a.Fin, a.H, a.L, max_block(a) + 1);
+}
+static bool use_mf(const GnnArgs& a, py::dict t, bool backward = false) {
+  const bool off = !(gnn_path() & (backward ? 32 : 16));
+  const bool uniq = t.contains("uniq") && t["uniq"].cast<bool>() && t.contains("s_dst");
+  return !off && uniq && gnn_mf_supported(a.Fin, a.H, a.NM, a.L, max_block(a) + 1, a.layer_of);
 }
 static GnnArgs make_args(py::dict t, uintptr_t params, uintptr_t x, uintptr_t topo, int B, int P, int Fin, int H,
                          std::vector<int> layer_of) {
@@ -608,6 +631,11 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
                    a.deg, a.nnodes, a.emb, B, P, Fin, H, a.L, a.M, a.NM, a.layer_of, stream, num_cus());
     return;
   }
+  if (use_mf(a, tables)) {
+    const ClArgsMirror c = to_cl(a, tables);
+    gnn_mf_forward(&c, stream, num_cus());
+    return;
+  }
   if (use_cl(a)) {
     const ClArgsMirror c = to_cl(a, tables);
     gnn_cl_forward(&c, stream, num_cus());
@@ -632,9 +660,10 @@ void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo
   GnnArgs a = make_args(tables, params, x, topo, B, P, Fin, H, layer_of);
   a.demb = ptr<const float>(demb);
   a.partials = ptr<float>(partials);
-  if (use_cl(a, true)) {
+  if (use_mf(a, tables, true) || use_cl(a, true)) {
     const ClArgsMirror c = to_cl(a, tables);
-    const int rows = gnn_cl_backward(&c, stream, num_cus(), max_rows);
+    const int rows = use_mf(a, tables, true) ? gnn_mf_backward(&c, stream, num_cus(), max_rows)
+                                     : gnn_cl_backward(&c, stream, num_cus(), max_rows);
     hipLaunchKernelGGL(column_sum_kernel, dim3((a.n_params + 31) / 32), dim3(256), 0, stream_of(stream),
                        (const float*)a.partials, ptr<float>(grad_out), rows, a.n_params);
     check_launch();
@@ -694,7 +723,7 @@ void register_gnn(py::module_& m) {
   m.def("gnn_fused_fits", &gnn_fused_fits);
   m.def("gnn_set_cu_budget", &gnn_set_cu_budget, "CUs available to GNN launches (0 = whole device)");
   m.def("gnn_set_profile", &gnn_set_profile, "device int64[12] phase-cycle counters for the generic backward (0 = off)");
-  m.def("gnn_set_path", &gnn_set_path, "bit0: channel-lane forward, bit1: channel-lane backward");
+  m.def("gnn_set_path", &gnn_set_path, "bit0/1: channel-lane fwd/bwd, bit2: node-lane fwd, bit3: auto node-lane, bit4/5: MFMA fwd/bwd");
   m.def("gnn_get_path", &gnn_path);
 }
 

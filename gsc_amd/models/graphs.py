@@ -30,6 +30,9 @@ class GraphSet:
             loops = np.arange(t.n, dtype=np.int64)
             msgs.append((np.concatenate([ei[0], loops]), np.concatenate([ei[1], loops])))
         self.M = max(len(s) for s, _ in msgs)
+        # every (source, target) pair at most once: the MFMA kernels scatter attention weights into a
+        # dense [target][source] matrix (gsc_amd/ops/gnn.py falls back to other kernels otherwise)
+        self.unique_messages = all(len(set(zip(s.tolist(), d.tolist()))) == len(s) for s, d in msgs)
         src = np.zeros((T, self.M), np.int64)
         dst = np.zeros((T, self.M), np.int64)
         valid = np.zeros((T, self.M), bool)
@@ -90,6 +93,19 @@ class GraphSet:
         self.out_ptr = torch.from_numpy(out_ptr).to(dev)
         self.out_msg = torch.from_numpy(out_msg).to(dev)
         self.n_nodes_i32 = self.n_nodes.to(torch.int32)
+        # one-hot message matrices of the MFMA backward (csrc/ops/gnn_mf.hip), bf16 [T, 32, MP]:
+        # s_dst[t, i, q] = 1 if message q (target-sorted order) ends at node i, s_src likewise for
+        # its source; dX_r = s_dst G and dX_l = s_src G are then matrix-core products
+        self.mf_mp = ((self.M + 15) // 16) * 16
+        s_dst = np.zeros((T, 32, self.mf_mp), np.float32)
+        s_src = np.zeros((T, 32, self.mf_mp), np.float32)
+        if self.max_nodes <= 32:
+            for i, (s, _) in enumerate(msgs):
+                q = np.arange(len(s))
+                s_dst[i, in_dst[i, :len(s)], q] = 1.0
+                s_src[i, in_src[i, :len(s)], q] = 1.0
+        self.s_dst = torch.from_numpy(s_dst).to(dev, torch.bfloat16)
+        self.s_src = torch.from_numpy(s_src).to(dev, torch.bfloat16)
 
     @property
     def num_topologies(self) -> int:

@@ -16,7 +16,8 @@ def _tables(graphs) -> dict:
                  out_msg=graphs.out_msg.data_ptr(), deg=graphs.deg.data_ptr(), nnodes=graphs.n_nodes_i32.data_ptr(),
                  nmsgs=graphs.num_msgs.data_ptr(), M=int(graphs.M), NM=int(graphs.max_nodes),
                  in_src=graphs.in_src.data_ptr(), in_dst=graphs.in_dst.data_ptr(), out_q=graphs.out_q.data_ptr(),
-                 out_dst=graphs.out_dst.data_ptr())
+                 out_dst=graphs.out_dst.data_ptr(), uniq=bool(graphs.unique_messages),
+                 s_dst=graphs.s_dst.data_ptr(), s_src=graphs.s_src.data_ptr(), MP=int(graphs.mf_mp))
         graphs._kernel_tables = t
     return t
 

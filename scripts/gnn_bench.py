@@ -15,6 +15,8 @@ sys.path.insert(0, ROOT)
 
 PHASES = ["topo", "fwd-recompute", "bias", "d-alpha", "softmax-bwd", "d-att", "dxl/dxr", "dW", "d-bl/br|dh(cl)",
           "dh|relu-mask(cl)", "-", "-"]
+MF_PHASES = ["topo+x", "fwd-recompute", "x_l/x_r", "bias+p+ssum", "scatter dX", "dX images", "dW mfma", "dh mfma",
+             "-", "-", "-", "-"]
 
 
 def main():
@@ -73,9 +75,10 @@ def main():
         p = prof.cpu().tolist()
         tot = sum(p)
         print("backward phase cycles per graph (s_memtime ticks, summed over waves; cl: bias+d-alpha in 'd-alpha'):")
+        names = MF_PHASES if nat.gnn_get_path() & 32 else PHASES
         for k, v in enumerate(p):
             if v:
-                print(f"  {PHASES[k]:>14}: {v / B:10.1f}  ({100 * v / tot:5.1f} %)")
+                print(f"  {names[k]:>14}: {v / B:10.1f}  ({100 * v / tot:5.1f} %)")
 
 
 if __name__ == "__main__":
