@@ -335,15 +335,17 @@ class BatchedTrainer:
 
     @staticmethod
     def auto_sim_cus(sim) -> int:
-        """CUs for one round of the simulator's env workgroups (as many envs per CU as LDS holds),
-        rounded up to whole CU-mask groups of 8 (one CU per XCD) and capped at half the device.
-        Measured on MI355X, 256 Abilene envs: 64 CUs -> 49.6k env-steps/s vs 37.3k unpartitioned."""
+        """CUs for one round of the simulator's env workgroups, at most 3 envs (waves) per CU so every
+        simulator wave keeps a SIMD to itself and the fourth SIMD takes learner waves, rounded up to
+        whole CU-mask groups of 8 (one CU per XCD) plus one group of slack, capped at half the device.
+        Measured on MI355X, 256 Abilene envs with the MFMA GNN learner (env-steps/s): 64 CUs (4 per
+        CU) 65.3k, 80 CUs 65.5k, 96 CUs 70.5k, 112 CUs 70.1k, 128 CUs 69.7k, 160 CUs 60.5k."""
         nat = sim.native
         n = nat.cu_count()
         lds = max(int(sim.ctx.lds_per_env), 1)
-        per_cu = max(1, (160 * 1024) // lds)
+        per_cu = max(1, min(3, (160 * 1024) // lds))
         need = -(-sim.E // per_cu)
-        k = 8 * -(-need // 8)
+        k = 8 * -(-need // 8) + (8 if per_cu > 1 else 0)
         return int(min(max(k, 8), n // 2))
 
     def _schedule_next(self) -> None:
