@@ -100,20 +100,59 @@ class DDPGLearner:
         return allreduce_sum_(flat.grad, async_op=True)
 
     # -- update stages (eager or captured into HIP graphs) ---------------------------------------
-    def _stage_critic(self, b: Batch) -> None:
-        """TD target + critic loss -> critic gradients in ``critic_flat.grad``."""
+    def _side_streams(self):
+        """Two side streams for the independent branches of an update (GPU only; opt-in with
+        GSC_LEARNER_BRANCHES=1).  Measured on MI355X (headline bench, 3 alternating runs each): off
+        70.3k, on 66.8k env-steps/s -- the learner already fits under the simulator kernel, and the
+        extra concurrency lands learner waves on the simulator's CUs and slows the critical path."""
+        if self.device.type != "cuda" or os.environ.get("GSC_LEARNER_BRANCHES", "0") == "0":
+            return None
+        if getattr(self, "_sides", None) is None:
+            self._sides = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
+        return self._sides
+
+    def _target(self, b: Batch) -> torch.Tensor:
         g, masks = self.graphs, self.masks
         with torch.no_grad(), self._autocast():
             # the clamped target action stays bf16: the target critic consumes it as a GEMM operand
             a2 = self.target_actor(b.next_obs, b.topo, g, masks).clamp(-1, 1)
             q2 = self.target_critic(b.next_obs, b.topo, g, masks, a2).float().view(-1)
-            y = b.rewards + (1 - b.dones) * self.gamma * q2
+            return b.rewards + (1 - b.dones) * self.gamma * q2
+
+    def _stage_critic(self, b: Batch) -> None:
+        """TD target + critic loss -> critic gradients in ``critic_flat.grad``, and the actor forward.
+
+        On the GPU the three independent chains -- target actor/critic on next_obs, critic on obs,
+        actor on obs -- run as parallel branches (two side streams; inside a HIP graph they become
+        concurrent graph branches), so their many small kernels overlap instead of queueing."""
+        g, masks = self.graphs, self.masks
+        side = self._side_streams()
+        if side is None:
+            y = self._target(b)
+            with self._autocast():
+                q = self.critic(b.obs, b.topo, g, masks, b.actions).float().view(-1)
+            self._stage_actor_fwd(b)
+        else:
+            cur = torch.cuda.current_stream(self.device)
+            s_t, s_a = side
+            s_t.wait_stream(cur)
+            s_a.wait_stream(cur)
+            with torch.cuda.stream(s_t):
+                y = self._target(b)
+            with torch.cuda.stream(s_a):
+                self._stage_actor_fwd(b)
+            with self._autocast():
+                q = self.critic(b.obs, b.topo, g, masks, b.actions).float().view(-1)
+            cur.wait_stream(s_t)
+            y.record_stream(cur)
         with self._autocast():
-            q = self.critic(b.obs, b.topo, g, masks, b.actions).float().view(-1)
             lq = F.mse_loss(q, y)
         grads = torch.autograd.grad(lq, self.critic_flat.params)
         self.critic_flat.set_grads(grads)
         self._lq, self._qv = lq.detach(), q.detach().mean()
+        if side is not None:
+            cur.wait_stream(side[1])
+            self._a.record_stream(cur)
 
     def _composed(self) -> bool:
         # one topology and at least one actor hidden layer: critic(obs, actor(obs)) re-associated
@@ -151,9 +190,8 @@ class DDPGLearner:
     def update(self, b: Batch) -> None:
         """One DDPG update, eager.  The critic-gradient all-reduce overlaps the actor forward."""
         inv_world = 1.0 / self.dist.world_size
-        self._stage_critic(b)
+        self._stage_critic(b)        # includes the actor forward (it does not read critic weights)
         h_c = self._allreduce(self.critic_flat)
-        self._stage_actor_fwd(b)     # does not read critic weights
         if h_c is not None:
             h_c.wait()
         self._stage_actor_grad(b, inv_world)
@@ -205,13 +243,12 @@ class DDPGLearner:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 self._stage_critic(b)
-                self._stage_actor_fwd(b)
                 self._stage_actor_grad(b, inv_world)
                 self._stage_actor_opt(inv_world)
             graphs.append(g)
         else:
             stages = [lambda: self._stage_critic(b),
-                      lambda: (self._stage_actor_fwd(b), self._stage_actor_grad(b, inv_world)),
+                      lambda: self._stage_actor_grad(b, inv_world),
                       lambda: self._stage_actor_opt(inv_world)]
             for fn in stages:
                 g = torch.cuda.CUDAGraph()
@@ -293,10 +330,15 @@ class BatchedTrainer:
         self.schedule = list(network_schedule) if network_schedule else [0]
         self.period = int(period) if period else 0
         self.sim.set_topologies(self.schedule[0])
-        self.obs = self.sim.reset().clone()
+        # acting observations and actions are double-buffered by step parity: with the simulator
+        # overlapped, step t's replay insert runs after step t+1's simulator launch (off the
+        # sim -> act -> sim critical path) and still reads step t's buffers
+        self._obs_bufs = [self.sim.reset().clone(), None]
+        self._obs_bufs[1] = torch.empty_like(self._obs_bufs[0])
         self.topo = self.sim.topo_cur.to(torch.int64).clone()
         self.masks = self.learner.masks
-        self.act_buf = torch.empty(self.E, sim.action_dim, device=self.device)
+        self._act_bufs = [torch.empty(self.E, sim.action_dim, device=self.device) for _ in range(2)]
+        self._pending = None  # (obs, topo, act, out) of the last step, not yet in replay / metrics
         # device-side metric accumulators (read back only when logging)
         self.acc_succ = torch.zeros((), dtype=torch.float64, device=self.device)
         self.acc_drop = torch.zeros((), dtype=torch.float64, device=self.device)
@@ -356,6 +398,42 @@ class BatchedTrainer:
             idx = (nxt // self.period) % len(self.schedule) if self.period else 0
             self.sim.set_topologies(self.schedule[idx])
 
+    @property
+    def obs(self) -> torch.Tensor:
+        """Observation the next step acts on."""
+        return self._obs_bufs[self.global_step & 1]
+
+    @property
+    def act_buf(self) -> torch.Tensor:
+        return self._act_bufs[self.global_step & 1]
+
+    def _record(self, obs, topo, act, out) -> None:
+        """Replay insert + device-side metric accumulation of one finished step."""
+        with trace_range("replay"):
+            self.replay.add(obs, topo, act, out.reward, out.next_obs, out.done)
+        st = out.stats
+        self.acc_succ += st[:, 0].sum()
+        self.acc_drop += st[:, 1].sum()
+        d = out.done.to(torch.float64)
+        self.acc_return += (out.ep_return.to(torch.float64) * d).sum()
+        self.acc_episodes += d.sum()
+
+    def _flush_pending(self) -> None:
+        if self._pending is not None:
+            p, self._pending = self._pending, None
+            self._record(*p)
+
+    def flush(self) -> None:
+        """Complete the deferred replay insert / metrics of the last step (before reading them)."""
+        if self._pending is not None:
+            if self.learn_stream is not None:
+                self.learn_stream.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self.learn_stream):
+                    self._flush_pending()
+                torch.cuda.current_stream(self.device).wait_stream(self.learn_stream)
+            else:
+                self._flush_pending()
+
     def step(self) -> None:
         if self.learn_stream is not None:
             self.learn_stream.wait_stream(torch.cuda.current_stream(self.device))
@@ -367,43 +445,40 @@ class BatchedTrainer:
 
     def _step(self) -> None:
         warm = self.global_step < self.learning_starts
+        k = self.global_step & 1
+        obs, topo = self._obs_bufs[k], self.topo
         with trace_range("act"):
-            mu = self.learner.act(self.obs, self.topo)
+            mu = self.learner.act(obs, topo)
         with trace_range("explore"):
-            act = explore_postprocess(mu, self.masks.index_select(0, self.topo), self.sim.n_pad, warm, self.rand_mu,
+            act = explore_postprocess(mu, self.masks.index_select(0, topo), self.sim.n_pad, warm, self.rand_mu,
                                       self.rand_sigma, seed=self.t.seed * 131 + self.dist.rank,
-                                      step=self.global_step, out=self.act_buf)
+                                      step=self.global_step, out=self._act_bufs[k])
         self._schedule_next()
-        train = self.global_step >= self.learning_starts - 1 and len(self.replay) > 0
+        train = self.global_step >= self.learning_starts - 1 and (len(self.replay) > 0 or self._pending is not None)
         if self.sim_stream is not None and train:
-            # simulator kernel (one wave per env) runs concurrently with the learner update, which
-            # samples transitions already in the replay ring (up to the previous step)
+            # simulator kernel (one wave per env) runs concurrently with the previous step's replay
+            # insert and the learner update, which samples transitions up to the previous step
             main = torch.cuda.current_stream(self.device)
             self.sim_stream.wait_stream(main)
             with torch.cuda.stream(self.sim_stream):
-                out = self.sim.step(act)
+                out = self.sim.step(act, buffer_set=k)
+            self._flush_pending()
             with trace_range("learn"):
                 self._learn()
             main.wait_stream(self.sim_stream)
-            train = False
+            self._pending = (obs, topo, act, out)
         else:
+            self._flush_pending()
             with trace_range("sim"):
-                out = self.sim.step(act)
-        with trace_range("replay"):
-            self.replay.add(self.obs, self.topo, act, out.reward, out.next_obs, out.done)
-        st = out.stats
-        self.acc_succ += st[:, 0].sum()
-        self.acc_drop += st[:, 1].sum()
-        d = out.done.to(torch.float64)
-        self.acc_return += (out.ep_return.to(torch.float64) * d).sum()
-        self.acc_episodes += d.sum()
-        self.obs.copy_(out.obs)
+                out = self.sim.step(act, buffer_set=k)
+            self._record(obs, topo, act, out)
+            if train:
+                with trace_range("learn"):
+                    self._learn()
+        self._obs_bufs[k ^ 1].copy_(out.obs)
         if (self.global_step + 1) % self.sim.episode_steps == 0:
             self.episode += 1
             self.topo = self.sim.topo_next.to(torch.int64).clone()
-        if train:
-            with trace_range("learn"):
-                self._learn()
         self.global_step += 1
         if self.t.check_every and self.global_step % self.t.check_every == 0:
             self.sim.check_flags()
@@ -419,6 +494,7 @@ class BatchedTrainer:
                 self.learner.update(self.replay.sample(self.batch_size))
 
     def metrics(self, reset: bool = True) -> dict:
+        self.flush()
         vals = torch.stack([self.acc_succ, self.acc_drop, self.acc_return, self.acc_episodes])
         allreduce_sum_(vals)
         s, d, r, e = [float(v) for v in vals.cpu()]
@@ -437,6 +513,7 @@ class BatchedTrainer:
                                                                   r.dones))
 
     def state_dict(self, include_replay: bool = True) -> dict:
+        self.flush()
         sd = {"learner": self.learner.state_dict(), "global_step": self.global_step, "episode": self.episode,
               "sim_states": self.sim.states.cpu(), "obs": self.obs.cpu(), "topo": self.topo.cpu(),
               "rng": self.replay.gen.get_state()}
@@ -449,6 +526,7 @@ class BatchedTrainer:
         self.global_step = int(sd["global_step"])
         self.episode = int(sd["episode"])
         self.sim.states.copy_(sd["sim_states"].to(self.device))
+        self._pending = None
         self.obs.copy_(sd["obs"].to(self.device))
         self.topo = sd["topo"].to(self.device)
         if "replay" in sd:

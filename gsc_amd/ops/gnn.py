@@ -74,13 +74,14 @@ class _GnnEmbed(torch.autograd.Function):
         B, P, Fin = x.shape
         grad = torch.empty_like(flat)
         rows = 1024
-        key = (x.device, flat.numel())
+        stream = torch.cuda.current_stream(x.device)
+        key = (x.device, flat.numel(), stream.cuda_stream)  # concurrent branches must not share partials
         partials = _PARTIALS.get(key)
         if partials is None:
             partials = _PARTIALS[key] = torch.empty(rows, flat.numel(), device=x.device, dtype=torch.float32)
         nat.gnn_backward(_tables(ctx.graphs), flat.data_ptr(), x.data_ptr(), topo.data_ptr(),
                          demb.contiguous().float().data_ptr(), partials.data_ptr(), rows, grad.data_ptr(), B, P, Fin,
-                         H, layer_of, torch.cuda.current_stream(x.device).cuda_stream)
+                         H, layer_of, stream.cuda_stream)
         out, off = [], 0
         for s in ctx.shapes:
             n = 1

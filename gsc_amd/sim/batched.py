@@ -207,6 +207,11 @@ class BatchedSimulator:
         self.done = torch.zeros(self.E, dtype=torch.uint8, device=dev)
         self.stats = torch.zeros((self.E, self.native.SIM_NUM_STATS), dtype=torch.float32, device=dev)
         self.ep_return = torch.zeros(self.E, dtype=torch.float32, device=dev)
+        # output buffer sets for step(buffer_set=k): set 0 is the attributes above; set 1 lets a caller
+        # read step t's outputs (replay insert) while step t+1 already writes its own
+        self._out_sets = [(self.obs, self.next_obs, self.reward, self.done, self.stats, self.ep_return),
+                          tuple(torch.zeros_like(t) for t in (self.obs, self.next_obs, self.reward, self.done,
+                                                               self.stats, self.ep_return))]
         self.topo_cur = self.topo_next.clone()
         self.prof = None
 
@@ -231,22 +236,23 @@ class BatchedSimulator:
         """Accumulate per-env cycle counters (event selection / handlers / total / events) in ``self.prof``."""
         self.prof = torch.zeros(self.E * 4 + self.E * 32, dtype=torch.int64, device=self.device) if on else None
 
-    def step(self, actions: torch.Tensor) -> SimStepOut:
+    def step(self, actions: torch.Tensor, buffer_set: int = 0) -> SimStepOut:
         if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
             actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
         if actions.dim() != 2 or actions.shape[0] != self.E or actions.shape[1] < self.action_dim:
             raise ValueError(f"actions must be [E={self.E}, >= {self.action_dim}], got {tuple(actions.shape)}")
+        obs, next_obs, reward, done_u8, stats, ep_return = self._out_sets[buffer_set]
         self.ctx.step(self.states.data_ptr(), self.topo_next.data_ptr(), self.seeds.data_ptr(), actions.data_ptr(),
-                      actions.shape[1], self.obs.data_ptr(), self.next_obs.data_ptr(), self.reward.data_ptr(),
-                      self.done.data_ptr(), self.stats.data_ptr(), self.ep_return.data_ptr(), self.E, self._stream(),
+                      actions.shape[1], obs.data_ptr(), next_obs.data_ptr(), reward.data_ptr(),
+                      done_u8.data_ptr(), stats.data_ptr(), ep_return.data_ptr(), self.E, self._stream(),
                       self.prof.data_ptr() if (self.prof is not None and self.is_device) else 0)
-        done = self.done.bool()
+        done = done_u8.bool()
         # envs that finished were reset onto their scheduled topology
         torch.where(done, self.topo_next, self.topo_cur, out=self.topo_cur)
-        return SimStepOut(self.obs, self.next_obs, self.reward, done, self.stats, self.ep_return)
+        return SimStepOut(obs, next_obs, reward, done, stats, ep_return)
 
     def check_flags(self) -> int:
-        flags = int(self.stats[:, 12].max().item())
+        flags = int(max(t[4][:, 12].max() for t in self._out_sets).item())
         if flags:
             raise RuntimeError(f"batched simulator overflow/bad state flags={flags} (caps {self.dims}); "
                                "increase flow/proc/event capacities")
