@@ -499,6 +499,7 @@ struct ClArgsMirror {
   const void* s_dst;
   const void* s_src;
   int MP;
+  void* blob;
 };
 bool gnn_cl_supported(int Fin, int H, int L, int n_blocks);
 bool gnn_nl_supported(int Fin, int H, int NP, int L);
@@ -510,6 +511,7 @@ int gnn_cl_backward(const void* args, uintptr_t stream, int cus, int max_rows);
 bool gnn_mf_supported(int Fin, int H, int NM, int L, int n_blocks, const int* layer_of);
 void gnn_mf_forward(const void* args, uintptr_t stream, int cus);
 int gnn_mf_backward(const void* args, uintptr_t stream, int cus, int max_rows);
+int gnn_mf_saved_bytes(const void* args);
 
 static unsigned long long* g_gnn_prof = nullptr;  // device buffer of 12 counters, or null
 void gnn_set_profile(uintptr_t p) { g_gnn_prof = reinterpret_cast<unsigned long long*>(p); }
@@ -618,7 +620,7 @@ static void set_lds(const void* fn, size_t lds) {
 }
 
 void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo, uintptr_t emb, int B, int P, int Fin,
-                 int H, std::vector<int> layer_of, uintptr_t stream) {
+                 int H, std::vector<int> layer_of, uintptr_t stream, uintptr_t blob) {
   GnnArgs a = make_args(tables, params, x, topo, B, P, Fin, H, layer_of);
   a.emb = ptr<float>(emb);
   // node-lane forward: forced by path bit 2, and chosen automatically for graphs with >= 32 node
@@ -632,7 +634,9 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
     return;
   }
   if (use_mf(a, tables)) {
-    const ClArgsMirror c = to_cl(a, tables);
+    ClArgsMirror c = to_cl(a, tables);
+    // the saved state is only consumed by the MFMA backward
+    c.blob = blob && use_mf(a, tables, true) ? reinterpret_cast<void*>(blob) : nullptr;
     gnn_mf_forward(&c, stream, num_cus());
     return;
   }
@@ -656,12 +660,13 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
 
 void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo, uintptr_t demb, uintptr_t partials,
                   int max_rows, uintptr_t grad_out, int B, int P, int Fin, int H, std::vector<int> layer_of,
-                  uintptr_t stream) {
+                  uintptr_t stream, uintptr_t blob) {
   GnnArgs a = make_args(tables, params, x, topo, B, P, Fin, H, layer_of);
   a.demb = ptr<const float>(demb);
   a.partials = ptr<float>(partials);
   if (use_mf(a, tables, true) || use_cl(a, true)) {
-    const ClArgsMirror c = to_cl(a, tables);
+    ClArgsMirror c = to_cl(a, tables);
+    c.blob = reinterpret_cast<void*>(blob);
     const int rows = use_mf(a, tables, true) ? gnn_mf_backward(&c, stream, num_cus(), max_rows)
                                      : gnn_cl_backward(&c, stream, num_cus(), max_rows);
     hipLaunchKernelGGL(column_sum_kernel, dim3((a.n_params + 31) / 32), dim3(256), 0, stream_of(stream),
@@ -714,11 +719,24 @@ bool gnn_fused_fits(int M, int NM, int P, int Fin, int H, std::vector<int> layer
   return fwd <= 160 * 1024 && bwd <= 160 * 1024;
 }
 
+// Bytes per graph the grad-requiring forward saves for the MFMA backward (0: that path does not apply).
+int gnn_saved_bytes(py::dict tables, int P, int Fin, int H, std::vector<int> layer_of) {
+  GnnArgs a = make_args(tables, 0, 0, 0, 1, P, Fin, H, layer_of);
+  if (!use_mf(a, tables) || !use_mf(a, tables, true)) return 0;
+  const ClArgsMirror c = to_cl(a, tables);
+  return gnn_mf_saved_bytes(&c);
+}
+
 int gnn_num_params(int Fin, int H, int max_block) { return block_offset(max_block, Fin, H) + block_size(max_block == 0 ? Fin : H, H); }
 
 void register_gnn(py::module_& m) {
-  m.def("gnn_forward", &gnn_forward);
-  m.def("gnn_backward", &gnn_backward);
+  m.def("gnn_forward", &gnn_forward, py::arg("tables"), py::arg("params"), py::arg("x"), py::arg("topo"), py::arg("emb"),
+        py::arg("B"), py::arg("P"), py::arg("Fin"), py::arg("H"), py::arg("layer_of"), py::arg("stream"),
+        py::arg("blob") = 0);
+  m.def("gnn_backward", &gnn_backward, py::arg("tables"), py::arg("params"), py::arg("x"), py::arg("topo"),
+        py::arg("demb"), py::arg("partials"), py::arg("max_rows"), py::arg("grad_out"), py::arg("B"), py::arg("P"),
+        py::arg("Fin"), py::arg("H"), py::arg("layer_of"), py::arg("stream"), py::arg("blob") = 0);
+  m.def("gnn_saved_bytes", &gnn_saved_bytes, "per-graph bytes of the forward state saved for the MFMA backward");
   m.def("gnn_num_params", &gnn_num_params);
   m.def("gnn_fused_fits", &gnn_fused_fits);
   m.def("gnn_set_cu_budget", &gnn_set_cu_budget, "CUs available to GNN launches (0 = whole device)");

@@ -48,6 +48,7 @@ struct ClArgs {
   const void* s_dst;         // MFMA backward: bf16 [T, 32, MP] one-hot target / source of each message
   const void* s_src;
   int MP;                    // messages padded to a multiple of 16
+  void* blob;                // MFMA path: per-graph forward state saved for the backward (or null)
 };
 
 __device__ __forceinline__ void cl_wave_sync() {

@@ -48,6 +48,7 @@ struct MfLayout {  // per-wave LDS offsets (bytes)
   int hR[kClMaxLayers], hT[kClMaxLayers], al[kClMaxLayers];
   int xl, xr, E, mx, sm, dy, U, da, topo, encW, encK, per_wave;
   int hTrows0, hTrows;  // rows of the [k][node] images: encoder input (Fin padded to 4), hidden (HPF)
+  int blob;         // bytes of the per-layer images (hR, hT, alpha of every conv) = saved state per graph
   int NV, NVS, MS;  // node tile (16 | 32), [k][node] image stride, G^T image stride (bf16)
 };
 
@@ -557,7 +558,7 @@ __device__ __forceinline__ void mf_layer_bwd(const ClArgs& a, const MfW* wT, con
   }
 }
 
-template <int HPF, bool K2>
+template <int HPF, bool K2, bool LOADED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void gnn_mf_bwd_kernel(ClArgs a, MfLayout m) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int CG = HPF / 4;
@@ -606,11 +607,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void g
     T.deg = reinterpret_cast<float*>(T.idst + a.M);
     mf_load_topo(T, a, a.topo[g], lane);
     const int n = T.n;
-    mf_load_x<true>(a, g, n, reinterpret_cast<__bf16*>(W + m.hR[0]), reinterpret_cast<__bf16*>(W + m.hT[0]), E, NV,
-                    NVS, lane);
+    if (LOADED) {
+      // the forward saved every conv's input images and alpha: one bulk copy instead of a recompute
+      const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.blob) + (long)g * m.blob);
+      for (int i = lane; i < m.blob / 16; i += 64) reinterpret_cast<uint4*>(W)[i] = src[i];
+      cl_wave_sync();
+    } else {
+      mf_load_x<true>(a, g, n, reinterpret_cast<__bf16*>(W + m.hR[0]), reinterpret_cast<__bf16*>(W + m.hT[0]), E, NV,
+                      NVS, lane);
+    }
     // forward recompute: keep each conv's input (both bf16 images) and alpha; the last conv's
     // output is not needed (its gradient comes from the mean pool)
-    for (int l = 0; l < a.L; ++l) {
+    for (int l = 0; !LOADED && l < a.L; ++l) {
       const float* vec = lds + (l == 0 ? 0 : kMfVec);
       const __bf16* hin = reinterpret_cast<const __bf16*>(W + m.hR[l]);
       float* al = reinterpret_cast<float*>(W + m.al[l]);
@@ -641,7 +649,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void g
       const __bf16* hin = reinterpret_cast<const __bf16*>(W + m.hR[l]);
       const __bf16* hT = reinterpret_cast<const __bf16*>(W + m.hT[l]);
       const float* al = reinterpret_cast<const float*>(W + m.al[l]);
-      if (l + 1 < a.L) {  // x_l / x_r of this conv (the forward loop left the last conv's in place)
+      if (LOADED || l + 1 < a.L) {  // x_l / x_r of this conv (a recompute leaves the last conv's in place)
         f32x16 xa, xb;
         if (l == 0) mf_linear<false>(mf_frags(frags, 0, lane), vec, hin, NV, lane, xa, xb);
         else mf_linear<K2>(mf_frags(frags, 1, lane), vec, hin, NV, lane, xa, xb);
@@ -733,6 +741,67 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void g
   }
 }
 
+// Forward that also saves, per graph, every conv's input images (hR, hT) and alpha in the
+// backward's LDS arrangement (MfLayout::blob bytes), so the MFMA backward loads them instead of
+// recomputing the forward.  Used when the embedder's parameters require gradients.
+template <int HPF, bool K2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gnn_mf_fwd_save_kernel(ClArgs a,
+                                                                                                   MfLayout m) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  mf_stage_vec(a, lds);
+  const bf16x8* frags = reinterpret_cast<const bf16x8*>(lds + mf_vec_floats(a.n_blocks));
+  mf_stage_frags(a, reinterpret_cast<bf16x8*>(lds + mf_vec_floats(a.n_blocks)), 2);
+  __syncthreads();
+  char* const W0 = reinterpret_cast<char*>(lds + mf_vec_floats(a.n_blocks) + 2 * kMfFragSet);
+  int woff = wave * m.per_wave;
+  MfTopo T;
+  mf_bind_topo(T, W0 + woff + m.topo, a);
+  const int half = lane >> 5, c = lane & 31;
+  const int NV = m.NV, NVS = m.NVS;
+  for (int g = blockIdx.x * a.waves + wave; g < a.B; g += gridDim.x * a.waves) {
+    asm volatile("" : "+v"(woff));  // see gnn_mf_bwd_kernel
+    char* W = W0 + woff;
+    float* xl = reinterpret_cast<float*>(W + m.xl);
+    float* xr = reinterpret_cast<float*>(W + m.xr);
+    __bf16* E = reinterpret_cast<__bf16*>(W + m.E);
+    int* mx = reinterpret_cast<int*>(W + m.mx);
+    float* sm = reinterpret_cast<float*>(W + m.sm);
+    T.isrc = reinterpret_cast<int*>(W + m.topo);
+    T.idst = T.isrc + a.M;
+    T.deg = reinterpret_cast<float*>(T.idst + a.M);
+    mf_load_topo(T, a, a.topo[g], lane);
+    const int n = T.n;
+    mf_load_x<true>(a, g, n, reinterpret_cast<__bf16*>(W + m.hR[0]), reinterpret_cast<__bf16*>(W + m.hT[0]), E, NV,
+                    NVS, lane);
+    float pool = 0.f;
+    for (int l = 0; l < a.L; ++l) {
+      const float* vec = lds + (l == 0 ? 0 : kMfVec);
+      const __bf16* hin = reinterpret_cast<const __bf16*>(W + m.hR[l]);
+      float* al = reinterpret_cast<float*>(W + m.al[l]);
+      if (l + 1 < a.L) {
+        __bf16* ho = reinterpret_cast<__bf16*>(W + m.hR[l + 1]);
+        __bf16* hoT = reinterpret_cast<__bf16*>(W + m.hT[l + 1]);
+        if (l == 0)
+          mf_layer<HPF, false, 0, true>(mf_frags(frags, 0, lane), vec, T, hin, xl, xr, al, mx, sm, E, ho, hoT, NV,
+                                        NVS, a.H, lane);
+        else
+          mf_layer<HPF, K2, 0, true>(mf_frags(frags, 1, lane), vec, T, hin, xl, xr, al, mx, sm, E, ho, hoT, NV, NVS,
+                                     a.H, lane);
+      } else {
+        pool = mf_layer<HPF, K2, 1, false>(mf_frags(frags, 1, lane), vec, T, hin, xl, xr, al, mx, sm, E, nullptr,
+                                           nullptr, NV, NVS, a.H, lane);
+      }
+    }
+    pool += __shfl_xor(pool, 32);
+    if (half == 0 && c < a.H) a.emb[(long)g * a.H + c] = pool / (float)n;
+    cl_wave_sync();
+    uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<char*>(a.blob) + (long)g * m.blob);
+    for (int i = lane; i < m.blob / 16; i += 64) dst[i] = reinterpret_cast<const uint4*>(W)[i];
+    cl_wave_sync();
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
@@ -757,6 +826,7 @@ static MfLayout mf_layout(const ClArgs& a, bool bwd, int HPF) {
       m.hT[l] = take((l == 0 ? m.hTrows0 : m.hTrows) * m.NVS * 2);
       m.al[l] = take(M4b);
     }
+    m.blob = o;
     m.dy = take(fb);
     const int gt = HPF * m.MS * 2, dx = 2 * hRb;
     m.U = take(gt > dx ? gt : dx);
@@ -790,18 +860,22 @@ bool gnn_mf_supported(int Fin, int H, int NM, int L, int n_blocks, const int* la
 
 template <int HPF, bool K2>
 static void mf_launch_fwd(ClArgs a, hipStream_t st, int cus) {
-  const MfLayout m = mf_layout(a, false, HPF);
+  const bool save = a.blob != nullptr;
+  const MfLayout m = mf_layout(a, save, HPF);
   a.waves = 4;
   const size_t lds = sizeof(float) * (mf_vec_floats(a.n_blocks) + 2 * kMfFragSet) + (size_t)a.waves * m.per_wave;
   GSC_CHECK(lds <= 160 * 1024, "GNN (MFMA) forward working set exceeds LDS");
-  const void* fn = (const void*)gnn_mf_fwd_kernel<HPF, K2>;
+  const void* fn = save ? (const void*)gnn_mf_fwd_save_kernel<HPF, K2> : (const void*)gnn_mf_fwd_kernel<HPF, K2>;
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = (int)((160 * 1024) / lds);
   if (per_cu > 4) per_cu = 4;  // 4 waves/SIMD (VGPR budget)
   const int need = (a.B + a.waves - 1) / a.waves;
   const int cap = cus * (per_cu > 0 ? per_cu : 1);
   const int grid = need < cap ? need : cap;
-  hipLaunchKernelGGL((gnn_mf_fwd_kernel<HPF, K2>), dim3(grid > 0 ? grid : 1), dim3(64 * a.waves), lds, st, a, m);
+  if (save)
+    hipLaunchKernelGGL((gnn_mf_fwd_save_kernel<HPF, K2>), dim3(grid > 0 ? grid : 1), dim3(64 * a.waves), lds, st, a, m);
+  else
+    hipLaunchKernelGGL((gnn_mf_fwd_kernel<HPF, K2>), dim3(grid > 0 ? grid : 1), dim3(64 * a.waves), lds, st, a, m);
   check_launch();
 }
 
@@ -818,7 +892,8 @@ static int mf_launch_bwd(ClArgs a, hipStream_t st, int cus, int max_rows) {
     a.waves--;
   }
   GSC_CHECK(lds <= 160 * 1024, "GNN (MFMA) backward working set exceeds LDS");
-  const void* fn = (const void*)gnn_mf_bwd_kernel<HPF, K2>;
+  const bool loaded = a.blob != nullptr;
+  const void* fn = loaded ? (const void*)gnn_mf_bwd_kernel<HPF, K2, true> : (const void*)gnn_mf_bwd_kernel<HPF, K2, false>;
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = (int)((160 * 1024) / lds);
   if (per_cu * a.waves > 8) per_cu = 8 / a.waves;  // 2 waves/SIMD (VGPR budget)
@@ -827,7 +902,10 @@ static int mf_launch_bwd(ClArgs a, hipStream_t st, int cus, int max_rows) {
   int grid = need < cap ? need : cap;
   if (grid > max_rows) grid = max_rows;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((gnn_mf_bwd_kernel<HPF, K2>), dim3(grid), dim3(64 * a.waves), lds, st, a, m);
+  if (loaded)
+    hipLaunchKernelGGL((gnn_mf_bwd_kernel<HPF, K2, true>), dim3(grid), dim3(64 * a.waves), lds, st, a, m);
+  else
+    hipLaunchKernelGGL((gnn_mf_bwd_kernel<HPF, K2, false>), dim3(grid), dim3(64 * a.waves), lds, st, a, m);
   check_launch();
   return grid;
 }
@@ -837,6 +915,11 @@ void gnn_mf_forward(const void* args_generic, uintptr_t stream, int cus) {
   if (a.H <= 16) mf_launch_fwd<24, false>(a, stream_of(stream), cus);
   else if (a.H <= 24) mf_launch_fwd<24, true>(a, stream_of(stream), cus);
   else mf_launch_fwd<32, true>(a, stream_of(stream), cus);
+}
+
+int gnn_mf_saved_bytes(const void* args_generic) {
+  const ClArgs& a = *reinterpret_cast<const ClArgs*>(args_generic);
+  return mf_layout(a, true, a.H <= 24 ? 24 : 32).blob;
 }
 
 int gnn_mf_backward(const void* args_generic, uintptr_t stream, int cus, int max_rows) {

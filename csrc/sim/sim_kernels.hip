@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -44,6 +45,7 @@ struct SimArgs {
   int use_lds;
   long topo_stage;           // bytes of LDS reserved for the staged topology tables
   unsigned long long* prof;  // optional [E, 4] cycle counters: select, dispatch, merge, events (diagnostic)
+  int prio;                  // wave priority of the step kernel (s_setprio), see sim_step_kernel
   unsigned long long* prof_types;  // optional [E, 16, 2] dispatch cycles / count per process type
 };
 
@@ -329,6 +331,12 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int env = blockIdx.x;
   const int lane = threadIdx.x;
+  // The simulator step is the training loop's critical path (issue-bound, one wave per env) while
+  // the learner runs concurrently with slack: give its waves issue priority over co-resident
+  // learner waves on the same SIMD (GSC_SIM_PRIO, default 3; measured +0.6 %).
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
   // [SimConst][topology tables][state blob (LDS mode)]
   SimConst* Ks = reinterpret_cast<SimConst*>(smem);
   if (lane == 0) *Ks = a.K;
@@ -477,6 +485,8 @@ class SimContext {
                      ep_return, E);
     a.prof = ptr<unsigned long long>(prof);
     a.prof_types = prof ? ptr<unsigned long long>(prof) + (long)E * 4 : nullptr;
+    static const int prio = getenv("GSC_SIM_PRIO") ? atoi(getenv("GSC_SIM_PRIO")) : 3;
+    a.prio = prio;
     if (device_) {
       const size_t lds = const_stage_bytes() + topo_stage_ + (use_lds_ ? (size_t)L_.total : 0);
       const hipStream_t st = stream_of(stream);

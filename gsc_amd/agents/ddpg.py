@@ -37,6 +37,9 @@ from gsc_amd.utils.tracing import trace_range
 from .replay import Batch, DeviceReplay
 
 
+_DIAG_NO_LEARN = os.environ.get("GSC_DIAG_NO_LEARN", "0") == "1"
+
+
 class DDPGLearner:
     def __init__(self, cfg: dict, obs_dim: int, action_dim: int, graphs: GraphSet, C: int, F_: int, device,
                  dist_info: Optional[DistInfo] = None, amp_bf16: Optional[bool] = None, seed: int = 0):
@@ -484,6 +487,8 @@ class BatchedTrainer:
             self.sim.check_flags()
 
     def _learn(self) -> None:
+        if _DIAG_NO_LEARN:  # diagnostics only (never in bench numbers): measures the act + sim chain alone
+            return
         for _ in range(self.t.updates_per_step):
             if self.graphed:
                 if self._batch is None:

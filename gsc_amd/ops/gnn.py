@@ -1,6 +1,7 @@
 """Autograd wrapper around the fused HIP GATv2 embedder kernels (``csrc/ops/gnn.hip``)."""
 from __future__ import annotations
 
+import os
 from typing import List
 
 import torch
@@ -46,6 +47,8 @@ def _flat(params: List[torch.Tensor]) -> torch.Tensor:
 
 
 _PARTIALS = {}
+# GSC_GNN_SAVE=0: the backward recomputes the forward instead of loading its saved state
+_NO_SAVE = os.environ.get("GSC_GNN_SAVE", "1") == "0"
 
 
 class _GnnEmbed(torch.autograd.Function):
@@ -53,15 +56,21 @@ class _GnnEmbed(torch.autograd.Function):
     def forward(ctx, x, topo, graphs, meta, *params):
         nat = load_native()
         B, P, Fin = x.shape
-        H, layer_of = meta
+        H, layer_of, grad_mode = meta
         flat = _flat(list(params))
         x = x.contiguous().float()
         topo = topo.to(torch.int32).contiguous()
         emb = torch.empty(B, H, device=x.device, dtype=torch.float32)
+        # grad-requiring forward: save the per-layer state for the backward (MFMA path) instead of
+        # having it recompute the forward
+        nbytes = 0 if _NO_SAVE else nat.gnn_saved_bytes(_tables(graphs), P, Fin, H, layer_of) if grad_mode and any(ctx.needs_input_grad[4:]) \
+            else 0
+        blob = torch.empty(B * nbytes if B > 0 else 0, device=x.device, dtype=torch.uint8)
         if B > 0:
             nat.gnn_forward(_tables(graphs), flat.data_ptr(), x.data_ptr(), topo.data_ptr(), emb.data_ptr(), B, P, Fin,
-                            H, layer_of, torch.cuda.current_stream(x.device).cuda_stream)
-        ctx.save_for_backward(x, topo, flat)
+                            H, layer_of, torch.cuda.current_stream(x.device).cuda_stream,
+                            blob.data_ptr() if blob.numel() else 0)
+        ctx.save_for_backward(x, topo, flat, blob)
         ctx.graphs, ctx.meta = graphs, meta
         ctx.shapes = [p.shape for p in params]
         return emb
@@ -69,8 +78,8 @@ class _GnnEmbed(torch.autograd.Function):
     @staticmethod
     def backward(ctx, demb):
         nat = load_native()
-        x, topo, flat = ctx.saved_tensors
-        H, layer_of = ctx.meta
+        x, topo, flat, blob = ctx.saved_tensors
+        H, layer_of, _ = ctx.meta
         B, P, Fin = x.shape
         grad = torch.empty_like(flat)
         rows = 1024
@@ -81,7 +90,7 @@ class _GnnEmbed(torch.autograd.Function):
             partials = _PARTIALS[key] = torch.empty(rows, flat.numel(), device=x.device, dtype=torch.float32)
         nat.gnn_backward(_tables(ctx.graphs), flat.data_ptr(), x.data_ptr(), topo.data_ptr(),
                          demb.contiguous().float().data_ptr(), partials.data_ptr(), rows, grad.data_ptr(), B, P, Fin,
-                         H, layer_of, stream.cuda_stream)
+                         H, layer_of, stream.cuda_stream, blob.data_ptr() if blob.numel() else 0)
         out, off = [], 0
         for s in ctx.shapes:
             n = 1
@@ -104,4 +113,4 @@ def gnn_fits(embedder, graphs, P: int, Fin: int) -> bool:
 
 def gnn_embed(embedder, x: torch.Tensor, topo: torch.Tensor, graphs) -> torch.Tensor:
     params = embedder.flat_parameters()
-    return _GnnEmbed.apply(x, topo, graphs, (embedder.hidden_dim, _layer_of(embedder)), *params)
+    return _GnnEmbed.apply(x, topo, graphs, (embedder.hidden_dim, _layer_of(embedder), torch.is_grad_enabled()), *params)
