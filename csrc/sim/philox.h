@@ -15,6 +15,16 @@
 #define GSC_HD_CALL inline
 #endif
 
+// Wave-uniform hint for handler control values (type, state, indices, branch conditions): the
+// device handlers run in one lane, so every loaded value is technically per-lane; reading it back
+// through readfirstlane puts it in an SGPR, which turns the exec-mask branch trees of a VGPR
+// switch into scalar branches and moves index arithmetic to the scalar ALU.  Identity on the host.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GSC_UNI(x) __builtin_amdgcn_readfirstlane((int)(x))
+#else
+#define GSC_UNI(x) ((int)(x))
+#endif
+
 namespace gsc {
 
 struct Philox4 {

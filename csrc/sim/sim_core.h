@@ -246,7 +246,7 @@ GSC_HD void timeout(Env& S, int pid, double delay) { push_event(S, S.h->now + de
 GSC_HD int alloc_proc(Env& S, uint8_t type, uint8_t state, int flow, int parent) {
   Header* h = S.h;
   if (h->proc_top <= 0) { h->flags |= FLAG_PROC_OVERFLOW; return -1; }
-  const int pid = S.proc_free[--h->proc_top];
+  const int pid = GSC_UNI(S.proc_free[--h->proc_top]);
   Proc& p = S.procs[pid];
   p.type = type; p.state = state; p.flow = (int16_t)flow; p.parent = (int16_t)parent;
   p.a = p.b = p.c = p.ret = 0; p.x = p.y = 0.0;
@@ -268,7 +268,7 @@ GSC_HD void respawn_self(Env& S, int pid, uint8_t state) {
 }
 // Generator return: completion event (NORMAL, delay 0); resumes the waiting parent if any.
 GSC_HD void proc_return(Env& S, int pid, int16_t value) {
-  const int parent = S.procs[pid].parent;
+  const int parent = GSC_UNI(S.procs[pid].parent);
   if (parent >= 0) {
     S.procs[parent].ret = value;
     push_event(S, S.h->now, 1u, (int16_t)parent);
@@ -282,7 +282,7 @@ GSC_HD void proc_return(Env& S, int pid, int16_t value) {
 GSC_HD int alloc_flow(Env& S) {
   Header* h = S.h;
   if (h->flow_top <= 0) { h->flags |= FLAG_FLOW_OVERFLOW; return -1; }
-  const int fid = S.flow_free[--h->flow_top];
+  const int fid = GSC_UNI(S.flow_free[--h->flow_top]);
   const int used = S.d.flow_cap - h->flow_top;
   if (used > h->max_flows) h->max_flows = used;
   return fid;
@@ -352,13 +352,13 @@ GSC_HD void end_flow(Env& S, int pid, int fid) {
 // FlowSimulator.handle_flow (flowsimulator.py:72-128)
 GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid) {
   const Proc P = S.procs[pid];
-  const int fid = P.flow;
+  const int fid = GSC_UNI(P.flow);
   Flow f = S.flows[fid];
-  uint8_t state = P.state;
+  int state = GSC_UNI(P.state);
   for (;;) {
     switch (state) {
       case H_LOOP:
-        if (f.departed) {
+        if (GSC_UNI(f.departed)) {
           completed_flow(S, f);
           end_flow(S, pid, fid);
           return;
@@ -367,7 +367,7 @@ GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid
         spawn(S, P_DECIDE, D_INIT, fid, pid);
         return;
       case H_AFTER_DECIDE: {
-        const int nxt = P.ret;
+        const int nxt = GSC_UNI(P.ret);
         if (nxt < 0) { dropped_flow(S, f, R_DECISION); end_flow(S, pid, fid); return; }
         S.procs[pid].state = H_AFTER_FWD;
         const int c = spawn(S, P_FORWARD, F_INIT, fid, pid);
@@ -375,8 +375,8 @@ GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid
         return;
       }
       case H_AFTER_FWD:
-        if (!P.ret) { dropped_flow(S, f, R_LINK); end_flow(S, pid, fid); return; }
-        if (!f.fwd_eg) {
+        if (!GSC_UNI(P.ret)) { dropped_flow(S, f, R_LINK); end_flow(S, pid, fid); return; }
+        if (!GSC_UNI(f.fwd_eg)) {
           S.procs[pid].state = H_AFTER_PROC;
           spawn(S, P_PROCESS, PR_INIT, fid, pid);
           return;
@@ -384,7 +384,7 @@ GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid
         state = H_LOOP;
         break;
       case H_AFTER_PROC:
-        if (!P.ret) { dropped_flow(S, f, R_NODE); end_flow(S, pid, fid); return; }
+        if (!GSC_UNI(P.ret)) { dropped_flow(S, f, R_NODE); end_flow(S, pid, fid); return; }
         state = H_LOOP;
         break;
       default:
@@ -398,23 +398,26 @@ GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid
 // DefaultDecisionMaker.decide_next_node (default_decision_maker.py:18-81): weighted round robin.
 GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid) {
   const Proc P = S.procs[pid];
-  if (P.state == D_INIT) {
+  if (GSC_UNI(P.state) == D_INIT) {
     S.procs[pid].state = D_RUN;
     timeout(S, pid, 0.0);
     return;
   }
-  Flow f = S.flows[P.flow];
-  if (f.ttl <= 0) { proc_return(S, pid, -1); return; }
-  if (f.fwd_eg) {
-    if (f.egress < 0) S.flows[P.flow].egress = f.node;
-    proc_return(S, pid, f.egress < 0 ? f.node : f.egress);
+  const int fid = GSC_UNI(P.flow);
+  Flow f = S.flows[fid];
+  if (GSC_UNI(f.ttl <= 0)) { proc_return(S, pid, -1); return; }
+  if (GSC_UNI(f.fwd_eg)) {
+    const int eg = GSC_UNI(f.egress), node = GSC_UNI(f.node);
+    if (eg < 0) S.flows[fid].egress = (int16_t)node;
+    proc_return(S, pid, (int16_t)(eg < 0 ? node : eg));
     return;
   }
-  const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
-  const int sf = K.chain[f.sfc * kMaxF + f.pos];
-  S.flows[P.flow].cur_sf = (int16_t)sf;
-  S.requested[(f.node * C + f.sfc) * Sd + sf] += f.dr;
-  const int row = ((f.node * C + f.sfc) * Sd + sf) * N;
+  const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = GSC_UNI(T.n);
+  const int node = GSC_UNI(f.node), sfc = GSC_UNI(f.sfc);
+  const int sf = GSC_UNI(K.chain[sfc * kMaxF + GSC_UNI(f.pos)]);
+  S.flows[fid].cur_sf = (int16_t)sf;
+  S.requested[(node * C + sfc) * Sd + sf] += f.dr;
+  const int row = ((node * C + sfc) * Sd + sf) * N;
   const double* p = S.sched + row;
   int32_t* cnt = S.wrr + row;
   int total = 0;
@@ -427,6 +430,7 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
     const double diff = p[d] > 0 ? p[d] - ratio : -1.0;
     if (diff > best_v) { best_v = diff; best = d; }
   }
+  best = GSC_UNI(best);
   cnt[best]++;
   proc_return(S, pid, (int16_t)best);
 }
@@ -434,27 +438,28 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
 // DefaultFlowForwarder.forward_flow (default_forwarder.py:21-90) + return_link_resources.
 GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid) {
   Proc P = S.procs[pid];
-  const int fid = P.flow;
+  const int fid = GSC_UNI(P.flow);
   Flow f = S.flows[fid];
-  const int n = T.n;
-  const int nxt = P.b;
-  if (P.state == F_INIT) {
-    const int cur = f.node;
+  const int n = GSC_UNI(T.n);
+  const int nxt = GSC_UNI(P.b);
+  if (GSC_UNI(P.state) == F_INIT) {
+    const int cur = GSC_UNI(f.node);
     const double pd = (cur != nxt) ? T.pdelay[cur * n + nxt] : 0.0;
-    if (f.ttl - pd <= 0) { S.flows[fid].ttl = 0; proc_return(S, pid, 0); return; }
-    if (cur == f.egress && f.fwd_eg) { f.departed = 1; S.flows[fid].departed = 1; }
+    if (GSC_UNI(f.ttl - pd <= 0)) { S.flows[fid].ttl = 0; proc_return(S, pid, 0); return; }
+    if (GSC_UNI(cur == f.egress && f.fwd_eg)) { f.departed = 1; S.flows[fid].departed = 1; }
     if (cur == nxt) { proc_return(S, pid, 1); return; }
     P.a = (int16_t)cur;
     P.c = 0;
     P.x = pd;
   } else {  // F_AFTER_HOP
-    const int hop = T.pnodes[(P.a * n + nxt) * T.H + P.c];
-    const int e = T.edge_id[f.node * n + hop];
+    const int pa = GSC_UNI(P.a), pc = GSC_UNI(P.c);
+    const int hop = GSC_UNI(T.pnodes[(pa * n + nxt) * T.H + pc]);
+    const int e = GSC_UNI(T.edge_id[GSC_UNI(f.node) * n + hop]);
     const int c = spawn(S, P_RETLINK, RL_INIT, -1, -1);
     if (c >= 0) { S.procs[c].a = (int16_t)e; S.procs[c].x = f.dr; S.procs[c].y = f.duration; }
     f.node = (int16_t)hop;
-    P.c++;
-    if (P.c >= T.plen[P.a * n + nxt]) {
+    P.c = (int16_t)(pc + 1);
+    if (GSC_UNI(pc + 1 >= T.plen[pa * n + nxt])) {
       add_path_delay(S, P.x);
       f.e2e += P.x;
       f.ttl -= P.x;
@@ -467,13 +472,13 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
     }
   }
   // next hop
-  const int hop = T.pnodes[(P.a * n + nxt) * T.H + P.c];
-  const int cur = f.node;
-  const int e = T.edge_id[cur * n + hop];
+  const int hop = GSC_UNI(T.pnodes[(GSC_UNI(P.a) * n + nxt) * T.H + GSC_UNI(P.c)]);
+  const int cur = GSC_UNI(f.node);
+  const int e = GSC_UNI(T.edge_id[cur * n + hop]);
   Flow& fm = S.flows[fid];
   fm.node = f.node;
   const double lrem = S.link_rem[e];
-  if (lrem - f.dr >= 0) {
+  if (GSC_UNI(lrem - f.dr >= 0)) {
     S.link_rem[e] = lrem - f.dr;
   } else {
     proc_return(S, pid, 0);
@@ -481,7 +486,7 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
   }
   S.link_passed[e] += f.dr;
   const double hd = T.pdelay[cur * n + hop];
-  if (hop == f.egress && f.fwd_eg) fm.departed = 1;
+  if (GSC_UNI(hop == f.egress && f.fwd_eg)) fm.departed = 1;
   P.state = F_AFTER_HOP;
   S.procs[pid] = P;
   timeout(S, pid, hd);
@@ -490,34 +495,35 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
 
 GSC_HD_CALL void run_retlink(Env& S, int pid) {
   const Proc P = S.procs[pid];
-  if (P.state == RL_INIT) {
+  if (GSC_UNI(P.state) == RL_INIT) {
     S.procs[pid].state = RL_AFTER;
     timeout(S, pid, P.y);
     return;
   }
-  S.link_rem[P.a] += P.x;
+  S.link_rem[GSC_UNI(P.a)] += P.x;
   proc_return(S, pid, 0);
 }
 
 // DefaultFlowProcessor.process_flow (default_processor.py:14-50) + get_processing_delay.
 GSC_HD_CALL void run_process(Env& S, const SimConst& K, const TopoDev& T, int pid) {
   Proc P = S.procs[pid];
-  const int fid = P.flow;
+  const int fid = GSC_UNI(P.flow);
   const int Sd = S.d.S;
-  if (P.state == PR_INIT) {
+  const int pstate = GSC_UNI(P.state);
+  if (pstate == PR_INIT) {
     Flow f = S.flows[fid];
-    const int node = f.node;
-    const int sf = K.chain[f.sfc * kMaxF + f.pos];
+    const int node = GSC_UNI(f.node);
+    const int sf = GSC_UNI(K.chain[GSC_UNI(f.sfc) * kMaxF + GSC_UNI(f.pos)]);
     Flow& fm = S.flows[fid];
     fm.cur_sf = (int16_t)sf;
-    if (!S.placement[node * Sd + sf]) { proc_return(S, pid, 0); return; }
+    if (!GSC_UNI(S.placement[node * Sd + sf])) { proc_return(S, pid, 0); return; }
     const double pd = fabs(rng_normal(S, K.pd_mean[sf], K.pd_std[sf]));
-    if (f.ttl - pd <= 0) { fm.ttl = 0; proc_return(S, pid, 0); return; }
+    if (GSC_UNI(f.ttl - pd <= 0)) { fm.ttl = 0; proc_return(S, pid, 0); return; }
     S.h->num_proc_delays++;
     S.h->total_proc_delay += pd;
     fm.e2e = f.e2e + pd;
     fm.ttl = f.ttl - pd;
-    if (pd == 0.0) { proc_return(S, pid, 0); return; }  // reference: `if not processing_delay`
+    if (GSC_UNI(pd == 0.0)) { proc_return(S, pid, 0); return; }  // reference: `if not processing_delay`
     P.x = pd;
     P.a = (int16_t)node;
     P.b = (int16_t)sf;
@@ -527,8 +533,8 @@ GSC_HD_CALL void run_process(Env& S, const SimConst& K, const TopoDev& T, int pi
     if (c >= 0) { S.procs[c].a = (int16_t)node; S.procs[c].b = (int16_t)sf; }
     return;
   }
-  if (P.state == PR_AFTER_REQ) {
-    if (!P.ret) { proc_return(S, pid, 0); return; }
+  if (pstate == PR_AFTER_REQ) {
+    if (!GSC_UNI(P.ret)) { proc_return(S, pid, 0); return; }
     S.procs[pid].state = PR_AFTER_WAIT;
     timeout(S, pid, P.x);
     return;
@@ -543,24 +549,25 @@ GSC_HD_CALL void run_process(Env& S, const SimConst& K, const TopoDev& T, int pi
 // BaseFlowProcessor.request_resources (base_processor.py:51-101).
 GSC_HD_CALL void run_request(Env& S, const SimConst& K, int pid) {
   const Proc P = S.procs[pid];
-  if (P.state == RQ_AFTER) { proc_return(S, pid, 1); return; }
-  Flow f = S.flows[P.flow];
-  const int node = P.a, sf = P.b, Sd = S.d.S;
+  if (GSC_UNI(P.state) == RQ_AFTER) { proc_return(S, pid, 1); return; }
+  const int fid = GSC_UNI(P.flow);
+  Flow f = S.flows[fid];
+  const int node = GSC_UNI(P.a), sf = GSC_UNI(P.b), Sd = S.d.S;
   double demanded = 0.0;
   for (int s = 0; s < Sd; ++s)
-    if (S.sf_present[node * Sd + s]) demanded += S.sf_load[node * Sd + s] + (s == sf ? f.dr : 0.0);
+    if (GSC_UNI(S.sf_present[node * Sd + s])) demanded += S.sf_load[node * Sd + s] + (s == sf ? f.dr : 0.0);
   const double cap = S.node_cap[node];
-  if (!(demanded <= cap)) { proc_return(S, pid, 0); return; }
-  Flow& fm = S.flows[P.flow];
+  if (GSC_UNI(!(demanded <= cap))) { proc_return(S, pid, 0); return; }
+  Flow& fm = S.flows[fid];
   fm.proc_idx = f.proc_idx + 1;
   S.proc_traffic[node * Sd + sf] += f.dr;
   S.sf_load[node * Sd + sf] += f.dr;
   S.node_rem[node] = cap - demanded;
   if (demanded > S.max_usage[node]) S.max_usage[node] = demanded;
   const double ready = S.sf_start[node * Sd + sf] + K.startup[sf];
-  if (!(ready <= S.h->now)) {
+  if (GSC_UNI(!(ready <= S.h->now))) {
     const double rem = ready - S.h->now;
-    if (f.ttl - rem <= 0) { fm.ttl = 0; proc_return(S, pid, 0); return; }
+    if (GSC_UNI(f.ttl - rem <= 0)) { fm.ttl = 0; proc_return(S, pid, 0); return; }
     fm.e2e = f.e2e + rem;
     fm.ttl = f.ttl - rem;
     S.procs[pid].state = RQ_AFTER;
@@ -574,34 +581,35 @@ GSC_HD_CALL void run_request(Env& S, const SimConst& K, int pid) {
 GSC_HD_CALL void run_finish(Env& S, const SimConst& K, int pid) {
   const Proc P = S.procs[pid];
   const int Sd = S.d.S;
-  if (P.state == FI_INIT) {
-    const Flow f = S.flows[P.flow];
-    Flow& fm = S.flows[P.flow];
-    const int pos = f.pos + 1;
+  if (GSC_UNI(P.state) == FI_INIT) {
+    const int fid = GSC_UNI(P.flow);
+    const Flow f = S.flows[fid];
+    Flow& fm = S.flows[fid];
+    const int pos = GSC_UNI(f.pos) + 1;
     fm.pos = (int16_t)pos;
-    if (pos == K.chain_len[f.sfc]) fm.fwd_eg = 1;
+    if (pos == GSC_UNI(K.chain_len[GSC_UNI(f.sfc)])) fm.fwd_eg = 1;
     Proc& pm = S.procs[pid];
     pm.x = f.dr;
     pm.state = FI_AFTER;
     timeout(S, pid, f.duration);
     return;
   }
-  const int node = P.a, sf = P.b;
+  const int node = GSC_UNI(P.a), sf = GSC_UNI(P.b);
   const double load = S.sf_load[node * Sd + sf] - P.x;
   S.sf_load[node * Sd + sf] = load;
-  if (load == 0.0 && !S.placement[node * Sd + sf]) S.sf_present[node * Sd + sf] = 0;
+  if (GSC_UNI(load == 0.0 && !S.placement[node * Sd + sf])) S.sf_present[node * Sd + sf] = 0;
   double used = 0.0;
   for (int s = 0; s < Sd; ++s)
-    if (S.sf_present[node * Sd + s]) used += S.sf_load[node * Sd + s];
+    if (GSC_UNI(S.sf_present[node * Sd + s])) used += S.sf_load[node * Sd + s];
   S.node_rem[node] = S.node_cap[node] - used;
   proc_return(S, pid, 0);
 }
 
 // FlowSimulator.init_arrival + DefaultFlowGenerator.generate_flow.
 GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  const int node = S.procs[pid].a;
+  const int node = GSC_UNI(S.procs[pid].a);
   const double mean = S.inter_arr[node];
-  if (mean != mean) { proc_return(S, pid, 0); return; }  // None: arrivals at this node stop
+  if (GSC_UNI(mean != mean)) { proc_return(S, pid, 0); return; }  // None: arrivals at this node stop
   Header* h = S.h;
   h->total_flow_count++;
   const double inter = K.det_arrival ? mean : -log(1.0 - rng_u01(S)) * mean;
@@ -609,7 +617,7 @@ GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pi
   for (;;) {
     dr = rng_normal(S, K.dr_mean, K.dr_std);
     size = K.det_size ? K.size_shape : exp(-log(1.0 - rng_u01(S)) / K.size_shape);  // pareto(a) + 1
-    if (dr >= 0.0 && size >= 0.0) break;
+    if (GSC_UNI(dr >= 0.0 && size >= 0.0)) break;
   }
   const int sfc = rng_int(S, K.C);
   const int eg = T.n_eg > 0 ? T.egress[rng_int(S, T.n_eg)] : -1;
@@ -643,7 +651,7 @@ GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pi
 
 // ResultWriter.begin_writing / write_network_state: the run-window clock.
 GSC_HD_CALL void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  switch (S.procs[pid].state) {
+  switch (GSC_UNI(S.procs[pid].state)) {
     case W_BEGIN:
     case W_AFTER:
       respawn_self(S, pid, W_INIT);
@@ -713,7 +721,7 @@ GSC_HD_CALL void run_trace(Env& S, const SimConst& K, const TopoDev& T, int pid)
 }
 
 GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  switch (S.procs[pid].type) {
+  switch (GSC_UNI(S.procs[pid].type)) {
     case P_HANDLE: run_handle(S, K, T, pid); break;
     case P_DECIDE: run_decide(S, K, T, pid); break;
     case P_FORWARD: run_forward(S, K, T, pid); break;

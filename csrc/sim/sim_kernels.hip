@@ -88,6 +88,31 @@ __device__ __forceinline__ void copy16(char* dst, const char* src, long bytes, i
   for (long i = lane; i < n16; i += 64) reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(src)[i];
 }
 
+// write_obs with one node per lane: per-feature max by a wave butterfly (max is exact, so the
+// values equal the serial host loop's), and optionally a second copy of the same observation.
+__device__ __forceinline__ void write_obs_wave(const Env& S, const SimConst& K, int n, float* obs, float* obs2,
+                                               int lane) {
+  for (int j = 0; j < K.n_obs; ++j) {
+    const int q = K.obs_feat[j];
+    float mx = -__builtin_inff();
+    for (int v = lane; v < n; v += 64) {
+      const float x = obs_feature(S, K, q, v);
+      mx = x > mx ? x : mx;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const float o = __shfl_xor(mx, off);
+      mx = o > mx ? o : mx;
+    }
+    const float den = mx + 1e-3f;
+    for (int v = lane; v < K.n_pad; v += 64) {
+      const float y = v < n ? clip01(obs_feature(S, K, q, v) / den) : 0.f;
+      obs[v * K.n_obs + j] = y;
+      if (obs2) obs2[v * K.n_obs + j] = y;
+    }
+  }
+}
+
 __device__ __forceinline__ int argmin_event_wave(const Env& S, int lane) {
   // the header copy is authoritative in lane 0 (the only lane that runs handlers)
   const int ne = __builtin_amdgcn_readfirstlane(S.h->n_events);
@@ -274,12 +299,44 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
       if (lane == 0) S.h->now = et;
       break;
     }
-    int ptype = 0;
+    // Lane 0 runs the handler, then keeps going while the smallest event the handler chain just
+    // scheduled precedes the queue head (lane 0 holds the head: entry 0 of set 0): those events
+    // -- process initialisations, completions and zero-delay timeouts at `now` -- are dispatched
+    // straight from the inbox without a round trip through the register queue.  Popping the
+    // minimum of (queue U inbox) is exactly the full queue's order.
+    int n_disp = 0;
     if (lane == 0) {
-      S.h->now = et;
-      if (prof) ptype = S.procs[ep].type;
-      dispatch(S, K, T, ep);
+      double t = et;
+      int p = ep;
+      const double head_t = pack_t(q.tlo[0], q.thi[0]);
+      const uint32_t head_k = q.key[0];
+      for (;;) {
+        S.h->now = t;
+        const unsigned long long td = prof ? __builtin_amdgcn_s_memtime() : 0;
+        const int ptype = prof ? S.procs[p].type : 0;
+        dispatch(S, K, T, p);
+        ++n_disp;
+        if (a.prof_types) {
+          a.prof_types[((long)env * 16 + ptype) * 2] += __builtin_amdgcn_s_memtime() - td;
+          a.prof_types[((long)env * 16 + ptype) * 2 + 1] += 1;
+        }
+        const int ni = S.h->n_events;
+        // pending-event high-water mark of the full queue (= host path's count after its last push)
+        if (q.n + ni > S.h->max_events) S.h->max_events = q.n + ni;
+        if (ni == 0 || n_disp >= 4096) break;
+        int bi = 0;
+        Event m = S.events[0];
+        for (int i = 1; i < ni; ++i) {
+          const Event c = S.events[i];
+          if (ev_less(c, m)) { m = c; bi = i; }
+        }
+        if (!(m.t < head_t || (m.t == head_t && m.key < head_k))) break;
+        remove_event(S, bi);
+        t = m.t;
+        p = m.proc;
+      }
     }
+    it += __builtin_amdgcn_readfirstlane(n_disp) - 1;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -290,11 +347,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
       t_sel += t1 - t0;
       t_hdl += t2 - t1;
       t_mrg += t3 - t2;
-      n_ev++;
-      if (a.prof_types && lane == 0) {
-        a.prof_types[((long)env * 16 + ptype) * 2] += t2 - t1;
-        a.prof_types[((long)env * 16 + ptype) * 2 + 1] += 1;
-      }
+      n_ev += __builtin_amdgcn_readfirstlane(n_disp);
     }
   }
   if (prof && lane == 0) {
@@ -319,10 +372,32 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   }
   if (lane == 0) S.h->n_events = q.n;
   __syncthreads();
+  // epilogue: reward/stats in lane 0, observations lane-parallel (they read only LDS state)
+  const long ostride = (long)K.n_pad * K.n_obs;
+  int done = 0;
   if (lane == 0) {
-    step_epilogue(S, a, K, env);  // on episode end env_init rebuilds S.events / n_events itself
-    *h_mem = h_reg;
+    S.h->run_times++;
+    const float r = compute_reward(S, K, T);
+    write_stats(S, a.stats + (long)env * kNumStats);
+    a.reward[env] = r;
+    S.h->episode_return += r;
+    S.h->run_count++;
+    done = S.h->run_count >= K.episode_steps;
+    a.done[env] = (uint8_t)done;
+    if (done) a.ep_return[env] = (float)S.h->episode_return;
   }
+  done = __builtin_amdgcn_readfirstlane(done);
+  write_obs_wave(S, K, T.n, a.next_obs + env * ostride, done ? nullptr : a.obs + env * ostride, lane);
+  if (done) {
+    __syncthreads();
+    if (lane == 0) {
+      const int topo = a.topo_next[env];
+      env_init(S, K, a.topos[topo], topo, a.seeds[env], S.h->episode + 1);
+    }
+    __syncthreads();
+    write_obs_wave(S, K, a.topos[a.topo_next[env]].n, a.obs + env * ostride, nullptr, lane);
+  }
+  if (lane == 0) *h_mem = h_reg;
   __syncthreads();
 }
 
