@@ -5,11 +5,13 @@ namespace gsc {
 void register_explore(py::module_& m);
 void register_gnn(py::module_& m);
 void register_optim(py::module_& m);
+void register_mlp(py::module_& m);
 void register_streams(py::module_& m);
 void register_ops(py::module_& m) {
   register_explore(m);
   register_gnn(m);
   register_optim(m);
+  register_mlp(m);
   register_streams(m);
 }
 }  // namespace gsc

@@ -146,21 +146,26 @@ __global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict_
     bad |= !isfinite(g[i]);
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
-__global__ void nonfinite_count_kernel(int* flag) { flag[1] += flag[0] ? 1 : 0; }
+// flagged steps counter; optionally advances the device Adam step counter unless the step is skipped
+__global__ void nonfinite_count_kernel(int* flag, long long* step) {
+  flag[1] += flag[0] ? 1 : 0;
+  if (step && !flag[0]) *step += 1;
+}
 
-void grad_guard(uintptr_t g, long n, uintptr_t flag, uintptr_t stream) {
+void grad_guard(uintptr_t g, long n, uintptr_t flag, uintptr_t stream, uintptr_t step) {
   hipStream_t st = stream_of(stream);
   GSC_HIP_CHECK(hipMemsetAsync(ptr<int>(flag), 0, sizeof(int), st));
   long grid = (n + 255) / 256;
   if (grid > 1024) grid = 1024;
   hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)(grid > 0 ? grid : 1)), dim3(256), 0, st, ptr<const float>(g), n,
                      ptr<int>(flag));
-  hipLaunchKernelGGL(nonfinite_count_kernel, dim3(1), dim3(1), 0, st, ptr<int>(flag));
+  hipLaunchKernelGGL(nonfinite_count_kernel, dim3(1), dim3(1), 0, st, ptr<int>(flag), ptr<long long>(step));
   check_launch();
 }
 
 void register_optim(py::module_& m) {
-  m.def("grad_guard", &grad_guard, "flag[0] = any non-finite gradient; flag[1] counts flagged steps");
+  m.def("grad_guard", &grad_guard, "flag[0] = any non-finite gradient; flag[1] counts flagged steps; step += !flag[0]",
+        py::arg("g"), py::arg("n"), py::arg("flag"), py::arg("stream"), py::arg("step") = 0);
   m.def("adam_polyak", &adam_polyak, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("target"),
         py::arg("n"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("step"), py::arg("tau"),
         py::arg("grad_scale"), py::arg("weight_decay"), py::arg("stream"), py::arg("step_ptr") = 0,

@@ -81,6 +81,11 @@ class DDPGLearner:
         self._a = None
         # GSC_COMPOSE=0 forces the materialised critic(obs, actor(obs)) path (A/B checks)
         self.compose_actor_critic = os.environ.get("GSC_COMPOSE", "1") != "0"
+        # GPU: the update runs on hand-written kernels only (native_update.py); GSC_NATIVE_LEARNER=0
+        # selects the autograd + PyTorch path (the CPU path, and the reference for the GPU tests)
+        self.native_ok = (self.device.type == "cuda" and self.amp and not self.actor.squash
+                          and os.environ.get("GSC_NATIVE_LEARNER", "1") != "0")
+        self._native = None
 
     def _autocast(self):
         if self.amp:
@@ -102,18 +107,7 @@ class DDPGLearner:
     def _allreduce(self, flat: FlatParams):
         return allreduce_sum_(flat.grad, async_op=True)
 
-    # -- update stages (eager or captured into HIP graphs) ---------------------------------------
-    def _side_streams(self):
-        """Two side streams for the independent branches of an update (GPU only; opt-in with
-        GSC_LEARNER_BRANCHES=1).  Measured on MI355X (headline bench, 3 alternating runs each): off
-        70.3k, on 66.8k env-steps/s -- the learner already fits under the simulator kernel, and the
-        extra concurrency lands learner waves on the simulator's CUs and slows the critical path."""
-        if self.device.type != "cuda" or os.environ.get("GSC_LEARNER_BRANCHES", "0") == "0":
-            return None
-        if getattr(self, "_sides", None) is None:
-            self._sides = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
-        return self._sides
-
+    # -- update stages of the autograd path (CPU; GPU reference with GSC_NATIVE_LEARNER=0) -------
     def _target(self, b: Batch) -> torch.Tensor:
         g, masks = self.graphs, self.masks
         with torch.no_grad(), self._autocast():
@@ -123,39 +117,15 @@ class DDPGLearner:
             return b.rewards + (1 - b.dones) * self.gamma * q2
 
     def _stage_critic(self, b: Batch) -> None:
-        """TD target + critic loss -> critic gradients in ``critic_flat.grad``, and the actor forward.
-
-        On the GPU the three independent chains -- target actor/critic on next_obs, critic on obs,
-        actor on obs -- run as parallel branches (two side streams; inside a HIP graph they become
-        concurrent graph branches), so their many small kernels overlap instead of queueing."""
+        """TD target + critic loss -> critic gradients in ``critic_flat.grad``."""
         g, masks = self.graphs, self.masks
-        side = self._side_streams()
-        if side is None:
-            y = self._target(b)
-            with self._autocast():
-                q = self.critic(b.obs, b.topo, g, masks, b.actions).float().view(-1)
-            self._stage_actor_fwd(b)
-        else:
-            cur = torch.cuda.current_stream(self.device)
-            s_t, s_a = side
-            s_t.wait_stream(cur)
-            s_a.wait_stream(cur)
-            with torch.cuda.stream(s_t):
-                y = self._target(b)
-            with torch.cuda.stream(s_a):
-                self._stage_actor_fwd(b)
-            with self._autocast():
-                q = self.critic(b.obs, b.topo, g, masks, b.actions).float().view(-1)
-            cur.wait_stream(s_t)
-            y.record_stream(cur)
+        y = self._target(b)
         with self._autocast():
+            q = self.critic(b.obs, b.topo, g, masks, b.actions).float().view(-1)
             lq = F.mse_loss(q, y)
         grads = torch.autograd.grad(lq, self.critic_flat.params)
         self.critic_flat.set_grads(grads)
         self._lq, self._qv = lq.detach(), q.detach().mean()
-        if side is not None:
-            cur.wait_stream(side[1])
-            self._a.record_stream(cur)
 
     def _composed(self) -> bool:
         # one topology and at least one actor hidden layer: critic(obs, actor(obs)) re-associated
@@ -190,27 +160,63 @@ class DDPGLearner:
     def _stage_actor_opt(self, inv_world: float) -> None:
         self.actor_opt.step(grad_scale=inv_world)
 
+    def native_update(self, batch_size: int):
+        if self._native is None or self._native.B != batch_size:
+            from .native_update import NativeDDPGUpdate
+            self._native = NativeDDPGUpdate(self, batch_size)
+        return self._native
+
     def update(self, b: Batch) -> None:
-        """One DDPG update, eager.  The critic-gradient all-reduce overlaps the actor forward."""
-        inv_world = 1.0 / self.dist.world_size
-        self._stage_critic(b)        # includes the actor forward (it does not read critic weights)
+        """One DDPG update, eager.
+
+        Data parallel: the critic-gradient all-reduce is issued as soon as the critic gradients exist
+        and runs on the communicator's stream while the actor's embedding + hidden layers (which do
+        not read critic weights) run on the compute stream; the critic step waits for it."""
+        s1, s2, s3, s4 = self._stages(b, 1.0 / self.dist.world_size)
+        s1()
         h_c = self._allreduce(self.critic_flat)
+        s2()
         if h_c is not None:
             h_c.wait()
-        self._stage_actor_grad(b, inv_world)
+        s3()
         h_a = self._allreduce(self.actor_flat)
         if h_a is not None:
             h_a.wait()
-        self._stage_actor_opt(inv_world)
+        s4()
         self.updates += 1
-        self.last = {"qf1_loss": self._lq, "actor_loss": self._la, "qf1_values": self._qv}
+        self.last = self._metrics_now()
 
     # -- HIP-graph replay ----------------------------------------------------------------------
+    def _stages(self, b: Batch, inv_world: float):
+        """The update as four stages: critic gradients | actor forward | critic step + actor
+        gradients | actor step.  The critic all-reduce runs between stages 1 and 3, concurrently
+        with stage 2; the actor all-reduce between stages 3 and 4."""
+        if self.native_ok:
+            nu = self.native_update(b.obs.shape[0])
+
+            def s1():
+                nu.prepare(b)
+                nu.stage_critic(b)
+
+            def s3():
+                self.critic_opt.step(grad_scale=inv_world)
+                nu.stage_actor_grad(b)
+
+            return [s1, lambda: nu.stage_actor_fwd(b), s3, lambda: self.actor_opt.step(grad_scale=inv_world)]
+        return [lambda: self._stage_critic(b), lambda: self._stage_actor_fwd(b),
+                lambda: self._stage_actor_grad(b, inv_world), lambda: self._stage_actor_opt(inv_world)]
+
+    def _metrics_now(self) -> Dict[str, torch.Tensor]:
+        if self.native_ok and self._native is not None:
+            return self._native.last_metrics()
+        return {"qf1_loss": self._lq, "actor_loss": self._la, "qf1_values": self._qv}
+
     def update_graphed(self, b: Batch, warmup: int = 2) -> None:
         """Same update, replayed from captured HIP graphs (``b`` must be the same static buffers on
-        every call).  One process: one graph for the whole update.  Data parallel: three graphs with
-        the two gradient all-reduces issued eagerly between them (collectives stay out of capture).
-        The first ``warmup`` calls run eagerly (they are real updates) on a side stream."""
+        every call).  One process: one graph for the whole update.  Data parallel: four graphs with
+        the gradient all-reduces issued eagerly between them (collectives stay out of capture); the
+        critic all-reduce overlaps the actor-forward graph.  The first ``warmup`` calls run eagerly
+        (they are real updates) on a side stream."""
         inv_world = 1.0 / self.dist.world_size
         if self._graphs is None:
             if self._graph_warm < warmup:
@@ -225,39 +231,32 @@ class DDPGLearner:
         if len(self._graphs) == 1:
             self._graphs[0].replay()
         else:
-            g1, g2, g3 = self._graphs
+            g1, g2, g3, g4 = self._graphs
             g1.replay()
             h = self._allreduce(self.critic_flat)
-            if h is not None:
-                h.wait()
             g2.replay()
-            h = self._allreduce(self.actor_flat)
             if h is not None:
                 h.wait()
             g3.replay()
+            h = self._allreduce(self.actor_flat)
+            if h is not None:
+                h.wait()
+            g4.replay()
         self.updates += 1
-        self.last = {"qf1_loss": self._lq, "actor_loss": self._la, "qf1_values": self._qv}
+        self.last = self._metrics_now()
 
     def _capture(self, b: Batch, inv_world: float) -> None:
         # thread-local capture: the RCCL watchdog thread keeps querying its events while we capture
         pool = torch.cuda.graph_pool_handle()
+        stages = self._stages(b, inv_world)
         graphs = []
-        if self.dist.world_size == 1:
+        groups = [stages] if self.dist.world_size == 1 else [[f] for f in stages]
+        for grp in groups:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
-                self._stage_critic(b)
-                self._stage_actor_grad(b, inv_world)
-                self._stage_actor_opt(inv_world)
-            graphs.append(g)
-        else:
-            stages = [lambda: self._stage_critic(b),
-                      lambda: self._stage_actor_grad(b, inv_world),
-                      lambda: self._stage_actor_opt(inv_world)]
-            for fn in stages:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+                for fn in grp:
                     fn()
-                graphs.append(g)
+            graphs.append(g)
         self._graphs = graphs
         # capture recorded but did not execute the update: the caller's replay performs it
 

@@ -1,0 +1,337 @@
+"""One DDPG update on hand-written kernels only (GPU path of :class:`DDPGLearner`).
+
+Reference: ``SimpleDDPG._update_critic / _update_actor / _update_target_networks``
+(``src/rlsp/agents/simple_ddpg.py:204-234``) on the networks of ``src/rlsp/agents/models.py:55-154``.
+Per update, on a replay batch (obs, topo, action, reward, next_obs, done):
+
+    y   = r + (1 - d) gamma Q'(s', clamp(mu'(s'), -1, 1))
+    Lq  = mean (Q(s, a) - y)^2              -> critic grads -> [all-reduce] -> Adam + Polyak (critic)
+    La  = -mean Q_new(s, mu(s))             -> actor grads  -> [all-reduce] -> Adam + Polyak (actor)
+
+Every product runs on the MFMA GEMM engine (``csrc/ops/mlp.hip``) with fused epilogues, the GATv2
+embedders on the MFMA GNN kernels, the output layer + losses in one head kernel, the optimizer in the
+fused Adam/Polyak kernel -- no autograd, no hipBLASLt, no PyTorch elementwise kernels; all buffers are
+preallocated, so the whole update is captured into HIP graphs.  Manual backward per layer:
+
+    first layer   h0 = relu(emb W_d^T + b + mask[topo] W_m^T (+ act W_a^T))   (mask block folded per topology)
+                  dW_d | db | S_t = dh0^T [emb | 1 | onehot(topo)],  dW_m = sum_t S_t (x) mask_t,
+                  dW_a = dh0^T act,  d emb = dh0 W_d
+    hidden        h = relu(x W^T + b):  dW = dh^T x,  db = dh^T 1,  dx = (dh W) * (x > 0)
+    actor output  a = (h W^T + b) * mask[topo]           (target: clamped to [-1, 1])
+
+The actor loss goes through the critic's action projection.  With one topology and at least one actor
+hidden layer the projection re-associates (``a W_a^T = h (W_a diag(m) W)^T + W_a (b * m)``), so no
+``[B, A]`` actor output is materialised; otherwise (several topologies, or ``GSC_COMPOSE=0``) the
+``[B, A]`` output and its gradient are materialised -- both paths are the same function.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+
+from gsc_amd.native import load as load_native
+from gsc_amd.ops.gnn import _layer_of, _tables
+from gsc_amd.ops.mlp import gemm
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+class _Net:
+    """Pointers/views of one Actor or QNetwork inside its FlatParams (fp32 master, bf16 shadow, grad)."""
+
+    def __init__(self, module, flat, grad: bool, H: int, A: int, is_critic: bool):
+        self.m, self.fp = module, flat
+        self.layers = list(module.mlp.layers)
+        self.H, self.A = H, A
+        self.is_critic = is_critic
+
+    def w16(self, i):
+        return self.layers[i].weight._bf16
+
+    def w32(self, i):
+        return self.layers[i].weight
+
+    def b32(self, i):
+        return self.layers[i].bias
+
+    def gw(self, i):
+        fp, p = self.fp, self.layers[i].weight
+        o = fp.offset_of(p)
+        return fp.grad[o:o + p.numel()].view_as(p)
+
+    def gb(self, i):
+        fp, p = self.fp, self.layers[i].bias
+        o = fp.offset_of(p)
+        return fp.grad[o:o + p.numel()].view_as(p)
+
+    @property
+    def nh(self) -> int:  # hidden layers
+        return len(self.layers) - 1
+
+    def width(self, i) -> int:
+        return self.layers[i].weight.shape[0]
+
+    def emb_ptr(self) -> int:
+        return self.fp.flat.data_ptr()  # the embedder block is the first run of the flat buffer
+
+
+class NativeDDPGUpdate:
+    def __init__(self, learner, batch_size: int):
+        from gsc_amd.agents.ddpg import DDPGLearner  # noqa: F401  (type reference)
+        L = learner
+        self.L = L
+        self.nat = load_native()
+        dev = L.device
+        self.dev = dev
+        self.B = B = int(batch_size)
+        self.H = H = L.actor.embedder.hidden_dim
+        self.A = A = L.actor.action_dim
+        self.masks = L.masks.float().contiguous()          # [T, A]
+        self.T = T = self.masks.shape[0]
+        self.gamma = float(L.gamma)
+        self.actor = _Net(L.actor, L.actor_flat, True, H, A, False)
+        self.critic = _Net(L.critic, L.critic_flat, True, H, A, True)
+        self.tactor = _Net(L.target_actor, L.target_actor_flat, False, H, A, False)
+        self.tcritic = _Net(L.target_critic, L.target_critic_flat, False, H, A, True)
+        if L.actor.squash:
+            raise NotImplementedError("native update: sigmoid-squashed actor output")
+        self.compose = (os.environ.get("GSC_COMPOSE", "1") != "0" and T == 1 and self.actor.nh >= 1)
+        self.graphs = L.graphs
+        self.tables = _tables(L.graphs)
+        self.layer_of = _layer_of(L.actor.embedder)
+        self.P = L.graphs.n_pad
+        mk = lambda *s, dt=F32: torch.zeros(*s, device=dev, dtype=dt)
+        # activations
+        self.emb = {k: mk(B, H) for k in ("ta", "tc", "c", "c2", "a")}
+        self.hid_a = [mk(B, self.actor.width(i), dt=BF16) for i in range(self.actor.nh)]
+        self.hid_ta = [mk(B, self.actor.width(i), dt=BF16) for i in range(self.actor.nh)]
+        self.hid_c = [mk(B, self.critic.width(i), dt=BF16) for i in range(self.critic.nh)]
+        self.act_buf = mk(B, A, dt=BF16)                     # target action / materialised actor output
+        cmax = max(self.critic.width(i) for i in range(self.critic.nh))
+        amax = max([self.actor.width(i) for i in range(self.actor.nh)] + [1])
+        wmax = max(cmax, amax)
+        self.hacc = mk(B, cmax)
+        self.y = mk(B)
+        self.dh = [mk(B, wmax, dt=BF16), mk(B, wmax, dt=BF16)]
+        self.dact = mk(B, A, dt=BF16) if not self.compose else None
+        self.demb = mk(B, H)
+        c1 = self.critic.width(0)
+        self.wa = {k: mk(c1, A, dt=BF16) for k in ("c", "tc", "cm")}   # aligned critic action blocks
+        self.rowtab = {k: mk(T, wmax) for k in ("a", "ta", "c", "tc")}
+        self.aug = mk(wmax, max(H + 1 + T, 1))
+        hl = self.actor.width(self.actor.nh - 1) if self.actor.nh else 1
+        self.mc32 = mk(c1, hl)
+        self.mc16 = mk(c1, hl, dt=BF16)
+        self.cb = mk(c1, 1)
+        self.dmc = mk(c1, hl + 1)
+        self.splits = None                                   # auto split-K for the batch reductions
+        self.slabs = mk(16 << 20)                            # split-K slabs (64 MB; bounds the split count)
+        self.head_blocks = 64
+        cm = self.critic.width(self.critic.nh - 1)
+        self.part = mk(self.head_blocks * (cm + 3))
+        self.metrics = mk(4)                                 # qf1_loss, qf1_values, actor_loss, -
+        # GNN saved state / backward partials
+        nat = self.nat
+        Fin = L.actor.embedder.input_dim
+        self.Fin = Fin
+        sb = nat.gnn_saved_bytes(self.tables, self.P, Fin, H, self.layer_of)
+        self.blob = {k: torch.empty(B * sb, device=dev, dtype=torch.uint8) for k in ("a", "c")}
+        self.gnn_rows = 1024
+        ne = sum(p.numel() for p in L.actor.embedder.flat_parameters())
+        self.gnn_partials = torch.empty(self.gnn_rows, ne, device=dev, dtype=F32)
+        self.gnn_grad = mk(ne)
+        self.topo32 = torch.zeros(B, dtype=torch.int32, device=dev)
+
+    # ------------------------------------------------------------------------------------------
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def _gnn_fwd(self, net: _Net, x: torch.Tensor, out: torch.Tensor, save: Optional[torch.Tensor]) -> None:
+        self.nat.gnn_forward(self.tables, net.emb_ptr(), x.data_ptr(), self.topo32.data_ptr(), out.data_ptr(), self.B,
+                             self.P, self.Fin, self.H, self.layer_of, self._stream(),
+                             save.data_ptr() if save is not None else 0)
+
+    def _gnn_bwd(self, net: _Net, x: torch.Tensor, demb: torch.Tensor, blob: torch.Tensor) -> None:
+        # the embedder gradient is the first run of the network's flat gradient buffer
+        self.nat.gnn_backward(self.tables, net.emb_ptr(), x.data_ptr(), self.topo32.data_ptr(), demb.data_ptr(),
+                              self.gnn_partials.data_ptr(), self.gnn_rows, net.fp.grad.data_ptr(), self.B, self.P,
+                              self.Fin, self.H, self.layer_of, self._stream(), blob.data_ptr())
+
+    def _rowtab(self, net: _Net, key: str) -> torch.Tensor:
+        """mask[t] @ W_m^T for every topology t: the folded mask block of the first layer [T, h0]."""
+        h0 = net.width(0)
+        out = self.rowtab[key][:, :h0]
+        w = net.w16(0)
+        self.nat.rowdot(self.masks.data_ptr(), self.masks.stride(0), self.T, w.data_ptr() + 2 * self.H, w.stride(0),
+                        h0, self.A, out.data_ptr(), out.stride(0), self._stream())
+        return out
+
+    def _wa(self, net: _Net, key: str, colmask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Aligned copy of the critic's action block W[:, H+A:] (optionally column-masked)."""
+        w = net.w16(0)
+        dst = self.wa[key]
+        H, A = self.H, self.A
+        self.nat.copy2d(w.data_ptr() + 2 * (H + A), w.stride(0), dst.data_ptr(), dst.stride(0), dst.shape[0], A,
+                        colmask.data_ptr() if colmask is not None else 0, self._stream())
+        return dst
+
+    def _first(self, net: _Net, emb, rowtab, out16, extra=None, wa=None, extra_bias=None):
+        """h0 = relu(emb W_d^T + b + rowtab[topo] (+ extra wa^T + extra_bias)) -> out16."""
+        h0 = net.width(0)
+        acc = False
+        if extra is not None:
+            gemm(extra, wa, "nt", out32=self.hacc[:, :h0], bias=extra_bias)
+            acc = True
+        gemm(emb, net.w16(0)[:, :self.H], "nt", out16=out16, bias=net.b32(0), rowtab=rowtab, topo=self.topo32,
+             relu=True, accumulate=acc, out32=self.hacc[:, :h0] if acc else None)
+
+    def _hidden_fwd(self, net: _Net, acts: List[torch.Tensor]) -> None:
+        for i in range(1, net.nh):
+            gemm(acts[i - 1], net.w16(i), "nt", out16=acts[i], bias=net.b32(i), relu=True)
+
+    def _hidden_bwd(self, net: _Net, acts: List[torch.Tensor], dh: torch.Tensor, grads: bool) -> torch.Tensor:
+        """Back through hidden layers nh-1 .. 1; ``dh`` = gradient at the last hidden activation's
+        pre-ReLU (already gated).  Returns the gated gradient at layer 0's pre-activation."""
+        cur = 0
+        bufs = self.dh
+        for i in range(net.nh - 1, 0, -1):
+            wi, wo = net.width(i - 1), net.width(i)
+            if grads:
+                gemm(dh, acts[i - 1], "tn", out32=net.gw(i), splits=self.splits, slabs=self.slabs)
+                gemm(dh, acts[i - 1][:, :0], "tn", out32=net.gb(i).view(-1, 1), aug_t=0, aug_topo=self.topo32)
+            nxt = bufs[cur][:, :wi] if dh.data_ptr() != bufs[cur].data_ptr() else bufs[cur ^ 1][:, :wi]
+            gemm(dh, net.w16(i), "nn", out16=nxt, gate=acts[i - 1])
+            dh = nxt
+        return dh
+
+    def _first_bwd(self, net: _Net, emb, dh0, extra=None) -> None:
+        """Gradients of the first layer (dense, bias, mask block, optional action block) + d emb."""
+        H, A, T = self.H, self.A, self.T
+        h0 = net.width(0)
+        aug = self.aug[:h0, :H + 1 + T]
+        gemm(dh0, emb, "tn", out32=aug, aug_t=T, aug_topo=self.topo32, splits=self.splits, slabs=self.slabs)
+        gw = net.gw(0)
+        self.nat.first_layer_grad(aug.data_ptr(), h0, H, T, A, self.masks.data_ptr(), self.masks.stride(0),
+                                  gw.data_ptr(), gw.stride(0), net.gb(0).data_ptr(), self._stream())
+        if extra is not None:
+            gemm(dh0, extra, "tn", out32=gw[:, H + A:], splits=self.splits, slabs=self.slabs)
+        gemm(dh0, net.w16(0)[:, :H], "nn", out32=self.demb)
+
+    def _critic_tail(self, net: _Net, acts, mode: int, dh_out: Optional[torch.Tensor], b) -> None:
+        last = net.nh
+        h = acts[last - 1]
+        w = net.w32(last)
+        self.nat.mlp_head(h.data_ptr(), h.stride(0), self.B, h.shape[1], mode, w.data_ptr(), net.b32(last).data_ptr(),
+                          self.gamma, b.rewards.data_ptr(), b.dones.data_ptr(), self.y.data_ptr(),
+                          dh_out.data_ptr() if dh_out is not None else 0, dh_out.stride(0) if dh_out is not None else 0,
+                          self.part.data_ptr() if mode else 0, self.head_blocks, self._stream())
+
+    def _head_reduce(self, net: _Net, C: int, mode: int) -> None:
+        nw = self.head_blocks
+        s = self._stream()
+        part = self.part.data_ptr()
+        if mode == 1:  # dW | db of the output layer (contiguous in the grad buffer), loss, q mean
+            gw = net.gw(net.nh)
+            self.nat.splitk_reduce(part, C + 3, nw, 1, C, C + 3, gw.data_ptr(), C, 1.0, 0, s)
+            self.nat.splitk_reduce(part + 4 * C, C + 3, nw, 1, 1, C + 3, net.gb(net.nh).data_ptr(), 1, 1.0, 0, s)
+            self.nat.splitk_reduce(part + 4 * (C + 1), C + 3, nw, 1, 1, C + 3, self.metrics.data_ptr(), 1,
+                                   1.0 / self.B, 0, s)
+            self.nat.splitk_reduce(part + 4 * (C + 2), C + 3, nw, 1, 1, C + 3, self.metrics.data_ptr() + 4, 1,
+                                   1.0 / self.B, 0, s)
+        else:          # actor loss = -mean q
+            self.nat.splitk_reduce(part + 4 * (C + 2), C + 3, nw, 1, 1, C + 3, self.metrics.data_ptr() + 8, 1,
+                                   -1.0 / self.B, 0, s)
+
+    # ------------------------------------------------------------------------------------------
+    def prepare(self, b) -> None:
+        """Batch-dependent inputs the kernels share (int32 topology ids)."""
+        self.topo32.copy_(b.topo)
+
+    def stage_critic(self, b) -> None:
+        """TD target (target nets) + critic loss + all critic gradients into ``critic_flat.grad``."""
+        H, A = self.H, self.A
+        ta, tc, c = self.tactor, self.tcritic, self.critic
+        # target actor on s'
+        self._gnn_fwd(ta, b.next_obs, self.emb["ta"], None)
+        self._first(ta, self.emb["ta"], self._rowtab(ta, "ta"), self.hid_ta[0])
+        self._hidden_fwd(ta, self.hid_ta)
+        last = ta.nh
+        gemm(self.hid_ta[last - 1], ta.w16(last), "nt", out16=self.act_buf, bias=ta.b32(last), colmask=self.masks,
+             topo=self.topo32, clamp=(-1.0, 1.0))
+        # target critic on (s', a')
+        self._gnn_fwd(tc, b.next_obs, self.emb["tc"], None)
+        self._first(tc, self.emb["tc"], self._rowtab(tc, "tc"), self.hid_c[0], extra=self.act_buf,
+                    wa=self._wa(tc, "tc"))
+        self._hidden_fwd(tc, self.hid_c)
+        self._critic_tail(tc, self.hid_c, 0, None, b)
+        # critic on (s, a): loss + gradients
+        self._gnn_fwd(c, b.obs, self.emb["c"], self.blob["c"])
+        self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], extra=b.actions, wa=self._wa(c, "c"))
+        self._hidden_fwd(c, self.hid_c)
+        C = c.width(c.nh - 1)
+        dh = self.dh[0][:, :C]
+        self._critic_tail(c, self.hid_c, 1, dh, b)
+        self._head_reduce(c, C, 1)
+        dh0 = self._hidden_bwd(c, self.hid_c, dh, grads=True)
+        self._first_bwd(c, self.emb["c"], dh0, extra=b.actions)
+        self._gnn_bwd(c, b.obs, self.demb, self.blob["c"])
+
+    def stage_actor_fwd(self, b) -> None:
+        """Actor embedding + hidden layers on s (independent of the critic step: overlaps its all-reduce)."""
+        a = self.actor
+        self._gnn_fwd(a, b.obs, self.emb["a"], self.blob["a"])
+        self._first(a, self.emb["a"], self._rowtab(a, "a"), self.hid_a[0])
+        self._hidden_fwd(a, self.hid_a)
+
+    def stage_actor_grad(self, b) -> None:
+        """Actor loss through the (updated, frozen) critic -> actor gradients into ``actor_flat.grad``."""
+        H, A = self.H, self.A
+        a, c = self.actor, self.critic
+        self._gnn_fwd(c, b.obs, self.emb["c2"], None)
+        hl = self.hid_a[a.nh - 1]
+        last = a.nh
+        rt_c = self._rowtab(c, "c")
+        wa = self._wa(c, "c")
+        if self.compose:
+            m = self.masks[0]
+            wam = self._wa(c, "cm", colmask=m)                       # W_a diag(m)
+            gemm(wam, a.w16(last), "nn", out32=self.mc32, slabs=self.slabs, splits=16)   # Mc = W_a diag(m) W
+            self.nat.cast2d(self.mc32.data_ptr(), self.mc32.stride(0), self.mc16.data_ptr(),
+                                     self.mc16.stride(0), self.mc32.shape[0], self.mc32.shape[1], self._stream())
+            bl = a.b32(last)                                                     # cb = W_a (b * m)
+            self.nat.rowdot(bl.data_ptr(), bl.numel(), 1, wam.data_ptr(), wam.stride(0), wam.shape[0], A,
+                            self.cb.data_ptr(), 1, self._stream())
+            self._first(c, self.emb["c2"], rt_c, self.hid_c[0], extra=hl, wa=self.mc16, extra_bias=self.cb.view(-1))
+        else:
+            gemm(hl, a.w16(last), "nt", out16=self.act_buf, bias=a.b32(last), colmask=self.masks, topo=self.topo32)
+            self._first(c, self.emb["c2"], rt_c, self.hid_c[0], extra=self.act_buf, wa=wa)
+        self._hidden_fwd(c, self.hid_c)
+        C = c.width(c.nh - 1)
+        dh = self.dh[0][:, :C]
+        self._critic_tail(c, self.hid_c, 2, dh, b)
+        self._head_reduce(c, C, 2)
+        dh0 = self._hidden_bwd(c, self.hid_c, dh, grads=False)      # gated grad at the critic's layer-0 pre-act
+        c1 = c.width(0)
+        hw = hl.shape[1]
+        dz = self.dh[1][:, :hw] if dh0.data_ptr() != self.dh[1].data_ptr() else self.dh[0][:, :hw]
+        if self.compose:
+            # dMc | dcb = dh0^T [h | 1];  dW = diag(m) W_a^T dMc;  db = diag(m) W_a^T dcb;  dh = (dh0 Mc) * (h > 0)
+            gemm(dh0, hl, "tn", out32=self.dmc, aug_t=0, aug_topo=self.topo32, splits=self.splits, slabs=self.slabs)
+            gemm(wa, self.dmc[:, :hw], "tn", out32=a.gw(last), rowscale=m)
+            gemm(wa, self.dmc[:, hw:hw + 1], "tn", out32=a.gb(last).view(-1, 1), rowscale=m)
+            gemm(dh0, self.mc16, "nn", out16=dz, gate=hl)
+        else:
+            gemm(dh0, wa, "nn", out16=self.dact, colmask=self.masks, topo=self.topo32)   # dL/da (masked)
+            gemm(self.dact, hl, "tn", out32=a.gw(last), splits=self.splits, slabs=self.slabs)
+            gemm(self.dact, hl[:, :0], "tn", out32=a.gb(last).view(-1, 1), aug_t=0, aug_topo=self.topo32)
+            gemm(self.dact, a.w16(last), "nn", out16=dz, gate=hl)
+        dh0a = self._hidden_bwd(a, self.hid_a, dz, grads=True)
+        self._first_bwd(a, self.emb["a"], dh0a)
+        self._gnn_bwd(a, b.obs, self.demb, self.blob["a"])
+
+    def last_metrics(self) -> dict:
+        m = self.metrics
+        return {"qf1_loss": m[0], "qf1_values": m[1], "actor_loss": m[2]}

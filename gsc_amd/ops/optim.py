@@ -16,12 +16,18 @@ import torch.nn as nn
 
 
 class FlatParams:
-    def __init__(self, module: nn.Module, align: int = 4):
+    def __init__(self, module: nn.Module, align: int = 4, matrix_align: int = 8):
         self.module = module
-        self.params: List[nn.Parameter] = [p for p in module.parameters()]
+        named = list(module.named_parameters())
+        self.params: List[nn.Parameter] = [p for _, p in named]
+        self.names = [n for n, _ in named]
         total = 0
         self.offsets = []
-        for p in self.params:
+        for name, p in named:
+            # MLP weight matrices start on a 16-byte boundary of the bf16 shadow (16-byte staging loads
+            # in the MFMA GEMMs); the GNN block stays packed (its kernels index it as one run)
+            if p.dim() == 2 and not name.startswith("embedder."):
+                total = -(-total // matrix_align) * matrix_align
             self.offsets.append(total)
             total += p.numel()
         self.numel = total
@@ -47,6 +53,12 @@ class FlatParams:
     def refresh_shadow(self) -> None:
         if self.flat16 is not None:
             self.flat16.copy_(self.flat)
+
+    def offset_of(self, param: torch.Tensor) -> int:
+        for p, o in zip(self.params, self.offsets):
+            if p is param:
+                return o
+        raise KeyError("parameter not managed by this FlatParams")
 
     def view(self) -> torch.Tensor:
         return self.flat[: self.numel]
@@ -132,10 +144,9 @@ class FusedAdamPolyak:
             stream = torch.cuda.current_stream(p.device).cuda_stream
             skip = 0
             if self.guard_enabled:
-                nat.grad_guard(g.data_ptr(), self.fp.numel, self.guard.data_ptr(), stream)
+                # a skipped step does not advance Adam's bias-correction counter (done on the device)
+                nat.grad_guard(g.data_ptr(), self.fp.numel, self.guard.data_ptr(), stream, self.step_t.data_ptr())
                 skip = self.guard.data_ptr()
-                # a skipped step does not advance Adam's bias-correction counter
-                self.step_t.add_(1 - self.guard[0].to(torch.int64))
             else:
                 self.step_t.add_(1)
             nat.adam_polyak(p.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
