@@ -49,12 +49,13 @@ def test_graphed_update_matches_eager():
 
 
 def test_bf16_shadows_match_autocast_casts():
-    """Updates using the bf16 parameter shadows == updates where autocast casts the fp32 weights."""
+    """Autograd path: updates using the bf16 parameter shadows == updates where autocast casts the fp32 weights."""
     dev = "cuda"
     cfg = yaml.safe_load(open(cfg_path("config", "agent", "sample_agent.yaml")))
     gs = GraphSet([load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml"))], 24, dev)
     a = DDPGLearner(cfg, 3, 1728, gs, 1, 3, dev, seed=9)
     b = DDPGLearner(cfg, 3, 1728, gs, 1, 3, dev, seed=9)
+    a.native_ok = b.native_ok = False  # autograd path: shadows vs autocast casts (the native path needs shadows)
     for fp in (b.actor_flat, b.critic_flat, b.target_actor_flat, b.target_critic_flat):
         fp.flat16 = None
         for p in fp.params:
