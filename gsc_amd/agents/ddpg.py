@@ -325,6 +325,7 @@ class BatchedTrainer:
         self.batch_size = tcfg.batch_size or 100 * self.E
         self.learning_starts = (tcfg.learning_starts if tcfg.learning_starts is not None
                                 else int(cfg.get("nb_steps_warmup_critic", 200)))
+        self._warmup_steps = max(int(self.learning_starts), 1)
         self.rand_mu = float(cfg.get("rand_mu", 0.0))
         self.rand_sigma = float(cfg.get("rand_sigma", 0.3))
         self.global_step = 0
@@ -535,7 +536,17 @@ class BatchedTrainer:
         self.topo = sd["topo"].to(self.device)
         if "replay" in sd:
             self.replay.load_state_dict(sd["replay"])
-        else:  # checkpoint without the replay ring: resume refills it (learning restarts after warm-up)
+        else:  # checkpoint without the replay ring: resume refills it for a full configured warm-up
             self.replay.pos, self.replay.full = 0, False
-            self.learning_starts = self.global_step + 1
+            self.learning_starts = self.global_step + self._warmup_steps
         self.replay.gen.set_state(sd["rng"])
+
+    def reseed(self, seed: int) -> None:
+        """Fresh rank-local randomness (resume of a checkpoint without this rank's state): new
+        simulator Philox keys (all envs restart their episode) and a new replay sampler stream."""
+        g = np.random.default_rng(seed)
+        self.sim.seeds.copy_(torch.from_numpy(g.integers(1, 2**31 - 1, size=self.E).astype(np.uint32)
+                                              .view(np.int32)).to(self.device))
+        self.sim.set_topologies(self.topo.to(torch.int32))
+        self._obs_bufs[self.global_step & 1].copy_(self.sim.reset())
+        self.replay.gen.manual_seed(int(seed) * 7919 + self.global_step)

@@ -211,8 +211,9 @@ class SimpleDDPG(RLSPAgent):
                 self._episode_end(ep_ret, {"charts/success_ratio": succ / max(succ + drop, 1)})
                 ep_ret, succ, drop = 0.0, 0, 0
                 self.obs, _ = self.env.reset(seed=h.seed)  # AutoResetWithSeed: same seed every episode
+            # reference simple_ddpg.py:308 trains at the episode end once global_step >= warm-up - 1
             if (self.global_step % self.episode_steps == self.episode_steps - 1
-                    and self.global_step > self.warmup):
+                    and self.global_step >= self.warmup - 1):
                 with trace_range("learn"):
                     for _ in range(self.episode_steps):
                         self.learner.update(self.rb.sample(self.batch_size, self.device))
@@ -323,12 +324,38 @@ class SimpleDDPG(RLSPAgent):
         broadcast_tensors([L.actor_flat.flat, L.critic_flat.flat, L.target_actor_flat.flat, L.target_critic_flat.flat])
         L.refresh_shadows()
 
+    def _per_rank(self) -> bool:
+        return self.backend == "batched" and self.dist.world_size > 1
+
     def save_checkpoint(self, path: str) -> None:
-        ckpt.save_checkpoint(path, self.state_dict(), meta={"experiment_id": self.agent_helper.experiment_id,
-                                                            "time": time.time()}, rank=self.dist.rank)
+        """Rank 0 writes ``path`` (learner + its trainer state).  Data parallel: every other rank writes
+        its own simulator states / replay ring / RNG state to ``ckpt.rank_path(path, r)`` -- the shards
+        are rank-seeded and must stay disjoint after a resume."""
+        sd = self.state_dict()
+        meta = {"experiment_id": self.agent_helper.experiment_id, "time": time.time(), "rank": self.dist.rank,
+                "world_size": self.dist.world_size}
+        if self._per_rank() and self.dist.rank > 0:
+            sd["trainer"].pop("learner", None)       # replicas are identical: rank 0's file holds the learner
+            ckpt.save_checkpoint(ckpt.rank_path(path, self.dist.rank), sd, meta=meta, rank=0)
+        else:
+            ckpt.save_checkpoint(path, sd, meta=meta, rank=self.dist.rank)
 
     def load_checkpoint(self, path: str) -> None:
-        self.load_state_dict(ckpt.load_checkpoint(path)["state"])
+        sd = ckpt.load_checkpoint(path)["state"]
+        if self._per_rank() and self.dist.rank > 0:
+            rp = ckpt.rank_path(path, self.dist.rank)
+            if os.path.exists(rp):
+                local = ckpt.load_checkpoint(rp)["state"]
+                local["trainer"]["learner"] = sd["trainer"]["learner"]
+                self.load_state_dict(local)
+                return
+            # no per-rank state (e.g. a checkpoint written by fewer ranks): take rank 0's learner and
+            # re-seed this rank's simulator streams / replay sampler so the shards stay disjoint
+            logger.warning(f"{rp} missing: rank {self.dist.rank} re-seeds its simulator and replay sampler")
+            self.load_state_dict(sd)
+            self.trainer.reseed(int(self.agent_helper.seed) * 1000 + self.dist.rank)
+            return
+        self.load_state_dict(sd)
 
     def close(self) -> None:
         if self.rewards_writer is not None:

@@ -12,8 +12,10 @@ unpickled:
 * ``agent_helper.obj`` — JSON (:meth:`AgentHelper.to_json`).
 * ``checkpoint.pt`` — full training state (actor, critic, both targets, Adam moments, replay ring,
   simulator state blobs, RNG states, global step / episode).  Rank 0 writes (atomically: temp
-  file + rename); on resume every rank loads the same file and the learner re-broadcasts from
-  rank 0, so replicas stay bit-identical.
+  file + rename); data parallel, rank r > 0 also writes its rank-local trainer state (simulator
+  states, replay ring, sampler RNG -- all rank-seeded) to ``checkpoint.rank{r}.pt``.  On resume
+  every rank loads the learner from rank 0's file plus its own rank-local state, and the learner
+  re-broadcasts from rank 0, so replicas stay bit-identical and the env/replay shards disjoint.
 """
 from __future__ import annotations
 
@@ -52,6 +54,14 @@ def load_actor(path: str, device="cpu"):
     actor.load_state_dict(d["state_dict"])
     actor.to(device).eval()
     return actor, {k: v for k, v in d.items() if k != "state_dict"}
+
+
+def rank_path(path: str, rank: int) -> str:
+    """File of rank ``rank``'s local trainer state (rank 0: ``path`` itself)."""
+    if rank == 0:
+        return path
+    root, ext = os.path.splitext(path)
+    return f"{root}.rank{rank}{ext}"
 
 
 def save_checkpoint(path: str, state: dict, meta: Optional[dict] = None, rank: int = 0) -> None:

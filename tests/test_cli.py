@@ -127,3 +127,16 @@ def test_inference_script(small):
     r1 = inference.main([os.path.join(base, runs[0])])
     r2 = inference.main([os.path.join(base, runs[0]), "--envs", "2"])
     assert r1[0]["success_ratio"] == pytest.approx(r2[0]["success_ratio"])  # deterministic config
+
+
+def test_oracle_trains_at_first_episode_end_when_warmup_equals_episode(small):
+    """Reference simple_ddpg.py:308 gates the episode-end updates on global_step >= warm-up - 1: with
+    nb_steps_warmup_critic == episode_steps the first episode already ends with episode_steps updates."""
+    from gsc_amd.agents import SimpleDDPG
+    tmp, agent, sched = small
+    cfg = yaml.safe_load(open(agent))
+    cfg["nb_steps_warmup_critic"] = cfg["episode_steps"]
+    open(agent, "w").write(yaml.safe_dump(cfg))
+    a = SimpleDDPG(_helper(tmp, agent, sched), backend="oracle", device="cpu", results_writers=False)
+    a.train(1)
+    assert a.learner.updates == cfg["episode_steps"]

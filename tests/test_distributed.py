@@ -124,3 +124,60 @@ def test_dp_batched_trainer_replicas_identical():
     assert torch.equal(r[0]["actor"], r[1]["actor"])
     assert torch.equal(r[0]["critic"], r[1]["critic"])
     assert float(r[0]["succ"]) == float(r[1]["succ"]) > 0
+
+
+def _resume_worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from gsc_amd.agents import SimpleDDPG
+    from gsc_amd.parallel.dist import init_distributed, shutdown
+    from gsc_amd.utils.experiment import setup
+    info = init_distributed("cpu")
+    os.chdir(ROOT)
+    cfg = _cfg()
+    cfg.update(episode_steps=4, nb_steps_warmup_critic=3, mem_limit=64)
+    agent = os.path.join(out_dir, "agent.yaml")
+    sched = os.path.join(out_dir, "sched.yaml")
+    if rank == 0:
+        open(agent, "w").write(yaml.safe_dump(cfg))
+        open(sched, "w").write(yaml.safe_dump({"training_network_files": [ABILENE], "inference_network": ABILENE, "period": 10}))
+    torch.distributed.barrier()
+    svc, simc = cfg_path("service_functions", "abc.yaml"), cfg_path("config", "simulator", "sample_config.yaml")
+
+    def make():
+        h = setup(agent, ABILENE, svc, simc, sched, 7, 2, results_root=os.path.join(out_dir, f"r{rank}"))
+        return SimpleDDPG(h, backend="batched", num_envs=2, device="cpu", dist_info=info, results_writers=False,
+                          trainer_overrides={"batch_size": 8})
+
+    a = make()
+    a.train(1)
+    path = os.path.join(out_dir, "ck.pt")
+    a.save_checkpoint(path)
+    torch.distributed.barrier()
+    a.train(1)
+    b = make()
+    b.load_checkpoint(path)
+    b.train(1)
+    torch.save({"a_states": a.sim.states.clone(), "b_states": b.sim.states.clone(),
+                "a_actor": a.learner.actor_flat.flat.clone(), "b_actor": b.learner.actor_flat.flat.clone(),
+                "a_rng": a.trainer.replay.gen.get_state(), "b_rng": b.trainer.replay.gen.get_state()},
+               os.path.join(out_dir, f"res{rank}.pt"))
+    shutdown()
+
+
+def test_dp_resume_keeps_rank_local_state():
+    """Data-parallel checkpoint: rank r > 0 writes its own simulator states / replay / sampler RNG
+    (checkpoint.rank{r}.pt); after resume each rank continues its own shard exactly (== the run that
+    never stopped) and the shards stay distinct across ranks."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_resume_worker, args=(_free_port(), d), nprocs=WORLD, join=True, start_method="spawn")
+        assert os.path.exists(os.path.join(d, "ck.rank1.pt"))
+        r = [torch.load(os.path.join(d, f"res{i}.pt"), weights_only=True) for i in range(WORLD)]
+    for x in r:
+        assert torch.equal(x["a_states"], x["b_states"])
+        assert torch.equal(x["a_actor"], x["b_actor"])
+        assert torch.equal(x["a_rng"], x["b_rng"])
+    assert not torch.equal(r[0]["b_states"], r[1]["b_states"])
+    assert not torch.equal(r[0]["b_rng"], r[1]["b_rng"])
+    assert torch.equal(r[0]["b_actor"], r[1]["b_actor"])
