@@ -296,6 +296,8 @@ class TrainerConfig:
                                             # = sim_cus/8 per XCD), the learner the rest; 0: shared CUs;
                                             # -1: auto (enough CUs for one round of env waves, <= half the GPU)
     cuda_graphs: bool = True                # replay the DDPG update from captured HIP graphs (GPU only)
+    amp_bf16: Optional[bool] = None         # None: bf16 GEMM operands on the GPU, fp32 on CPU; False: fp32
+                                            # autograd learner everywhere (learning checks)
 
 
 class BatchedTrainer:
@@ -311,7 +313,7 @@ class BatchedTrainer:
         self.E = sim.E
         self.graphs = GraphSet(sim.topologies, sim.n_pad, self.device)
         self.learner = DDPGLearner(cfg, sim.n_obs, sim.action_dim, self.graphs, sim.C, sim.F, self.device,
-                                   self.dist, seed=tcfg.seed)
+                                   self.dist, amp_bf16=tcfg.amp_bf16, seed=tcfg.seed)
         cap = tcfg.replay_capacity or min(int(cfg.get("mem_limit", 10000)) * self.E, tcfg.replay_cap_max)
         # byte budget: large action spaces (50/200-node topologies, A = N^2 C F) bound the ring size
         adt = torch.bfloat16 if self.learner.amp else torch.float32

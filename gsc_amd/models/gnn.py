@@ -19,6 +19,7 @@ Two implementations with identical semantics:
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -28,6 +29,8 @@ import torch.nn.functional as F
 from .graphs import GraphSet
 
 NEG_SLOPE = 0.2
+# GSC_GNN_NATIVE=0: the PyTorch reference embedder on the GPU too (fp32 learning checks)
+_NATIVE_GNN = os.environ.get("GSC_GNN_NATIVE", "1") != "0"
 
 
 def glorot_(t: torch.Tensor) -> torch.Tensor:
@@ -115,7 +118,7 @@ class GNNEmbedder(nn.Module):
     def forward(self, x: torch.Tensor, topo: torch.Tensor, graphs: GraphSet, use_native: Optional[bool] = None):
         """x [B, n_pad, F_in], topo [B] (topology index into ``graphs``) -> [B, hidden]."""
         if use_native is None:
-            use_native = x.is_cuda
+            use_native = x.is_cuda and _NATIVE_GNN
         if use_native:
             from gsc_amd.ops.gnn import gnn_embed, gnn_fits
             if gnn_fits(self, graphs, x.shape[1], x.shape[2]):
