@@ -21,6 +21,7 @@ __device__ __forceinline__ double round10(double x) { return rint(x * 1e10) / 1e
 template <int PM>
 __global__ __launch_bounds__(64) void explore_postprocess_kernel(const float* __restrict__ mu,
                                                                  const float* __restrict__ mask,
+                                                                 const long long* __restrict__ topo,
                                                                  float* __restrict__ out, int E, int A, int P,
                                                                  int warmup, float rand_mu, float rand_sigma,
                                                                  uint32_t seed, uint32_t step, double thr, int passes) {
@@ -28,6 +29,8 @@ __global__ __launch_bounds__(64) void explore_postprocess_kernel(const float* __
   const long slice = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (slice >= (long)E * R) return;
   const long base = slice * P;
+  // mask row: per env [E, A], or the env's topology row of a [T, A] table
+  const float* mrow = topo ? mask + topo[slice / R] * (long)A + (slice % R) * P : mask + base;
   double w[PM];
 #pragma unroll
   for (int i = 0; i < PM; i += 2) {
@@ -37,8 +40,8 @@ __global__ __launch_bounds__(64) void explore_postprocess_kernel(const float* __
       const float u1 = (float)(r.v[1] >> 8) * (1.0f / 16777216.0f);
       float a0, a1;
       if (warmup) {
-        a0 = u0 * mask[base + i];
-        a1 = i + 1 < P ? u1 * mask[base + i + 1] : 0.f;
+        a0 = u0 * mrow[i];
+        a1 = i + 1 < P ? u1 * mrow[i + 1] : 0.f;
       } else {
         const float rad = sqrtf(-2.0f * __logf(1.0f - u0));  // 1 - u0 in (0, 1]
         float sn, cs;
@@ -97,7 +100,7 @@ __global__ __launch_bounds__(64) void explore_postprocess_kernel(const float* __
     if (i < P) out[base + i] = (float)w[i];
 }
 
-void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t out, int E, int A, int P, int warmup, float rand_mu,
+void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t out, int E, int A, int P, int warmup, float rand_mu,
                          float rand_sigma, uint32_t seed, uint32_t step, double thr, int passes, uintptr_t stream) {
   GSC_CHECK(A % P == 0, "action dim must be a multiple of n_pad");
   const long slices = (long)E * (A / P);
@@ -105,7 +108,7 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t out, int E, int
   const int grid = (int)((slices + block - 1) / block);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, stream_of(stream), ptr<const float>(mu),
-                       ptr<const float>(mask), ptr<float>(out), E, A, P, warmup, rand_mu, rand_sigma, seed, step,
+                       ptr<const float>(mask), ptr<const long long>(topo), ptr<float>(out), E, A, P, warmup, rand_mu, rand_sigma, seed, step,
                        thr, passes);
   };
   if (P <= 32) go(explore_postprocess_kernel<32>);

@@ -7,11 +7,13 @@ void register_gnn(py::module_& m);
 void register_optim(py::module_& m);
 void register_mlp(py::module_& m);
 void register_streams(py::module_& m);
+void register_replay(py::module_& m);
 void register_ops(py::module_& m) {
   register_explore(m);
   register_gnn(m);
   register_optim(m);
   register_mlp(m);
   register_streams(m);
+  register_replay(m);
 }
 }  // namespace gsc

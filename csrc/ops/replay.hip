@@ -1,0 +1,194 @@
+// Device replay ring: transition insert + Philox index sampling + row gather (reference
+// src/rlsp/agents/buffer.py:23-89, GraphReplayBuffer.add / sample).
+//
+// The ring cursor lives on the device (int64 state [pos, full, draws, -]) so insert and sample are
+// plain kernels with fixed arguments: both run inside captured HIP graphs, and nothing is read back
+// to the host.  Sampling follows the reference: uniform over the filled rows, and once the ring is
+// full the row at the write cursor (the next one to be overwritten) is excluded:
+//
+//     full:  idx = (pos + 1 + u * (cap - 1) >> 32) % cap        not full:  idx = u * pos >> 32
+//
+// with u the 32-bit Philox4x32-10 word (key = (seed, "repl"), counter = (draw << 32) | b / 4, word
+// b % 4) -- independent of launch shape, identical on the host path (CPU training, tests).
+#include <pybind11/pybind11.h>
+
+#include <cstring>
+
+#include "../common.h"
+#include "../sim/philox.h"
+
+namespace py = pybind11;
+
+namespace gsc {
+
+constexpr uint32_t kReplayKey1 = 0x7265706cu;  // "repl"
+
+struct ReplayState {  // int64 x 4 on the device (and in checkpoints)
+  long long pos, full, draws, pad;
+};
+
+GSC_HD int replay_index(uint32_t seed, long long draw, int b, long long pos, long long full, long long cap) {
+  const Philox4 r = philox4x32_10(seed, kReplayKey1, ((uint64_t)draw << 32) | (uint32_t)(b >> 2));
+  const uint64_t u = r.v[b & 3];
+  if (full) return (int)((pos + 1 + (long long)((u * (uint64_t)(cap - 1)) >> 32)) % cap);
+  return (int)((u * (uint64_t)pos) >> 32);
+}
+
+// ---- sample: one workgroup draws every index, then advances the draw counter --------------------
+__global__ __launch_bounds__(1024) void replay_index_kernel(ReplayState* st, uint32_t seed, int B, long long cap,
+                                                            int32_t* idx) {
+  const long long pos = st->pos, full = st->full, draw = st->draws;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) idx[b] = replay_index(seed, draw, b, pos, full, cap);
+  __syncthreads();
+  if (threadIdx.x == 0) st->draws = draw + 1;
+}
+
+// rows of `row_bytes` in granules of G bytes: dst[b] = src[idx[b]]
+template <class G>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const char* __restrict__ src, char* __restrict__ dst,
+                                                          const int32_t* __restrict__ idx, int B, long row_g) {
+  const long total = (long)B * row_g;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long b = i / row_g, k = i - b * row_g;
+    reinterpret_cast<G*>(dst)[i] = reinterpret_cast<const G*>(src)[(long)idx[b] * row_g + k];
+  }
+}
+
+// ---- insert: E rows at the cursor (no wrap-around bookkeeping on the host) ----------------------
+// kind 0: raw granule copy; 1: float32 -> bf16 (actions); 2: uint8 -> float32 (dones)
+template <class G, int KIND>
+__global__ __launch_bounds__(256) void insert_rows_kernel(const ReplayState* __restrict__ st, const char* __restrict__ src,
+                                                          char* __restrict__ dst, int E, long row_n, long long cap) {
+  const long long pos = st->pos;
+  const long total = (long)E * row_n;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long e = i / row_n, k = i - e * row_n;
+    const long d = ((pos + e) % cap) * row_n + k;
+    if constexpr (KIND == 0) reinterpret_cast<G*>(dst)[d] = reinterpret_cast<const G*>(src)[i];
+    if constexpr (KIND == 1) reinterpret_cast<__bf16*>(dst)[d] = (__bf16)reinterpret_cast<const float*>(src)[i];
+    if constexpr (KIND == 2) reinterpret_cast<float*>(dst)[d] = (float)reinterpret_cast<const uint8_t*>(src)[i];
+  }
+}
+
+__global__ void replay_advance_kernel(ReplayState* st, int E, long long cap) {
+  const long long p = st->pos + E;
+  if (p >= cap) st->full = 1;
+  st->pos = p % cap;
+}
+
+static int grid_for(long n) {
+  long g = (n + 255) / 256;
+  return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+}
+
+template <class F>
+static void by_granule(long bytes, uintptr_t a, uintptr_t b, F&& f) {
+  const uintptr_t al = a | b | (uintptr_t)bytes;
+  if (al % 16 == 0) f(int4{}, bytes / 16);
+  else if (al % 8 == 0) f(int2{}, bytes / 8);
+  else if (al % 4 == 0) f(int{}, bytes / 4);
+  else if (al % 2 == 0) f(short{}, bytes / 2);
+  else f(char{}, bytes);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host mirrors (CPU path): same index stream, same cursor semantics.
+// ------------------------------------------------------------------------------------------------
+static void host_indices(ReplayState* st, uint32_t seed, int B, long long cap, int32_t* idx) {
+  for (int b = 0; b < B; ++b) idx[b] = replay_index(seed, st->draws, b, st->pos, st->full, cap);
+  st->draws++;
+}
+
+// Launchers.  `device` selects the HIP kernels (pointers are device memory) or the host path.
+void replay_sample_indices(bool device, uintptr_t state, uint32_t seed, int B, long long cap, uintptr_t idx,
+                           uintptr_t stream) {
+  if (!device) {
+    host_indices(ptr<ReplayState>(state), seed, B, cap, ptr<int32_t>(idx));
+    return;
+  }
+  hipLaunchKernelGGL(replay_index_kernel, dim3(1), dim3(1024), 0, stream_of(stream), ptr<ReplayState>(state), seed, B,
+                     cap, ptr<int32_t>(idx));
+  check_launch();
+}
+
+void replay_gather(bool device, uintptr_t src, uintptr_t dst, uintptr_t idx, int B, long row_bytes,
+                   uintptr_t stream) {
+  if (!device) {
+    const int32_t* ix = ptr<int32_t>(idx);
+    for (int b = 0; b < B; ++b)
+      std::memcpy(ptr<char>(dst) + (long)b * row_bytes, ptr<char>(src) + (long)ix[b] * row_bytes, row_bytes);
+    return;
+  }
+  by_granule(row_bytes, src, dst, [&](auto g, long row_g) {
+    using G = decltype(g);
+    hipLaunchKernelGGL(gather_rows_kernel<G>, dim3(grid_for((long)B * row_g)), dim3(256), 0, stream_of(stream),
+                       ptr<const char>(src), ptr<char>(dst), ptr<const int32_t>(idx), B, row_g);
+  });
+  check_launch();
+}
+
+// kind as in insert_rows_kernel; row_n = elements per row (kind 0: bytes per row)
+void replay_insert(bool device, uintptr_t state, uintptr_t src, uintptr_t dst, int E, long row_n, long long cap,
+                   int kind, uintptr_t stream) {
+  if (!device) {
+    const long long pos = ptr<ReplayState>(state)->pos;
+    for (int e = 0; e < E; ++e) {
+      const long r = (long)((pos + e) % cap);
+      for (long k = 0; k < row_n; ++k) {
+        const long i = (long)e * row_n + k, d = r * row_n + k;
+        if (kind == 0) ptr<char>(dst)[d] = ptr<const char>(src)[i];
+        else if (kind == 1) {
+          // round-to-nearest-even float -> bf16 (same as the device conversion)
+          uint32_t u;
+          std::memcpy(&u, ptr<const float>(src) + i, 4);
+          const uint32_t lsb = (u >> 16) & 1u;
+          const uint16_t h = (u & 0x7fffffffu) > 0x7f800000u ? (uint16_t)((u >> 16) | 0x40u)
+                                                              : (uint16_t)((u + 0x7fffu + lsb) >> 16);
+          ptr<uint16_t>(dst)[d] = h;
+        } else if (kind == 2) ptr<float>(dst)[d] = (float)ptr<const uint8_t>(src)[i];
+      }
+    }
+    return;
+  }
+  const hipStream_t s = stream_of(stream);
+  if (kind == 0) {
+    by_granule(row_n, src, dst, [&](auto g, long row_g) {
+      using G = decltype(g);
+      hipLaunchKernelGGL((insert_rows_kernel<G, 0>), dim3(grid_for((long)E * row_g)), dim3(256), 0, s,
+                         ptr<const ReplayState>(state), ptr<const char>(src), ptr<char>(dst), E, row_g, cap);
+    });
+  } else if (kind == 1) {
+    hipLaunchKernelGGL((insert_rows_kernel<char, 1>), dim3(grid_for((long)E * row_n)), dim3(256), 0, s,
+                       ptr<const ReplayState>(state), ptr<const char>(src), ptr<char>(dst), E, row_n, cap);
+  } else {
+    hipLaunchKernelGGL((insert_rows_kernel<char, 2>), dim3(grid_for((long)E * row_n)), dim3(256), 0, s,
+                       ptr<const ReplayState>(state), ptr<const char>(src), ptr<char>(dst), E, row_n, cap);
+  }
+  check_launch();
+}
+
+void replay_advance(bool device, uintptr_t state, int E, long long cap, uintptr_t stream) {
+  if (!device) {
+    ReplayState* st = ptr<ReplayState>(state);
+    const long long p = st->pos + E;
+    if (p >= cap) st->full = 1;
+    st->pos = p % cap;
+    return;
+  }
+  hipLaunchKernelGGL(replay_advance_kernel, dim3(1), dim3(1), 0, stream_of(stream), ptr<ReplayState>(state), E, cap);
+  check_launch();
+}
+
+int replay_index_host(uint32_t seed, long long draw, int b, long long pos, long long full, long long cap) {
+  return replay_index(seed, draw, b, pos, full, cap);
+}
+
+void register_replay(py::module_& m) {
+  m.def("replay_sample_indices", &replay_sample_indices);
+  m.def("replay_gather", &replay_gather);
+  m.def("replay_insert", &replay_insert);
+  m.def("replay_advance", &replay_advance);
+  m.def("replay_index", &replay_index_host, "one sampled index (host; for tests)");
+}
+
+}  // namespace gsc

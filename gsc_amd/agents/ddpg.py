@@ -86,6 +86,7 @@ class DDPGLearner:
         self.native_ok = (self.device.type == "cuda" and self.amp and not self.actor.squash
                           and os.environ.get("GSC_NATIVE_LEARNER", "1") != "0")
         self._native = None
+        self._act_native = None
 
     def _autocast(self):
         if self.amp:
@@ -101,8 +102,18 @@ class DDPGLearner:
 
     @torch.no_grad()
     def act(self, obs: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:
+        """Greedy actor output (fp32).  GPU: native kernels (:class:`NativeAct`) when the batch is the
+        trainer's acting batch; otherwise the module forward."""
+        na = self._act_native
+        if na is not None and obs.shape[0] == na.E and obs.is_contiguous():
+            return na(obs, topo)
         with self._autocast():
             return self.actor(obs, topo, self.graphs, self.masks).float()
+
+    def enable_native_act(self, E: int) -> None:
+        from .native_update import NativeAct
+        if NativeAct.supported(self):
+            self._act_native = NativeAct(self, E)
 
     def _allreduce(self, flat: FlatParams):
         return allreduce_sum_(flat.grad, async_op=True)
@@ -344,6 +355,8 @@ class BatchedTrainer:
         self.masks = self.learner.masks
         self._act_bufs = [torch.empty(self.E, sim.action_dim, device=self.device) for _ in range(2)]
         self._pending = None  # (obs, topo, act, out) of the last step, not yet in replay / metrics
+        if self.device.type == "cuda":
+            self.learner.enable_native_act(self.E)
         # device-side metric accumulators (read back only when logging)
         self.acc_succ = torch.zeros((), dtype=torch.float64, device=self.device)
         self.acc_drop = torch.zeros((), dtype=torch.float64, device=self.device)
@@ -455,9 +468,9 @@ class BatchedTrainer:
         with trace_range("act"):
             mu = self.learner.act(obs, topo)
         with trace_range("explore"):
-            act = explore_postprocess(mu, self.masks.index_select(0, topo), self.sim.n_pad, warm, self.rand_mu,
-                                      self.rand_sigma, seed=self.t.seed * 131 + self.dist.rank,
-                                      step=self.global_step, out=self._act_bufs[k])
+            act = explore_postprocess(mu, self.masks, self.sim.n_pad, warm, self.rand_mu, self.rand_sigma,
+                                      seed=self.t.seed * 131 + self.dist.rank, step=self.global_step,
+                                      out=self._act_bufs[k], topo=topo)
         self._schedule_next()
         train = self.global_step >= self.learning_starts - 1 and (len(self.replay) > 0 or self._pending is not None)
         if self.sim_stream is not None and train:
@@ -523,7 +536,7 @@ class BatchedTrainer:
         self.flush()
         sd = {"learner": self.learner.state_dict(), "global_step": self.global_step, "episode": self.episode,
               "sim_states": self.sim.states.cpu(), "obs": self.obs.cpu(), "topo": self.topo.cpu(),
-              "rng": self.replay.gen.get_state()}
+              "rng": self.replay.rng_state()}
         if include_replay:
             sd["replay"] = self.replay.state_dict()
         return sd
@@ -538,10 +551,11 @@ class BatchedTrainer:
         self.topo = sd["topo"].to(self.device)
         if "replay" in sd:
             self.replay.load_state_dict(sd["replay"])
-        else:  # checkpoint without the replay ring: resume refills it for a full configured warm-up
+        self.replay.set_rng_state(sd["rng"])
+        if "replay" not in sd:  # checkpoint without the replay ring: resume refills it for a full warm-up
             self.replay.pos, self.replay.full = 0, False
+            self.replay.state[:2] = 0
             self.learning_starts = self.global_step + self._warmup_steps
-        self.replay.gen.set_state(sd["rng"])
 
     def reseed(self, seed: int) -> None:
         """Fresh rank-local randomness (resume of a checkpoint without this rank's state): new
@@ -551,4 +565,4 @@ class BatchedTrainer:
                                               .view(np.int32)).to(self.device))
         self.sim.set_topologies(self.topo.to(torch.int32))
         self._obs_bufs[self.global_step & 1].copy_(self.sim.reset())
-        self.replay.gen.manual_seed(int(seed) * 7919 + self.global_step)
+        self.replay.reseed(int(seed) * 7919 + self.global_step)

@@ -335,3 +335,49 @@ class NativeDDPGUpdate:
     def last_metrics(self) -> dict:
         m = self.metrics
         return {"qf1_loss": m[0], "qf1_values": m[1], "actor_loss": m[2]}
+
+
+class NativeAct:
+    """Acting forward ``mu(s)`` of the E environments on the native kernels (fp32 output): the
+    actor's embedder, first layer (topology mask block folded), hidden layers and masked output
+    layer -- the same products as the update's actor stages, without autograd or hipBLASLt.
+    Reference: ``Actor.forward`` (``src/rlsp/agents/models.py:119-154``)."""
+
+    def __init__(self, learner, E: int):
+        L = learner
+        self.L, self.nat, self.E = L, load_native(), int(E)
+        dev = L.device
+        self.H, self.A = L.actor.embedder.hidden_dim, L.actor.action_dim
+        self.net = _Net(L.actor, L.actor_flat, False, self.H, self.A, False)
+        self.masks = L.masks.float().contiguous()
+        self.T = self.masks.shape[0]
+        self.tables = _tables(L.graphs)
+        self.layer_of = _layer_of(L.actor.embedder)
+        self.P, self.Fin = L.graphs.n_pad, L.actor.embedder.input_dim
+        n = self.net
+        self.emb = torch.zeros(E, self.H, device=dev)
+        self.hid = [torch.zeros(E, n.width(i), device=dev, dtype=BF16) for i in range(n.nh)]
+        self.rowtab = torch.zeros(self.T, n.width(0), device=dev)
+        self.out = torch.zeros(E, self.A, device=dev)
+        self.topo32 = torch.zeros(E, dtype=torch.int32, device=dev)
+
+    @staticmethod
+    def supported(learner) -> bool:
+        return bool(learner.native_ok and len(learner.actor.mlp.layers) >= 2)
+
+    def __call__(self, obs: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:
+        n, s = self.net, torch.cuda.current_stream(self.L.device).cuda_stream
+        assert obs.shape[0] == self.E and obs.is_contiguous() and obs.dtype == F32
+        self.topo32.copy_(topo)
+        self.nat.gnn_forward(self.tables, n.emb_ptr(), obs.data_ptr(), self.topo32.data_ptr(), self.emb.data_ptr(),
+                             self.E, self.P, self.Fin, self.H, self.layer_of, s, 0)
+        w = n.w16(0)
+        self.nat.rowdot(self.masks.data_ptr(), self.masks.stride(0), self.T, w.data_ptr() + 2 * self.H, w.stride(0),
+                        n.width(0), self.A, self.rowtab.data_ptr(), self.rowtab.stride(0), s)
+        gemm(self.emb, w[:, :self.H], "nt", out16=self.hid[0], bias=n.b32(0), rowtab=self.rowtab, topo=self.topo32,
+             relu=True)
+        for i in range(1, n.nh):
+            gemm(self.hid[i - 1], n.w16(i), "nt", out16=self.hid[i], bias=n.b32(i), relu=True)
+        gemm(self.hid[n.nh - 1], n.w16(n.nh), "nt", out32=self.out, bias=n.b32(n.nh), colmask=self.masks,
+             topo=self.topo32)
+        return self.out

@@ -2,8 +2,9 @@
 
 ``DeviceReplay`` keeps transitions in HBM as structure-of-arrays tensors (node features, topology
 id, post-processed action, reward, done) — masks and edge lists are derived from the topology id
-instead of being stored per transition.  Adds are one indexed copy of E rows; sampling is a
-device ``randint`` + gather, so the learner never touches the host.  Sampling follows the
+instead of being stored per transition.  Inserts and samples are native kernels (Philox index
+draw + row gathers, ``csrc/ops/replay.hip``) with the ring cursor on the device, so the learner
+never touches the host and sampling is captured with the update.  Sampling follows the
 reference ``GraphReplayBuffer.sample`` (``buffer.py:56-62``): uniform over the filled part, and
 once full the slot at the write position (the next one to be overwritten) is excluded.
 
@@ -27,37 +28,71 @@ class Batch(NamedTuple):
 
 
 class DeviceReplay:
+    """Structure-of-arrays ring in HBM (or host memory on CPU) driven by the native replay kernels
+    (``csrc/ops/replay.hip``): the write cursor and the sampler's draw counter live in a device int64
+    ``state`` tensor ``[pos, full, draws, -]``, so :meth:`add` and :meth:`sample` are fixed-argument
+    kernel launches that run inside captured HIP graphs.  Indices come from Philox4x32-10 keyed by
+    ``seed`` (rank-specific) and the draw counter -- the same stream on the host path."""
+
     def __init__(self, capacity: int, n_pad: int, n_obs: int, action_dim: int, device,
                  action_dtype=torch.float32, seed: int = 0):
+        from gsc_amd.native import load as load_native
+        self.nat = load_native()
         self.capacity = int(capacity)
         dev = torch.device(device)
         self.device = dev
+        self.is_dev = dev.type == "cuda"
         self.obs = torch.zeros((self.capacity, n_pad, n_obs), dtype=torch.float32, device=dev)
         self.next_obs = torch.zeros_like(self.obs)
         self.topo = torch.zeros(self.capacity, dtype=torch.int64, device=dev)
         self.actions = torch.zeros((self.capacity, action_dim), dtype=action_dtype, device=dev)
         self.rewards = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
         self.dones = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
-        self.pos = 0
+        self.state = torch.zeros(4, dtype=torch.int64, device=dev)   # pos, full, draws, -
+        self.seed = int(seed) & 0xffffffff
+        self.pos = 0        # host mirrors of the device cursor (deterministic: E rows per add)
         self.full = False
-        self.gen = torch.Generator(device=dev)
-        self.gen.manual_seed(seed)
+        self._idx = {}
 
     def __len__(self) -> int:
         return self.capacity if self.full else self.pos
 
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream if self.is_dev else 0
+
+    def reseed(self, seed: int) -> None:
+        self.seed = int(seed) & 0xffffffff
+        self.state[2] = 0
+
     @torch.no_grad()
     def add(self, obs, topo, actions, rewards, next_obs, dones) -> None:
+        """Insert E rows at the device cursor.  ``dones``: uint8/bool/float [E]."""
         E = obs.shape[0]
         if E > self.capacity:
             raise ValueError("batch larger than replay capacity")
-        idx = (torch.arange(E, device=self.device) + self.pos) % self.capacity
-        self.obs.index_copy_(0, idx, obs)
-        self.next_obs.index_copy_(0, idx, next_obs)
-        self.topo.index_copy_(0, idx, topo.to(torch.int64))
-        self.actions.index_copy_(0, idx, actions.to(self.actions.dtype))
-        self.rewards.index_copy_(0, idx, rewards.float())
-        self.dones.index_copy_(0, idx, dones.float())
+        nat, s, dev, cap, st = self.nat, self._stream(), self.is_dev, self.capacity, self.state.data_ptr()
+        obs, next_obs = obs.contiguous().float(), next_obs.contiguous().float()
+        topo = topo.to(torch.int64).contiguous()
+        rewards = rewards.contiguous().float()
+        ob = obs[0].numel() * 4
+        nat.replay_insert(dev, st, obs.data_ptr(), self.obs.data_ptr(), E, ob, cap, 0, s)
+        nat.replay_insert(dev, st, next_obs.data_ptr(), self.next_obs.data_ptr(), E, ob, cap, 0, s)
+        nat.replay_insert(dev, st, topo.data_ptr(), self.topo.data_ptr(), E, 8, cap, 0, s)
+        nat.replay_insert(dev, st, rewards.data_ptr(), self.rewards.data_ptr(), E, 4, cap, 0, s)
+        A = self.actions.shape[1]
+        if self.actions.dtype == torch.bfloat16 and actions.dtype == torch.float32:
+            a = actions.contiguous()
+            nat.replay_insert(dev, st, a.data_ptr(), self.actions.data_ptr(), E, A, cap, 1, s)
+        else:
+            a = actions.to(self.actions.dtype).contiguous()
+            nat.replay_insert(dev, st, a.data_ptr(), self.actions.data_ptr(), E, A * a.element_size(), cap, 0, s)
+        if dones.dtype in (torch.uint8, torch.bool):
+            d = dones.contiguous().view(torch.uint8)
+            nat.replay_insert(dev, st, d.data_ptr(), self.dones.data_ptr(), E, 1, cap, 2, s)
+        else:
+            d = dones.contiguous().float()
+            nat.replay_insert(dev, st, d.data_ptr(), self.dones.data_ptr(), E, 4, cap, 0, s)
+        nat.replay_advance(dev, st, E, cap, s)
         new = self.pos + E
         if new >= self.capacity:
             self.full = True
@@ -65,27 +100,41 @@ class DeviceReplay:
 
     @torch.no_grad()
     def sample(self, batch_size: int, out: Optional[Batch] = None) -> Batch:
-        """Uniform sample; with ``out`` the rows are gathered into those (static) buffers."""
-        if self.full:
-            idx = (torch.randint(1, self.capacity, (batch_size,), device=self.device, generator=self.gen)
-                   + self.pos) % self.capacity
-        else:
-            if self.pos == 0:
-                raise RuntimeError("cannot sample from an empty replay buffer")
-            idx = torch.randint(0, self.pos, (batch_size,), device=self.device, generator=self.gen)
+        """Uniform sample (reference buffer.py:56-62); with ``out`` the rows are gathered into those
+        (static) buffers -- graph-capturable."""
+        if len(self) == 0:
+            raise RuntimeError("cannot sample from an empty replay buffer")
+        B = int(batch_size)
+        idx = self._idx.get(B)
+        if idx is None:
+            idx = self._idx[B] = torch.empty(B, dtype=torch.int32, device=self.device)
         if out is None:
-            return Batch(self.obs.index_select(0, idx), self.topo.index_select(0, idx),
-                         self.actions.index_select(0, idx), self.rewards.index_select(0, idx),
-                         self.next_obs.index_select(0, idx), self.dones.index_select(0, idx))
+            out = self.empty_batch(B)
+        nat, s, dev = self.nat, self._stream(), self.is_dev
+        nat.replay_sample_indices(dev, self.state.data_ptr(), self.seed, B, self.capacity, idx.data_ptr(), s)
         for src, dst in zip((self.obs, self.topo, self.actions, self.rewards, self.next_obs, self.dones), out):
-            torch.index_select(src, 0, idx, out=dst)
+            assert dst.is_contiguous() and dst.shape[0] == B and dst.dtype == src.dtype
+            nat.replay_gather(dev, src.data_ptr(), dst.data_ptr(), idx.data_ptr(), B, src[0].numel() * src.element_size(), s)
         return out
+
+    def last_indices(self, batch_size: int) -> torch.Tensor:
+        return self._idx[int(batch_size)]
 
     def empty_batch(self, batch_size: int) -> Batch:
         """Static batch buffers (for :meth:`sample` ``out=`` and HIP-graph replay)."""
         mk = lambda t: torch.empty((batch_size,) + tuple(t.shape[1:]), dtype=t.dtype, device=self.device)
         return Batch(mk(self.obs), mk(self.topo), mk(self.actions), mk(self.rewards), mk(self.next_obs),
                      mk(self.dones))
+
+    def rng_state(self) -> torch.Tensor:
+        return torch.cat([self.state.cpu(), torch.tensor([self.seed], dtype=torch.int64)])
+
+    def set_rng_state(self, t: torch.Tensor) -> None:
+        t = t.to(torch.int64).cpu()
+        if t.numel() != 5:
+            raise ValueError("replay sampler state: expected [pos, full, draws, -, seed]")
+        self.state.copy_(t[:4].to(self.device))
+        self.seed = int(t[4])
 
     def state_dict(self) -> dict:
         n = len(self)
@@ -98,6 +147,8 @@ class DeviceReplay:
         for k in ("obs", "next_obs", "topo", "actions", "rewards", "dones"):
             getattr(self, k)[:n].copy_(sd[k].to(self.device))
         self.pos, self.full = int(sd["pos"]), bool(sd["full"])
+        self.state[0] = self.pos
+        self.state[1] = int(self.full)
 
 
 class GraphReplayBuffer:

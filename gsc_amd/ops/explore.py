@@ -59,20 +59,28 @@ def explore_postprocess_reference(mu: torch.Tensor, mask: torch.Tensor, n_pad: i
 
 def explore_postprocess(mu: torch.Tensor, mask: torch.Tensor, n_pad: int, warmup: bool, rand_mu: float,
                         rand_sigma: float, seed: int, step: int, threshold: float = 0.1, passes: int = 2,
-                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """mu [E, A] actor output, mask [E, A] -> post-processed actions [E, A] (float32)."""
+                        out: Optional[torch.Tensor] = None, topo: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """mu [E, A] actor output -> post-processed actions [E, A] (float32).  ``mask``: [E, A] per-env
+    masks, or with ``topo`` [E] the per-topology table [T, A] (row ``topo[e]`` masks env e)."""
     if mu.is_cuda:
         from gsc_amd.native import load
         nat = load()
         E, A = mu.shape
         mu = mu.contiguous().float()
         mask = mask.contiguous().float()
+        if topo is not None:
+            topo = topo.to(torch.int64).contiguous()
+        else:
+            assert mask.shape[0] == E
         if out is None:
             out = torch.empty(E, A, device=mu.device, dtype=torch.float32)
-        nat.explore_postprocess(mu.data_ptr(), mask.data_ptr(), out.data_ptr(), E, A, n_pad, int(warmup),
-                                float(rand_mu), float(rand_sigma), int(seed) & 0xffffffff, int(step),
-                                float(threshold), int(passes), torch.cuda.current_stream(mu.device).cuda_stream)
+        nat.explore_postprocess(mu.data_ptr(), mask.data_ptr(), topo.data_ptr() if topo is not None else 0,
+                                out.data_ptr(), E, A, n_pad, int(warmup), float(rand_mu), float(rand_sigma),
+                                int(seed) & 0xffffffff, int(step), float(threshold), int(passes),
+                                torch.cuda.current_stream(mu.device).cuda_stream)
         return out
+    if topo is not None:
+        mask = mask.index_select(0, topo.to(torch.int64))
     g = torch.Generator(device=mu.device)
     g.manual_seed((int(seed) * 1000003 + int(step)) & 0x7fffffffffffffff)
     return explore_postprocess_reference(mu, mask, n_pad, warmup, rand_mu, rand_sigma, g, threshold, passes)

@@ -161,7 +161,7 @@ def _resume_worker(rank, port, out_dir):
     b.train(1)
     torch.save({"a_states": a.sim.states.clone(), "b_states": b.sim.states.clone(),
                 "a_actor": a.learner.actor_flat.flat.clone(), "b_actor": b.learner.actor_flat.flat.clone(),
-                "a_rng": a.trainer.replay.gen.get_state(), "b_rng": b.trainer.replay.gen.get_state()},
+                "a_rng": a.trainer.replay.rng_state(), "b_rng": b.trainer.replay.rng_state()},
                os.path.join(out_dir, f"res{rank}.pt"))
     shutdown()
 

@@ -113,3 +113,23 @@ def test_native_update_graphed_matches_eager():
     assert torch.equal(g1.actor_flat.flat, g2.actor_flat.flat)
     assert torch.equal(g1.critic_flat.flat, g2.critic_flat.flat)
     assert torch.equal(g1.target_actor_flat.flat, g2.target_actor_flat.flat)
+
+
+@pytest.mark.parametrize("T", [1, 2])
+def test_native_act_matches_fp32_module(T):
+    """Acting forward on the native kernels (embedder, folded mask block, hidden, masked output)
+    against the fp32 PyTorch actor on the same weights."""
+    cfg = _cfg()
+    ref, gpu = _learners(cfg, T)
+    E = 300
+    gpu.enable_native_act(E)
+    assert gpu._act_native is not None
+    b = _batch(E, T, "cpu", seed=5)
+    with torch.no_grad():
+        want = ref.actor(b.obs, b.topo, ref.graphs, ref.masks)
+    got = gpu.act(b.obs.cuda().contiguous(), b.topo.cuda()).cpu()
+    err = ((got - want).norm() / want.norm()).item()
+    assert err < 0.02, err
+    # masked entries (padding nodes / other topologies' rows) are exactly zero
+    m = ref.masks[b.topo]
+    assert torch.equal(got * (1 - m), torch.zeros_like(got))
