@@ -179,6 +179,44 @@ void replay_advance(bool device, uintptr_t state, int E, long long cap, uintptr_
   check_launch();
 }
 
+// ---- trainer metrics: acc[0..3] += (sum succ, sum drop, sum return of finished episodes, finished) ----
+__global__ __launch_bounds__(256) void step_metrics_kernel(const float* __restrict__ stats, int nstats,
+                                                           const float* __restrict__ ep_return,
+                                                           const uint8_t* __restrict__ done, int E, double* acc) {
+  __shared__ double red[4][256];
+  double v[4] = {0, 0, 0, 0};
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    v[0] += stats[(long)e * nstats];
+    v[1] += stats[(long)e * nstats + 1];
+    if (done[e]) { v[2] += ep_return[e]; v[3] += 1.0; }
+  }
+  for (int j = 0; j < 4; ++j) red[j][threadIdx.x] = v[j];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int j = 0; j < 4; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) acc[threadIdx.x] += red[threadIdx.x][0];
+}
+
+void step_metrics(bool device, uintptr_t stats, int nstats, uintptr_t ep_return, uintptr_t done, int E, uintptr_t acc,
+                  uintptr_t stream) {
+  if (!device) {
+    double v[4] = {0, 0, 0, 0};
+    for (int e = 0; e < E; ++e) {
+      v[0] += ptr<const float>(stats)[(long)e * nstats];
+      v[1] += ptr<const float>(stats)[(long)e * nstats + 1];
+      if (ptr<const uint8_t>(done)[e]) { v[2] += ptr<const float>(ep_return)[e]; v[3] += 1.0; }
+    }
+    for (int j = 0; j < 4; ++j) ptr<double>(acc)[j] += v[j];
+    return;
+  }
+  hipLaunchKernelGGL(step_metrics_kernel, dim3(1), dim3(256), 0, stream_of(stream), ptr<const float>(stats), nstats,
+                     ptr<const float>(ep_return), ptr<const uint8_t>(done), E, ptr<double>(acc));
+  check_launch();
+}
+
 int replay_index_host(uint32_t seed, long long draw, int b, long long pos, long long full, long long cap) {
   return replay_index(seed, draw, b, pos, full, cap);
 }
@@ -189,6 +227,7 @@ void register_replay(py::module_& m) {
   m.def("replay_insert", &replay_insert);
   m.def("replay_advance", &replay_advance);
   m.def("replay_index", &replay_index_host, "one sampled index (host; for tests)");
+  m.def("step_metrics", &step_metrics, "trainer metric accumulators (succ, drop, finished return, finished)");
 }
 
 }  // namespace gsc

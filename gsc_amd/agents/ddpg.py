@@ -222,23 +222,26 @@ class DDPGLearner:
             return self._native.last_metrics()
         return {"qf1_loss": self._lq, "actor_loss": self._la, "qf1_values": self._qv}
 
-    def update_graphed(self, b: Batch, warmup: int = 2) -> None:
+    def update_graphed(self, b: Batch, warmup: int = 2, pre=None) -> None:
         """Same update, replayed from captured HIP graphs (``b`` must be the same static buffers on
         every call).  One process: one graph for the whole update.  Data parallel: four graphs with
         the gradient all-reduces issued eagerly between them (collectives stay out of capture); the
         critic all-reduce overlaps the actor-forward graph.  The first ``warmup`` calls run eagerly
-        (they are real updates) on a side stream."""
+        (they are real updates) on a side stream.  ``pre`` (e.g. the replay sampler filling ``b``)
+        runs first and is captured with the update."""
         inv_world = 1.0 / self.dist.world_size
         if self._graphs is None:
             if self._graph_warm < warmup:
                 s = torch.cuda.Stream(self.device)
                 s.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(s):
+                    if pre is not None:
+                        pre()
                     self.update(b)
                 torch.cuda.current_stream(self.device).wait_stream(s)
                 self._graph_warm += 1
                 return
-            self._capture(b, inv_world)
+            self._capture(b, inv_world, pre)
         if len(self._graphs) == 1:
             self._graphs[0].replay()
         else:
@@ -256,10 +259,13 @@ class DDPGLearner:
         self.updates += 1
         self.last = self._metrics_now()
 
-    def _capture(self, b: Batch, inv_world: float) -> None:
+    def _capture(self, b: Batch, inv_world: float, pre=None) -> None:
         # thread-local capture: the RCCL watchdog thread keeps querying its events while we capture
         pool = torch.cuda.graph_pool_handle()
         stages = self._stages(b, inv_world)
+        if pre is not None:
+            s1 = stages[0]
+            stages[0] = lambda: (pre(), s1())
         graphs = []
         groups = [stages] if self.dist.world_size == 1 else [[f] for f in stages]
         for grp in groups:
@@ -358,10 +364,8 @@ class BatchedTrainer:
         if self.device.type == "cuda":
             self.learner.enable_native_act(self.E)
         # device-side metric accumulators (read back only when logging)
-        self.acc_succ = torch.zeros((), dtype=torch.float64, device=self.device)
-        self.acc_drop = torch.zeros((), dtype=torch.float64, device=self.device)
-        self.acc_return = torch.zeros((), dtype=torch.float64, device=self.device)
-        self.acc_episodes = torch.zeros((), dtype=torch.float64, device=self.device)
+        # [succ, drop, return of finished episodes, finished episodes] (one native kernel per step)
+        self.acc = torch.zeros(4, dtype=torch.float64, device=self.device)
         self.episode_returns: List[float] = []
         self.graphed = bool(tcfg.cuda_graphs and self.device.type == "cuda")
         self._batch = None
@@ -430,11 +434,10 @@ class BatchedTrainer:
         with trace_range("replay"):
             self.replay.add(obs, topo, act, out.reward, out.next_obs, out.done)
         st = out.stats
-        self.acc_succ += st[:, 0].sum()
-        self.acc_drop += st[:, 1].sum()
-        d = out.done.to(torch.float64)
-        self.acc_return += (out.ep_return.to(torch.float64) * d).sum()
-        self.acc_episodes += d.sum()
+        self.replay.nat.step_metrics(self.device.type == "cuda", st.data_ptr(), st.shape[1], out.ep_return.data_ptr(),
+                                     out.done.data_ptr(), self.E, self.acc.data_ptr(),
+                                     torch.cuda.current_stream(self.device).cuda_stream
+                                     if self.device.type == "cuda" else 0)
 
     def _flush_pending(self) -> None:
         if self._pending is not None:
@@ -508,19 +511,19 @@ class BatchedTrainer:
             if self.graphed:
                 if self._batch is None:
                     self._batch = self.replay.empty_batch(self.batch_size)
-                self.replay.sample(self.batch_size, out=self._batch)
-                self.learner.update_graphed(self._batch)
+                    B, out = self.batch_size, self._batch
+                    self._sampler = lambda: self.replay.sample(B, out=out)
+                self.learner.update_graphed(self._batch, pre=self._sampler)
             else:
                 self.learner.update(self.replay.sample(self.batch_size))
 
     def metrics(self, reset: bool = True) -> dict:
         self.flush()
-        vals = torch.stack([self.acc_succ, self.acc_drop, self.acc_return, self.acc_episodes])
+        vals = self.acc.clone()
         allreduce_sum_(vals)
         s, d, r, e = [float(v) for v in vals.cpu()]
         if reset:
-            for t in (self.acc_succ, self.acc_drop, self.acc_return, self.acc_episodes):
-                t.zero_()
+            self.acc.zero_()
         out = {"success_ratio": s / (s + d) if s + d > 0 else 0.0, "succ": s, "drop": d, "episodes": e,
                "mean_episode_return": r / e if e > 0 else float("nan")}
         for k, v in self.learner.last.items():

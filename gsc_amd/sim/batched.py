@@ -246,7 +246,7 @@ class BatchedSimulator:
                       actions.shape[1], obs.data_ptr(), next_obs.data_ptr(), reward.data_ptr(),
                       done_u8.data_ptr(), stats.data_ptr(), ep_return.data_ptr(), self.E, self._stream(),
                       self.prof.data_ptr() if (self.prof is not None and self.is_device) else 0)
-        done = done_u8.bool()
+        done = done_u8.view(torch.bool)  # 0/1 bytes: zero-copy
         # envs that finished were reset onto their scheduled topology
         torch.where(done, self.topo_next, self.topo_cur, out=self.topo_cur)
         return SimStepOut(obs, next_obs, reward, done, stats, ep_return)
