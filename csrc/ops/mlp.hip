@@ -315,20 +315,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* slabs, 
 }
 
 // out[t][n] = sum_a x[t][a] W[n][a]: the per-topology fold of a 0/1 mask block of a first-layer weight
-// (x = masks, W = the mask columns) and small GEMVs (x = a bias vector).  One wave per (t, n).
+// (x = masks, W = the mask columns) and small GEMVs (x = a bias vector).  One workgroup per (t, n):
+// 256 lanes over a, fixed-order tree reduction (deterministic).
 __global__ __launch_bounds__(256) void rowdot_kernel(const float* x, long ldx, int T, const __hip_bfloat16* W,
                                                      long ldw, int N, int A, float* out, long ldo) {
-  const int lane = threadIdx.x & 63;
-  const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gw >= (long)T * N) return;
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long gw = blockIdx.x;
   const int t = (int)(gw / N), n = (int)(gw - (long)t * N);
   const float* xr = x + (long)t * ldx;
   const __hip_bfloat16* wr = W + (long)n * ldw;
   float s = 0.f;
-  for (int a = lane; a < A; a += 64) s += xr[a] * __bfloat162float(wr[a]);
+  for (int a = threadIdx.x; a < A; a += 256) s += xr[a] * __bfloat162float(wr[a]);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-  if (lane == 0) out[(long)t * ldo + n] = s;
+  if (lane == 0) red[wv] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[(long)t * ldo + n] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -617,8 +620,9 @@ void cast2d(uintptr_t src, long lds_, uintptr_t dst, long ldd, int R, int C, uin
 
 void rowdot(uintptr_t x, long ldx, int T, uintptr_t W, long ldw, int N, int A, uintptr_t out, long ldo,
             uintptr_t stream) {
-  const long waves = (long)T * N;
-  hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream_of(stream),
+  const long blocks = (long)T * N;
+  if (blocks <= 0) return;
+  hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)blocks), dim3(256), 0, stream_of(stream),
                      ptr<const float>(x), ldx, T, ptr<const __hip_bfloat16>(W), ldw, N, A, ptr<float>(out), ldo);
   check_launch();
 }

@@ -34,14 +34,13 @@ GSC_HD int replay_index(uint32_t seed, long long draw, int b, long long pos, lon
   return (int)((u * (uint64_t)pos) >> 32);
 }
 
-// ---- sample: one workgroup draws every index, then advances the draw counter --------------------
-__global__ __launch_bounds__(1024) void replay_index_kernel(ReplayState* st, uint32_t seed, int B, long long cap,
-                                                            int32_t* idx) {
-  const long long pos = st->pos, full = st->full, draw = st->draws;
-  for (int b = threadIdx.x; b < B; b += blockDim.x) idx[b] = replay_index(seed, draw, b, pos, full, cap);
-  __syncthreads();
-  if (threadIdx.x == 0) st->draws = draw + 1;
+// ---- sample: every thread draws one index; the draw counter advances in a second kernel ---------
+__global__ __launch_bounds__(256) void replay_index_kernel(const ReplayState* st, uint32_t seed, int B, long long cap,
+                                                           int32_t* idx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) idx[b] = replay_index(seed, st->draws, b, st->pos, st->full, cap);
 }
+__global__ void replay_draw_done_kernel(ReplayState* st) { st->draws += 1; }
 
 // rows of `row_bytes` in granules of G bytes: dst[b] = src[idx[b]]
 template <class G>
@@ -106,8 +105,9 @@ void replay_sample_indices(bool device, uintptr_t state, uint32_t seed, int B, l
     host_indices(ptr<ReplayState>(state), seed, B, cap, ptr<int32_t>(idx));
     return;
   }
-  hipLaunchKernelGGL(replay_index_kernel, dim3(1), dim3(1024), 0, stream_of(stream), ptr<ReplayState>(state), seed, B,
-                     cap, ptr<int32_t>(idx));
+  hipLaunchKernelGGL(replay_index_kernel, dim3((B + 255) / 256), dim3(256), 0, stream_of(stream),
+                     ptr<const ReplayState>(state), seed, B, cap, ptr<int32_t>(idx));
+  hipLaunchKernelGGL(replay_draw_done_kernel, dim3(1), dim3(1), 0, stream_of(stream), ptr<ReplayState>(state));
   check_launch();
 }
 

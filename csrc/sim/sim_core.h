@@ -228,6 +228,44 @@ GSC_HD int rng_int(Env& S, int n) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Wave-parallel helpers (device): the handlers run wave-uniform (every lane holds the same state),
+// so a loop over nodes / destinations can spread over the 64 lanes and reduce with DPP.
+// ------------------------------------------------------------------------------------------------
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ int wave_lane() { return (int)__lane_id(); }
+// DPP row_shr:1,2,4,8 + row_bcast:15,31: lane 63 ends up with the reduction of all 64 lanes
+template <class OP>
+__device__ __forceinline__ uint32_t dpp_red_u32(uint32_t v, uint32_t ident, OP op) {
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x111, 0xF, 0xF, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x112, 0xF, 0xF, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x114, 0xF, 0xF, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x118, 0xF, 0xF, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x142, 0xA, 0xF, false));
+  v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ int wave_sum_i32(int v) {
+  return (int)dpp_red_u32((uint32_t)v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+}
+// max of a double over the wave (exact), broadcast to every lane
+__device__ __forceinline__ double wave_max_f64(double v) {
+  const int ilo = 0, ihi = (int)0xFFF00000u;  // -inf
+#define GSC_DPP_MAXD(ctrl, rm)                                                                  \
+  {                                                                                            \
+    const int lo = __builtin_amdgcn_update_dpp(ilo, __double2loint(v), ctrl, rm, 0xF, false);  \
+    const int hi = __builtin_amdgcn_update_dpp(ihi, __double2hiint(v), ctrl, rm, 0xF, false);  \
+    const double o = __hiloint2double(hi, lo);                                                 \
+    v = o > v ? o : v;                                                                         \
+  }
+  GSC_DPP_MAXD(0x111, 0xF) GSC_DPP_MAXD(0x112, 0xF) GSC_DPP_MAXD(0x114, 0xF) GSC_DPP_MAXD(0x118, 0xF)
+  GSC_DPP_MAXD(0x142, 0xA) GSC_DPP_MAXD(0x143, 0xC)
+#undef GSC_DPP_MAXD
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
+                          __builtin_amdgcn_readlane(__double2loint(v), 63));
+}
+#endif
+
+// ------------------------------------------------------------------------------------------------
 // Event / process primitives (SimPy contract)
 // ------------------------------------------------------------------------------------------------
 GSC_HD void push_event(Env& S, double t, uint32_t prio, int16_t proc) {
@@ -292,15 +330,31 @@ GSC_HD void free_flow(Env& S, int fid) { S.flow_free[S.h->flow_top++] = (int16_t
 // ------------------------------------------------------------------------------------------------
 // Metrics hooks (reference coordsim/metrics/metrics.py)
 // ------------------------------------------------------------------------------------------------
-GSC_HD_CALL void reset_run_metrics(Env& S, const SimConst& K, int n) {
+// Make lane-parallel LDS writes of this wave visible to the (uniform) reads that follow.
+GSC_HD void lanes_sync(int ls) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (ls > 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+#else
+  (void)ls;
+#endif
+}
+
+// l0 / ls: this lane and the lane count sharing the work (device: wave_lane(), 64; host or a
+// single active lane: 0, 1)
+GSC_HD_CALL void reset_run_metrics(Env& S, const SimConst& K, int n, int l0, int ls) {
   Header* h = S.h;
   h->run_gen = h->run_processed = h->run_dropped = 0;
   h->run_e2e = h->run_max_e2e = h->run_total_path_delay = h->run_avg_path_delay = 0.0;
   const int N = S.d.N, Sd = S.d.S, C = S.d.C;
-  for (int v = 0; v < N; ++v) { S.run_drop_node[v] = 0; S.max_usage[v] = 0.0; }
-  for (int i = 0; i < N * Sd; ++i) S.proc_traffic[i] = 0.0;
-  for (int i = 0; i < N * C * Sd; ++i) S.requested[i] = 0.0;
-  for (int i = 0; i < N * C * Sd * N; ++i) S.wrr[i] = 0;
+  for (int v = l0; v < N; v += ls) { S.run_drop_node[v] = 0; S.max_usage[v] = 0.0; }
+  for (int i = l0; i < N * Sd; i += ls) S.proc_traffic[i] = 0.0;
+  for (int i = l0; i < N * C * Sd; i += ls) S.requested[i] = 0.0;
+  for (int i = l0; i < N * C * Sd * N; i += ls) S.wrr[i] = 0;
+  lanes_sync(ls);
   (void)K; (void)n;
 }
 
@@ -420,17 +474,36 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
   const int row = ((node * C + sfc) * Sd + sf) * N;
   const double* p = S.sched + row;
   int32_t* cnt = S.wrr + row;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // destinations over the lanes: total by a DPP sum, the first destination with the largest
+  // (weight - served ratio) by a DPP max + ballot (== the serial strict-greater scan)
+  const int lane = wave_lane();
+  int part = 0;
+  for (int d = lane; d < n; d += 64) part += cnt[d];
+  const int total = wave_sum_i32(part);
+  double lbest = -1e300;
+  int lidx = 0x7fffffff;
+  for (int d = lane; d < n; d += 64) {
+    const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0;
+    const double diff = p[d] > 0 ? p[d] - ratio : -1.0;
+    if (diff > lbest) { lbest = diff; lidx = d; }
+  }
+  const double best_v = wave_max_f64(lbest);
+  // lanes holding the max: the smallest destination index among them
+  const uint32_t cand = lbest == best_v ? (uint32_t)lidx : 0x7fffffffu;
+  int best = (int)dpp_red_u32(cand, 0x7fffffffu, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+  best = GSC_UNI(best);
+#else
   int total = 0;
   for (int d = 0; d < n; ++d) total += cnt[d];
   int best = 0;
   double best_v = -1e300;
-  const double inv_total = total > 0 ? 1.0 : 0.0;
   for (int d = 0; d < n; ++d) {
-    const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0 * inv_total;
+    const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0;
     const double diff = p[d] > 0 ? p[d] - ratio : -1.0;
     if (diff > best_v) { best_v = diff; best = d; }
   }
-  best = GSC_UNI(best);
+#endif
   cnt[best]++;
   proc_return(S, pid, (int16_t)best);
 }
@@ -657,7 +730,11 @@ GSC_HD_CALL void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid
       respawn_self(S, pid, W_INIT);
       return;
     default:  // W_INIT
-      reset_run_metrics(S, K, T.n);
+#if defined(__HIP_DEVICE_COMPILE__)
+      reset_run_metrics(S, K, T.n, wave_lane(), 64);
+#else
+      reset_run_metrics(S, K, T.n, 0, 1);
+#endif
       S.procs[pid].state = W_AFTER;
       timeout(S, pid, K.run_duration);
       return;
@@ -756,7 +833,8 @@ GSC_HD void remove_event(Env& S, int idx) {
 // ------------------------------------------------------------------------------------------------
 // Episode init / controller apply / observation + reward epilogue
 // ------------------------------------------------------------------------------------------------
-GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo, uint32_t seed, int episode) {
+GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo, uint32_t seed, int episode,
+                          int l0 = 0, int ls = 1) {
   Header* h = S.h;
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
   const double ewma = h->ewma_flows;
@@ -769,22 +847,22 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
   h->key0 = seed;
   h->key1 = K.same_seed_every_episode ? 0x5eedu : (0x5eedu ^ ((uint32_t)episode * 0x9E3779B9u));
   h->ctr = 0;
-  for (int v = 0; v < N; ++v) {
+  for (int v = l0; v < N; v += ls) {
     const double cap = v < n ? T.cap[v] : 0.0;
     S.node_cap[v] = cap;
     S.node_rem[v] = cap;
     S.inter_arr[v] = 0.0 / 0.0;  // NaN = None
     S.mmpp_state[v] = 0;
   }
-  for (int i = 0; i < N * Sd; ++i) { S.sf_present[i] = 0; S.placement[i] = 0; S.sf_load[i] = 0; S.sf_start[i] = 0; }
-  for (int i = 0; i < N * (Sd + 1); ++i) S.drop_locs[i] = 0;
-  for (int i = 0; i < N * C * Sd * N; ++i) S.sched[i] = 0.0;
-  for (int e = 0; e < S.d.E; ++e) { S.link_rem[e] = e < T.E ? T.edge_cap[e] : 0.0; S.link_passed[e] = 0.0; }
+  for (int i = l0; i < N * Sd; i += ls) { S.sf_present[i] = 0; S.placement[i] = 0; S.sf_load[i] = 0; S.sf_start[i] = 0; }
+  for (int i = l0; i < N * (Sd + 1); i += ls) S.drop_locs[i] = 0;
+  for (int i = l0; i < N * C * Sd * N; i += ls) S.sched[i] = 0.0;
+  for (int e = l0; e < S.d.E; e += ls) { S.link_rem[e] = e < T.E ? T.edge_cap[e] : 0.0; S.link_passed[e] = 0.0; }
   h->flow_top = S.d.flow_cap;
-  for (int i = 0; i < S.d.flow_cap; ++i) S.flow_free[i] = (int16_t)(S.d.flow_cap - 1 - i);
+  for (int i = l0; i < S.d.flow_cap; i += ls) S.flow_free[i] = (int16_t)(S.d.flow_cap - 1 - i);
   h->proc_top = S.d.proc_cap;
-  for (int i = 0; i < S.d.proc_cap; ++i) { S.proc_free[i] = (int16_t)(S.d.proc_cap - 1 - i); S.procs[i].type = P_FREE; }
-  reset_run_metrics(S, K, n);
+  for (int i = l0; i < S.d.proc_cap; i += ls) { S.proc_free[i] = (int16_t)(S.d.proc_cap - 1 - i); S.procs[i].type = P_FREE; }
+  reset_run_metrics(S, K, n, l0, ls);  // ends with lanes_sync
   // reference order: writer, (MMPP), (trace), arrivals; then one env.step()
   spawn(S, P_WRITER, W_BEGIN, -1, -1);
   if (K.use_states) {

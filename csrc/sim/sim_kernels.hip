@@ -46,7 +46,7 @@ struct SimArgs {
   long topo_stage;           // bytes of LDS reserved for the staged topology tables
   unsigned long long* prof;  // optional [E, 4] cycle counters: select, dispatch, merge, events (diagnostic)
   int prio;                  // wave priority of the step kernel (s_setprio), see sim_step_kernel
-  unsigned long long* prof_types;  // optional [E, 16, 2] dispatch cycles / count per process type
+  unsigned long long* prof_types;  // optional [E, 64, 2] dispatch cycles / count per (process type, state)
 };
 
 GSC_HD void step_epilogue(Env& S, const SimArgs& a, const SimConst& K, int env) {
@@ -247,24 +247,22 @@ __device__ __forceinline__ void rq_pop(RegQueue<QS>& q, double& t, int& proc) {
 }
 
 // Merge the events lane 0's handler appended to S.events (the inbox) into the register queue.
-template <int QS, bool UNI>
+template <int QS>
 __device__ __forceinline__ void rq_merge_inbox(RegQueue<QS>& q, Env& S, int lane) {
   const int nin = __builtin_amdgcn_readfirstlane(S.h->n_events);
   for (int i = 0; i < nin; ++i) {
     const Event e = S.events[i];
-    if (!rq_insert(q, e.t, e.key, e.proc, lane) && (UNI || lane == 0)) S.h->flags |= FLAG_EVENT_OVERFLOW;
+    if (!rq_insert(q, e.t, e.key, e.proc, lane)) S.h->flags |= FLAG_EVENT_OVERFLOW;
   }
-  if (UNI || lane == 0) {
-    if (q.n > S.h->max_events) S.h->max_events = q.n;
-    S.h->n_events = 0;
-  }
+  if (q.n > S.h->max_events) S.h->max_events = q.n;
+  S.h->n_events = 0;
   __builtin_amdgcn_wave_barrier();
 }
 
-// UNI: every lane runs the handlers on its own (identical) copy of the header and the same LDS
-// state, so loaded values are wave-uniform and control flow stays scalar; otherwise lane 0 alone
-// runs them (the other lanes idle under an exec mask).
-template <int QS, bool UNI>
+// Every lane runs the handlers on its own (identical) copy of the header and the same LDS state, so
+// loaded values are wave-uniform and control flow stays scalar; loops over nodes / destinations
+// inside a handler spread over the lanes (sim_core.h wave helpers).
+template <int QS>
 __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst& K, char* base, char* topo_lds,
                                                 int env, int lane) {
   Env S(base, a.L, a.D);
@@ -278,21 +276,19 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   // pending events -> sorted register queue; S.events then serves as the handlers' inbox
   RegQueue<QS> q;
   rq_init(q);
-  rq_merge_inbox<QS, UNI>(q, S, lane);
-  if (UNI) __syncthreads();  // every lane writes the same placement/sf tables: order the reads
-  if (UNI || lane == 0) {
-    controller_prologue(S, K, T);
-    schedule_stop(S, K);
-  }
+  rq_merge_inbox<QS>(q, S, lane);
+  __syncthreads();  // every lane writes the same placement/sf tables: order the reads
+  controller_prologue(S, K, T);
+  schedule_stop(S, K);
   __syncthreads();
-  rq_merge_inbox<QS, UNI>(q, S, lane);
+  rq_merge_inbox<QS>(q, S, lane);
   const bool prof = a.prof != nullptr;
   unsigned long long t_sel = 0, t_hdl = 0, t_mrg = 0, n_ev = 0;
   const unsigned long long t_begin = prof ? __builtin_amdgcn_s_memtime() : 0;
   for (long it = 0;; ++it) {
     const unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (q.n <= 0 || it > kMaxEventsPerStep) {
-      if (UNI || lane == 0) S.h->flags |= FLAG_BAD_STATE;
+      S.h->flags |= FLAG_BAD_STATE;
       break;
     }
     double et;
@@ -300,7 +296,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     rq_pop(q, et, ep);
     const unsigned long long t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (ep == kStopProc) {
-      if (UNI || lane == 0) S.h->now = et;
+      S.h->now = et;
       break;
     }
     // Lane 0 runs the handler, then keeps going while the smallest event the handler chain just
@@ -309,7 +305,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     // straight from the inbox without a round trip through the register queue.  Popping the
     // minimum of (queue U inbox) is exactly the full queue's order.
     int n_disp = 0;
-    if (UNI || lane == 0) {
+    {
       double t = et;
       int p = ep;
       // queue head = entry 0 of set 0, held by lane 0
@@ -319,12 +315,12 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
       for (;;) {
         S.h->now = t;
         const unsigned long long td = prof ? __builtin_amdgcn_s_memtime() : 0;
-        const int ptype = prof ? S.procs[p].type : 0;
+        const int ptype = prof ? S.procs[p].type * 4 + (S.procs[p].state < 3 ? S.procs[p].state : 3) : 0;
         dispatch(S, K, T, p);
         ++n_disp;
         if (a.prof_types && lane == 0) {
-          a.prof_types[((long)env * 16 + ptype) * 2] += __builtin_amdgcn_s_memtime() - td;
-          a.prof_types[((long)env * 16 + ptype) * 2 + 1] += 1;
+          a.prof_types[((long)env * 64 + ptype) * 2] += __builtin_amdgcn_s_memtime() - td;
+          a.prof_types[((long)env * 64 + ptype) * 2 + 1] += 1;
         }
         const int ni = S.h->n_events;
         // pending-event high-water mark of the full queue (= host path's count after its last push)
@@ -347,7 +343,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const unsigned long long t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
-    rq_merge_inbox<QS, UNI>(q, S, lane);
+    rq_merge_inbox<QS>(q, S, lane);
     if (prof) {
       const unsigned long long t3 = __builtin_amdgcn_s_memtime();
       t_sel += t1 - t0;
@@ -396,9 +392,9 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   write_obs_wave(S, K, T.n, a.next_obs + env * ostride, done ? nullptr : a.obs + env * ostride, lane);
   if (done) {
     __syncthreads();
-    if (lane == 0) {
+    {  // every lane (wave-uniform header copies), init loops spread over the lanes
       const int topo = a.topo_next[env];
-      env_init(S, K, a.topos[topo], topo, a.seeds[env], S.h->episode + 1);
+      env_init(S, K, a.topos[topo], topo, a.seeds[env], S.h->episode + 1, lane, 64);
     }
     __syncthreads();
     write_obs_wave(S, K, a.topos[a.topo_next[env]].n, a.obs + env * ostride, nullptr, lane);
@@ -407,7 +403,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   __syncthreads();
 }
 
-template <int QSETS, bool LDS_STATE, bool UNI>
+template <int QSETS, bool LDS_STATE>
 __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int env = blockIdx.x;
@@ -427,11 +423,11 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   if constexpr (LDS_STATE) {
     copy16(state_lds, g, a.state_bytes, lane);
     __syncthreads();
-    device_step_env<QSETS, UNI>(a, *Ks, state_lds, topo_lds, env, lane);
+    device_step_env<QSETS>(a, *Ks, state_lds, topo_lds, env, lane);
     copy16(g, state_lds, a.state_bytes, lane);
   } else {
     __syncthreads();
-    device_step_env<QSETS, UNI>(a, *Ks, g, topo_lds, env, lane);
+    device_step_env<QSETS>(a, *Ks, g, topo_lds, env, lane);
   }
 }
 
@@ -530,14 +526,10 @@ class SimContext {
       qsets_ = D_.event_cap <= 64 ? 1 : (D_.event_cap <= 128 ? 2 : (D_.event_cap <= 256 ? 4 : 8));
       if (need > 65536) {
         const void* fns[] = {
-            (const void*)sim_step_kernel<1, true, false>, (const void*)sim_step_kernel<2, true, false>,
-            (const void*)sim_step_kernel<4, true, false>, (const void*)sim_step_kernel<8, true, false>,
-            (const void*)sim_step_kernel<1, false, false>, (const void*)sim_step_kernel<2, false, false>,
-            (const void*)sim_step_kernel<4, false, false>, (const void*)sim_step_kernel<8, false, false>,
-            (const void*)sim_step_kernel<1, true, true>, (const void*)sim_step_kernel<2, true, true>,
-            (const void*)sim_step_kernel<4, true, true>, (const void*)sim_step_kernel<8, true, true>,
-            (const void*)sim_step_kernel<1, false, true>, (const void*)sim_step_kernel<2, false, true>,
-            (const void*)sim_step_kernel<4, false, true>, (const void*)sim_step_kernel<8, false, true>};
+            (const void*)sim_step_kernel<1, true>, (const void*)sim_step_kernel<2, true>,
+            (const void*)sim_step_kernel<4, true>, (const void*)sim_step_kernel<8, true>,
+            (const void*)sim_step_kernel<1, false>, (const void*)sim_step_kernel<2, false>,
+            (const void*)sim_step_kernel<4, false>, (const void*)sim_step_kernel<8, false>};
         for (auto f : fns) GSC_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
       }
     }
@@ -576,12 +568,9 @@ class SimContext {
     if (device_) {
       const size_t lds = const_stage_bytes() + topo_stage_ + (use_lds_ ? (size_t)L_.total : 0);
       const hipStream_t st = stream_of(stream);
-      static const bool uni = getenv("GSC_SIM_UNIFORM") ? atoi(getenv("GSC_SIM_UNIFORM")) != 0 : true;
-#define GSC_LAUNCH_SIM2(QS, U)                                                                     \
-  if (use_lds_) hipLaunchKernelGGL((sim_step_kernel<QS, true, U>), dim3(E), dim3(64), lds, st, a); \
-  else hipLaunchKernelGGL((sim_step_kernel<QS, false, U>), dim3(E), dim3(64), lds, st, a);
-#define GSC_LAUNCH_SIM(QS) \
-  if (uni) { GSC_LAUNCH_SIM2(QS, true) } else { GSC_LAUNCH_SIM2(QS, false) }
+#define GSC_LAUNCH_SIM(QS)                                                                       \
+  if (use_lds_) hipLaunchKernelGGL((sim_step_kernel<QS, true>), dim3(E), dim3(64), lds, st, a); \
+  else hipLaunchKernelGGL((sim_step_kernel<QS, false>), dim3(E), dim3(64), lds, st, a);
       switch (qsets_) {
         case 1: GSC_LAUNCH_SIM(1) break;
         case 2: GSC_LAUNCH_SIM(2) break;
@@ -589,7 +578,6 @@ class SimContext {
         default: GSC_LAUNCH_SIM(8) break;
       }
 #undef GSC_LAUNCH_SIM
-#undef GSC_LAUNCH_SIM2
       check_launch();
     } else {
       parallel_for(E, host_threads_, [&](int e) { host_step_env(a, e); });

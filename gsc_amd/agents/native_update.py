@@ -129,7 +129,7 @@ class NativeDDPGUpdate:
         self.dmc = mk(c1, hl + 1)
         self.splits = None                                   # auto split-K for the batch reductions
         self.slabs = mk(16 << 20)                            # split-K slabs (64 MB; bounds the split count)
-        self.head_blocks = 64
+        self.head_blocks = max(64, min(256, -(-B // 64)))    # one block per CU (>= 16 rows per wave)
         cm = self.critic.width(self.critic.nh - 1)
         self.part = mk(self.head_blocks * (cm + 3))
         self.metrics = mk(4)                                 # qf1_loss, qf1_values, actor_loss, -
@@ -233,13 +233,11 @@ class NativeDDPGUpdate:
         nw = self.head_blocks
         s = self._stream()
         part = self.part.data_ptr()
-        if mode == 1:  # dW | db of the output layer (contiguous in the grad buffer), loss, q mean
+        if mode == 1:  # dW | db of the output layer (contiguous in the grad buffer); loss, q mean
             gw = net.gw(net.nh)
-            self.nat.splitk_reduce(part, C + 3, nw, 1, C, C + 3, gw.data_ptr(), C, 1.0, 0, s)
-            self.nat.splitk_reduce(part + 4 * C, C + 3, nw, 1, 1, C + 3, net.gb(net.nh).data_ptr(), 1, 1.0, 0, s)
-            self.nat.splitk_reduce(part + 4 * (C + 1), C + 3, nw, 1, 1, C + 3, self.metrics.data_ptr(), 1,
-                                   1.0 / self.B, 0, s)
-            self.nat.splitk_reduce(part + 4 * (C + 2), C + 3, nw, 1, 1, C + 3, self.metrics.data_ptr() + 4, 1,
+            assert net.gb(net.nh).data_ptr() == gw.data_ptr() + 4 * C
+            self.nat.splitk_reduce(part, C + 3, nw, 1, C + 1, C + 3, gw.data_ptr(), C + 1, 1.0, 0, s)
+            self.nat.splitk_reduce(part + 4 * (C + 1), C + 3, nw, 1, 2, C + 3, self.metrics.data_ptr(), 2,
                                    1.0 / self.B, 0, s)
         else:          # actor loss = -mean q
             self.nat.splitk_reduce(part + 4 * (C + 2), C + 3, nw, 1, 1, C + 3, self.metrics.data_ptr() + 8, 1,

@@ -233,8 +233,9 @@ class BatchedSimulator:
         return self.obs
 
     def enable_profiling(self, on: bool = True) -> None:
-        """Accumulate per-env cycle counters (event selection / handlers / total / events) in ``self.prof``."""
-        self.prof = torch.zeros(self.E * 4 + self.E * 32, dtype=torch.int64, device=self.device) if on else None
+        """Accumulate per-env cycle counters in ``self.prof``: [E, 4] (event selection / handlers / merge / events)
+        then [E, 64, 2] handler cycles / dispatches per (process type, resume state)."""
+        self.prof = torch.zeros(self.E * 4 + self.E * 128, dtype=torch.int64, device=self.device) if on else None
 
     def step(self, actions: torch.Tensor, buffer_set: int = 0) -> SimStepOut:
         if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():

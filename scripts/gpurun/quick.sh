@@ -1,0 +1,9 @@
+#!/bin/bash
+# GPU: learner tests + GEMM epilogue micro-bench + GNN bench + bench.py (30 steps)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest $R/tests/test_gpu_learner.py $R/tests/test_gpu_replay.py $R/tests/test_gpu_graphs.py -x -q --timeout 200 --timeout-method thread > $OUT/quick_tests.log 2>&1 &&
+timeout -k 10 120 python $R/scripts/gemm_epi_bench.py > $OUT/gemm_epi.txt 2>&1 &&
+timeout -k 10 300 python $R/bench.py --steps 30 --warmup 5 > $OUT/bench.log 2>&1

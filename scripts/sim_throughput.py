@@ -52,12 +52,13 @@ print(f"envs={args.envs} steps={args.steps} state_bytes={sim.state_bytes} lds={s
 if args.profile:
     pr = sim.prof.double().cpu()
     p = pr[: args.envs * 4].view(-1, 4).sum(0)
-    ty = pr[args.envs * 4:].view(args.envs, 16, 2).sum(0)
+    ty = pr[args.envs * 4:].view(args.envs, 64, 2).sum(0)
     names = ["free", "writer", "mmpp", "trace", "arrival", "handle", "decide", "forward", "process", "request",
              "finish", "retlink"]
-    for i, nm in enumerate(names):
+    tot = ty[:, 0].sum()
+    for i in range(64):
         if ty[i, 1] > 0:
-            print(f"  {nm:8s} events/env-step={ty[i, 1] / (args.envs * args.steps):7.1f} "
-                  f"cycles/dispatch={ty[i, 0] / ty[i, 1]:7.0f} share={ty[i, 0] / ty[:, 0].sum():.2f}")
+            print(f"  {names[i // 4]:8s} state {i % 4} events/env-step={ty[i, 1] / (args.envs * args.steps):7.1f} "
+                  f"cycles/dispatch={ty[i, 0] / ty[i, 1]:7.0f} share={ty[i, 0] / tot:.3f}")
     print(f"cycles/event: select={p[0] / p[3]:.0f} dispatch={p[1] / p[3]:.0f} merge={p[2] / p[3]:.0f} "
           f"events/env-step={p[3] / (args.envs * args.steps):.0f}")
