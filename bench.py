@@ -27,6 +27,12 @@ sys.path.insert(0, ROOT)
 BASELINE_ENV_STEPS_PER_S = 57.4  # reference env-only throughput, Abilene + abc, 1 CPU core
 
 PRESETS = {
+    "line": dict(network=["configs/networks/line/line4-in1-cap1-delay10.graphml"],
+                 service="configs/service_functions/abc.yaml",
+                 sim_config="configs/config/simulator/sample_config.yaml",
+                 agent_config="configs/config/agent/sample_agent_flat.yaml", envs=1, batch=100, period=0,
+                 device="cpu",
+                 model="flat 2-layer MLP DDPG (graph_mode: False, actor/critic [64, 64]), 4-node line, 1 SFC (3 SFs)"),
     "abilene": dict(network=["configs/networks/abilene/abilene-in4-rand-cap1-2.graphml"],
                     service="configs/service_functions/abc.yaml",
                     sim_config="configs/config/simulator/sample_config.yaml",
@@ -54,7 +60,8 @@ def main():
     ap.add_argument("--batch-size", type=int, default=None, help="learner batch (default 100 * envs)")
     ap.add_argument("--updates-per-step", type=int, default=1)
     ap.add_argument("--preset", choices=sorted(PRESETS), default="abilene",
-                    help="abilene: BASELINE configs 2/3 (headline); syn50: config 4 (50-node + 3 SFCs + trace); "
+                    help="abilene: BASELINE configs 2/3 (headline); line: config 1 (4-node line, flat MLP, 1 CPU env); "
+                         "syn50: config 4 (50-node + 3 SFCs + trace); "
                          "syn200: config 5 (200-node topologies switched by the network scheduler)")
     ap.add_argument("--network", default=None, help="override the preset's network(s) (comma-separated)")
     ap.add_argument("--service", default=None)
@@ -86,7 +93,7 @@ def main():
         args.envs = pre["envs"]
     if args.batch_size is None:
         args.batch_size = pre["batch"]
-    device_type = args.device or ("cuda" if torch.cuda.is_available() else "cpu")
+    device_type = args.device or pre.get("device") or ("cuda" if torch.cuda.is_available() else "cpu")
     info = init_distributed(device_type)
     if device_type == "cuda":
         dev_index = info.local_rank % torch.cuda.device_count()
@@ -146,7 +153,7 @@ def main():
         rec = {
             "metric": "env-steps/sec (whole node) + flow success ratio, Abilene SFC" if args.preset == "abilene"
             else f"env-steps/sec (whole node) + flow success ratio, {args.preset} (BASELINE config "
-                 f"{'4' if args.preset == 'syn50' else '5'})",
+                 f"{ {'line': '1', 'syn50': '4', 'syn200': '5'}[args.preset] })",
             "value": float(f"{value:.6g}"),
             "unit": "env-steps/s",
             "n_gpus": info.world_size,

@@ -83,7 +83,7 @@ class DDPGLearner:
         self.compose_actor_critic = os.environ.get("GSC_COMPOSE", "1") != "0"
         # GPU: the update runs on hand-written kernels only (native_update.py); GSC_NATIVE_LEARNER=0
         # selects the autograd + PyTorch path (the CPU path, and the reference for the GPU tests)
-        self.native_ok = (self.device.type == "cuda" and self.amp and not self.actor.squash
+        self.native_ok = (self.device.type == "cuda" and self.amp and not self.actor.squash and self.actor.graph_mode
                           and os.environ.get("GSC_NATIVE_LEARNER", "1") != "0")
         self._native = None
         self._act_native = None
@@ -141,7 +141,7 @@ class DDPGLearner:
     def _composed(self) -> bool:
         # one topology and at least one actor hidden layer: critic(obs, actor(obs)) re-associated
         return (self.compose_actor_critic and self.masks.shape[0] == 1 and len(self.actor.mlp.layers) > 1
-                and not self.actor.squash)
+                and not self.actor.squash and self.actor.graph_mode)
 
     def _stage_actor_fwd(self, b: Batch) -> None:
         with self._autocast():
@@ -497,11 +497,14 @@ class BatchedTrainer:
                 with trace_range("learn"):
                     self._learn()
         self._obs_bufs[k ^ 1].copy_(out.obs)
-        if (self.global_step + 1) % self.sim.episode_steps == 0:
+        episode_end = (self.global_step + 1) % self.sim.episode_steps == 0
+        if episode_end:
             self.episode += 1
             self.topo = self.sim.topo_next.to(torch.int64).clone()
         self.global_step += 1
-        if self.t.check_every and self.global_step % self.t.check_every == 0:
+        # pool overflow (flows / processes / events dropped) fails the run at the latest at the end of
+        # the episode it happened in (one flag read per episode), or every check_every steps
+        if episode_end or (self.t.check_every and self.global_step % self.t.check_every == 0):
             self.sim.check_flags()
 
     def _learn(self) -> None:

@@ -124,9 +124,18 @@ class SimpleDDPG(RLSPAgent):
 
     # ------------------------------------------------------------------------------------------
     # acting
-    def _obs_tensor(self, obs: GraphObs):
+    def _node_rows(self, obs) -> torch.Tensor:
+        """[n, n_obs] node features of a GraphObs, or of the flat (feature-major) observation the
+        environment returns in flat mode (``graph_mode: False``)."""
+        if isinstance(obs, GraphObs):
+            return obs.x
+        flat = torch.as_tensor(np.asarray(obs), dtype=torch.float32)
+        return flat.view(self.n_obs, -1).t()
+
+    def _obs_tensor(self, obs):
+        rows = self._node_rows(obs)
         x = torch.zeros(1, self.n_pad, self.n_obs, dtype=torch.float32)
-        x[0, :obs.num_nodes] = obs.x
+        x[0, :rows.shape[0]] = rows
         return x.to(self.device)
 
     @torch.no_grad()
@@ -135,7 +144,7 @@ class SimpleDDPG(RLSPAgent):
 
         ``obs``: a :class:`GraphObs` (one env; ``topo`` = index into :attr:`network_files`,
         default: the inference network) or a padded ``[E, n_pad, F]`` tensor with ``topo [E]``."""
-        if isinstance(obs, GraphObs):
+        if isinstance(obs, GraphObs) or (isinstance(obs, np.ndarray) and obs.ndim == 1):
             t = self.topo_index[self.agent_helper.schedule["inference_network"]] if topo is None else int(topo)
             out = self.learner.act(self._obs_tensor(obs), torch.tensor([t], device=self.device))
             return out[0].cpu().numpy()
@@ -203,7 +212,8 @@ class SimpleDDPG(RLSPAgent):
             succ += stats["run_successful_flows"]
             drop += stats["run_dropped_flows"]
             ep_ret += float(reward)
-            self.rb.add(self.obs.x.numpy(), topo, next_obs.x.numpy(), action, reward, float(done))
+            self.rb.add(self._node_rows(self.obs).numpy(), topo, self._node_rows(next_obs).numpy(), action, reward,
+                        float(done))
             self.sps.add(1)
             self.obs = next_obs
             if done:

@@ -4,6 +4,13 @@ Actor (graph mode): ``emb = GNN(obs)``; ``MLP([emb | mask]) * mask`` with PyG ``
 (ReLU between layers, plain last layer, no norm) and **no output squashing** (Q6).
 Critic: ``MLP([GNN(obs) | mask | action]) -> Q``.
 
+Flat mode (``graph_mode: False``, reference ``models.py:115-122, 151``): the reference sizes the
+actor's first layer for ``obs + action`` inputs but feeds only the flattened observation (Q13, a
+shape error at the first forward).  Here flat mode is the evident intent: actor
+``MLP(flatten(obs)) -> action``, critic ``MLP([flatten(obs) | action]) -> Q`` (no embedder, no mask
+inputs; the actor output is still multiplied by the topology's action mask so padded nodes
+schedule nothing).
+
 The action mask is a per-topology constant, so its contribution to the first layer,
 ``mask @ W1[:, H:H+A]^T``, is evaluated once per topology and added like a bias instead of
 multiplying a ``[B, A]`` block of known zeros/ones (bit-for-bit the same function and the same
@@ -40,7 +47,7 @@ class MaskedInputMLP(nn.Module):
 
     def __init__(self, dense_dim: int, mask_dim: int, extra_dim: int, hidden: Sequence[int], out_dim: int):
         super().__init__()
-        self.dense_dim, self.mask_dim, self.extra_dim = dense_dim, mask_dim, extra_dim
+        self.dense_dim, self.mask_dim, self.extra_dim = dense_dim, mask_dim, extra_dim  # mask_dim 0: no mask input
         dims = [dense_dim + mask_dim + extra_dim, *hidden, out_dim]
         self.layers = nn.ModuleList([nn.Linear(dims[i], dims[i + 1]) for i in range(len(dims) - 1)])
 
@@ -55,9 +62,10 @@ class MaskedInputMLP(nn.Module):
         D, A = self.dense_dim, self.mask_dim
         w, w16 = sl(0, D)
         h = linear(dense, w, self.first.bias, w16=w16)
-        w, w16 = sl(D, D + A)
-        topo_bias = linear(masks, w, w16=w16)                # [T, h1]
-        h = h + select_rows(topo_bias, topo)
+        if A > 0:
+            w, w16 = sl(D, D + A)
+            topo_bias = linear(masks, w, w16=w16)            # [T, h1]
+            h = h + select_rows(topo_bias, topo)
         if extra is not None:
             w, w16 = sl(D + A, W.shape[1])
             h = h + linear(extra, w, w16=w16)
@@ -100,15 +108,24 @@ def _embedder(cfg: dict, in_dim: int) -> GNNEmbedder:
                        aggr=cfg.get("GNN_aggr", "mean"), num_iter=int(cfg["GNN_num_iter"]))
 
 
+def _flat_dim(cfg: dict, obs_dim: int, action_dim: int) -> int:
+    """Flattened observation size in flat mode: n_pad x obs features (n_pad from the action size)."""
+    P = int(cfg.get("max_nodes", 24))
+    return P * obs_dim
+
+
 class Actor(nn.Module):
     def __init__(self, cfg: dict, obs_dim: int, action_dim: int, low=0.0, high=1.0):
         super().__init__()
-        if not cfg.get("graph_mode", True):
-            raise NotImplementedError("non-graph (flat) mode is dimensionally broken in the reference (Q13)")
-        self.embedder = _embedder(cfg, obs_dim)
-        H = self.embedder.hidden_dim
+        self.graph_mode = bool(cfg.get("graph_mode", True))
         self.action_dim = action_dim
-        self.mlp = MaskedInputMLP(H, action_dim, 0, list(cfg["actor_hidden_layer_nodes"]), action_dim)
+        if self.graph_mode:
+            self.embedder = _embedder(cfg, obs_dim)
+            H, mdim = self.embedder.hidden_dim, action_dim
+        else:
+            self.embedder = None
+            H, mdim = _flat_dim(cfg, obs_dim, action_dim), 0
+        self.mlp = MaskedInputMLP(H, mdim, 0, list(cfg["actor_hidden_layer_nodes"]), action_dim)
         self.low, self.high = float(low), float(high)
         # reference: no output squashing (Q6); new optional key ``actor_output_activation: sigmoid``
         # bounds the policy to the [0, 1] action box (keeps the critic from being queried far outside
@@ -118,8 +135,11 @@ class Actor(nn.Module):
             raise ValueError(f"actor_output_activation must be none|sigmoid, got {act}")
         self.squash = act == "sigmoid"
 
+    def embed(self, x, topo, graphs: GraphSet):
+        return self.embedder(x, topo, graphs) if self.graph_mode else x.reshape(x.shape[0], -1)
+
     def forward(self, x, topo, graphs: GraphSet, masks: torch.Tensor):
-        emb = self.embedder(x, topo, graphs)
+        emb = self.embed(x, topo, graphs)
         if self.squash:
             return torch.sigmoid(self.mlp(emb, topo, masks)) * select_rows(masks, topo)
         if masks.shape[0] == 1:  # one topology: fold the output mask into the last layer
@@ -130,7 +150,7 @@ class Actor(nn.Module):
 
     def hidden(self, x, topo, graphs: GraphSet, masks: torch.Tensor):
         """Last hidden activation ``z`` with ``forward(x) = (z W^T + b) * mask`` (W, b = last layer)."""
-        return self.mlp.hidden(self.embedder(x, topo, graphs), topo, masks)
+        return self.mlp.hidden(self.embed(x, topo, graphs), topo, masks)
 
     def scale_action(self, a):
         return 2.0 * ((a - self.low) / (self.high - self.low)) - 1.0
@@ -142,14 +162,20 @@ class Actor(nn.Module):
 class QNetwork(nn.Module):
     def __init__(self, cfg: dict, obs_dim: int, action_dim: int):
         super().__init__()
-        if not cfg.get("graph_mode", True):
-            raise NotImplementedError("non-graph (flat) mode is dimensionally broken in the reference (Q13)")
-        self.embedder = _embedder(cfg, obs_dim)
-        H = self.embedder.hidden_dim
-        self.mlp = MaskedInputMLP(H, action_dim, action_dim, list(cfg["critic_hidden_layer_nodes"]), 1)
+        self.graph_mode = bool(cfg.get("graph_mode", True))
+        if self.graph_mode:
+            self.embedder = _embedder(cfg, obs_dim)
+            H, mdim = self.embedder.hidden_dim, action_dim
+        else:
+            self.embedder = None
+            H, mdim = _flat_dim(cfg, obs_dim, action_dim), 0
+        self.mlp = MaskedInputMLP(H, mdim, action_dim, list(cfg["critic_hidden_layer_nodes"]), 1)
+
+    def embed(self, x, topo, graphs: GraphSet):
+        return self.embedder(x, topo, graphs) if self.graph_mode else x.reshape(x.shape[0], -1)
 
     def forward(self, x, topo, graphs: GraphSet, masks: torch.Tensor, action: torch.Tensor):
-        emb = self.embedder(x, topo, graphs)
+        emb = self.embed(x, topo, graphs)
         return self.mlp(emb, topo, masks, action)
 
 
@@ -174,7 +200,7 @@ class QNetwork(nn.Module):
         m16 = shadow(masks)
         Mc, cb = composed_projection(Wa, last.weight, last.bias, masks[0],
                                      m16[0] if m16 is not None else None)   # [h1, z], [h1]
-        emb = self.embedder(x, topo, graphs)
+        emb = self.embed(x, topo, graphs)
         h = mlp.first_layer(emb, topo, masks) + linear(z, Mc, cb)
         for layer in mlp.layers[1:]:
             h = linear(F.relu(h), layer.weight, layer.bias)
