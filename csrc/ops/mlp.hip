@@ -65,6 +65,7 @@ struct Epilogue {
   long ld_gate;
   const float* rowscale;  // [M]: multiply row m
   int relu, clamp, accumulate;
+  int single_topo;       // rowtab / colmask have one row (every topo[m] == 0): no per-row gathers
   float lo, hi;
   float* c32;            // fp32 out (or split-K slabs)
   long ldc32;
@@ -252,13 +253,43 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   const bool split = gridDim.z > 1;
   float* c32 = e.c32 ? e.c32 + (split ? (long)blockIdx.z * g.slab : 0) : nullptr;
   const int col_l = lane & 31, hh = lane >> 5;
+  const bool per_row_topo = (e.rowtab || e.colmask) && !e.single_topo;
 #pragma unroll
-  for (int i = 0; i < RM; ++i)
+  for (int i = 0; i < RM; ++i) {
+    // topology of this lane's 16 rows, loaded once per row block (all gathers issued up front)
+    int tp[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long m = m0 + wm * 32 * RM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      tp[r] = (per_row_topo && m < g.M) ? e.topo[m] : 0;
+    }
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
       const long n = n0 + wn * 32 * RN + 32 * j + col_l;
       if (n >= g.N) continue;
       const float bn = (!split && e.bias) ? e.bias[n] : 0.f;
+      // per-topology row tables: one value per column with a single topology, else gathered per row
+      float rt[16], cm[16];
+      if (!split && e.rowtab) {
+        if (e.single_topo) {
+          const float x = e.rowtab[n];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) rt[r] = x;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) rt[r] = e.rowtab[(long)tp[r] * e.ld_rowtab + n];
+        }
+      }
+      if (!split && e.colmask) {
+        if (e.single_topo) {
+          const float x = e.colmask[n];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) cm[r] = x;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) cm[r] = e.colmask[(long)tp[r] * e.ld_colmask + n];
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const long m = m0 + wm * 32 * RM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -269,17 +300,18 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
           continue;
         }
         v = v * e.alpha + bn;
-        if (e.rowtab) v += e.rowtab[(long)e.topo[m] * e.ld_rowtab + n];
+        if (e.rowtab) v += rt[r];
         if (e.accumulate) v += c32[m * e.ldc32 + n];
         if (e.gate && !(__bfloat162float(e.gate[m * e.ld_gate + n]) > 0.f)) v = 0.f;
         if (e.relu) v = v > 0.f ? v : 0.f;
-        if (e.colmask) v *= e.colmask[(long)e.topo[m] * e.ld_colmask + n];
+        if (e.colmask) v *= cm[r];
         if (e.rowscale) v *= e.rowscale[m];
         if (e.clamp) v = fminf(fmaxf(v, e.lo), e.hi);
         if (c32) c32[m * e.ldc32 + n] = v;
         if (e.c16) e.c16[m * e.ldc16 + n] = __float2bfloat16(v);
       }
     }
+  }
 }
 
 // out[m][n] (row stride ldo) = alpha * sum_z slab[z][m][n] (+ out if accumulate).  A block takes 64
@@ -569,6 +601,7 @@ void gemm(int layout, int M, int N, int K, uintptr_t a, long lda, int adt, uintp
     e.hi = c[1].cast<float>();
   }
   e.accumulate = ep.contains("accumulate") ? ep["accumulate"].cast<int>() : 0;
+  e.single_topo = ep.contains("single_topo") ? ep["single_topo"].cast<int>() : 0;
   e.c32 = ptr<float>(gp("c32"));
   e.ldc32 = gl("ldc32", N);
   e.c16 = ptr<__hip_bfloat16>(gp("c16"));

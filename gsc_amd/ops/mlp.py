@@ -84,6 +84,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str = "nt", *, out16: Optiona
         ep["bias"] = bias.data_ptr()
     if rowtab is not None:
         ep.update(rowtab=rowtab.data_ptr(), ld_rowtab=_ld(rowtab))
+    # one-row tables (a single topology): every row uses row 0, read once per column
+    tabs = [t for t in (rowtab, colmask) if t is not None]
+    if tabs and all(t.shape[0] == 1 for t in tabs):
+        ep["single_topo"] = 1
     if topo is not None:
         assert topo.dtype == torch.int32
         ep["topo"] = topo.data_ptr()
