@@ -133,11 +133,11 @@ def main():
     if args.check_replicas and info.enabled:
         import torch.distributed as dist
         L = trainer.learner
-        sig = torch.stack([t.double().sum() for t in (L.actor_flat.flat, L.critic_flat.flat, L.target_actor_flat.flat,
-                                                      L.target_critic_flat.flat)])
-        sigs = [torch.zeros_like(sig) for _ in range(info.world_size)]
-        dist.all_gather(sigs, sig)
-        same = all(torch.equal(sigs[0], x) for x in sigs)
+        same = True
+        for t in (L.actor_flat.flat, L.critic_flat.flat, L.target_actor_flat.flat, L.target_critic_flat.flat):
+            got = [torch.empty_like(t) for _ in range(info.world_size)]
+            dist.all_gather(got, t)
+            same &= all(torch.equal(got[0], x) for x in got[1:])   # bitwise
         if info.is_main:
             print(json.dumps({"replicas_identical": bool(same), "updates": L.updates,
                               "graphed": bool(L._graphs is not None)}), flush=True)

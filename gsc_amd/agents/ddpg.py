@@ -59,9 +59,11 @@ class DDPGLearner:
         for m in (self.target_actor, self.target_critic):
             for p in m.parameters():
                 p.requires_grad_(False)
-        # identical replicas on every rank
-        broadcast_tensors([self.actor_flat.flat, self.critic_flat.flat, self.target_actor_flat.flat,
-                           self.target_critic_flat.flat])
+        # identical replicas on every rank (a learner built with world_size 1 stays process-local even
+        # inside a process group)
+        if self.dist.enabled:
+            broadcast_tensors([self.actor_flat.flat, self.critic_flat.flat, self.target_actor_flat.flat,
+                               self.target_critic_flat.flat])
         lr = float(cfg.get("learning_rate", 1e-3))
         tau = float(cfg.get("target_model_update", 1e-4))
         self.gamma = float(cfg.get("gamma", 0.99))
@@ -116,7 +118,7 @@ class DDPGLearner:
             self._act_native = NativeAct(self, E)
 
     def _allreduce(self, flat: FlatParams):
-        return allreduce_sum_(flat.grad, async_op=True)
+        return allreduce_sum_(flat.grad, async_op=True) if self.dist.enabled else None
 
     # -- update stages of the autograd path (CPU; GPU reference with GSC_NATIVE_LEARNER=0) -------
     def _target(self, b: Batch) -> torch.Tensor:
@@ -523,7 +525,8 @@ class BatchedTrainer:
     def metrics(self, reset: bool = True) -> dict:
         self.flush()
         vals = self.acc.clone()
-        allreduce_sum_(vals)
+        if self.dist.enabled:
+            allreduce_sum_(vals)
         s, d, r, e = [float(v) for v in vals.cpu()]
         if reset:
             self.acc.zero_()

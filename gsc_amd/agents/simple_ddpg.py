@@ -331,7 +331,9 @@ class SimpleDDPG(RLSPAgent):
         # keep replicas identical after a resume
         from gsc_amd.parallel.dist import broadcast_tensors
         L = self.learner
-        broadcast_tensors([L.actor_flat.flat, L.critic_flat.flat, L.target_actor_flat.flat, L.target_critic_flat.flat])
+        if self.dist.enabled:
+            broadcast_tensors([L.actor_flat.flat, L.critic_flat.flat, L.target_actor_flat.flat,
+                               L.target_critic_flat.flat])
         L.refresh_shadows()
 
     def _per_rank(self) -> bool:
