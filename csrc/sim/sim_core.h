@@ -133,10 +133,10 @@ struct Layout {
       sf_present, placement, total;
 };
 
-GSC_HD int align16(int x) { return (x + 15) & ~15; }
+__host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
 
-GSC_HD Layout make_layout(const Dims& d) {
-  Layout L;
+__host__ __device__ constexpr Layout make_layout(const Dims& d) {
+  Layout L{};
   int o = 0;
 #define GSC_TAKE(field, bytes) L.field = o; o += align16((int)(bytes));
   GSC_TAKE(hdr, sizeof(Header));
@@ -165,6 +165,18 @@ GSC_HD Layout make_layout(const Dims& d) {
 #undef GSC_TAKE
   L.total = o;
   return L;
+}
+
+// Compile-time dimension bucket: configurations whose dims fit it use these (padded) dims on the
+// host and the device alike -- same layout, same results (padding rows / SF columns / edges / pool
+// slots stay empty; the reward uses the real SF count K.S) -- and the device kernel specialised on
+// them sees every state-blob offset and stride as a constant (no per-array base registers).
+struct DimsBucketAbilene {  // <= 12 nodes, <= 4 SFs, 1 SFC, <= 16 edges (Abilene + 1 SFC class)
+  static constexpr Dims dims() { return Dims{12, 4, 1, 16, 160, 512, 128}; }
+};
+GSC_HD bool fits_bucket(const Dims& d, const Dims& b) {
+  return d.N <= b.N && d.S <= b.S && d.C == b.C && d.E <= b.E && d.flow_cap <= b.flow_cap &&
+         d.proc_cap <= b.proc_cap && d.event_cap == b.event_cap;
 }
 
 // Typed view of one env's state blob.
@@ -210,13 +222,25 @@ struct Env {
 // ------------------------------------------------------------------------------------------------
 // RNG helpers (per-env Philox stream; deterministic configs draw nothing)
 // ------------------------------------------------------------------------------------------------
+// The key schedule (10 round keys per word) is loop-invariant inside the event loop; an opaque copy
+// of the keys stops LICM from pinning all 20 round keys in SGPRs for the whole window (they are one
+// scalar add each to recompute; pinned, they pushed other values into spills).
+GSC_HD Philox4 env_philox(Env& S) {
+  uint32_t k0 = S.h->key0, k1 = S.h->key1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  k0 = __builtin_amdgcn_readfirstlane(k0);
+  k1 = __builtin_amdgcn_readfirstlane(k1);
+  asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
+  return philox4x32_10(k0, k1, S.h->ctr++);
+}
 GSC_HD double rng_u01(Env& S) {
-  Philox4 r = philox4x32_10(S.h->key0, S.h->key1, S.h->ctr++);
+  Philox4 r = env_philox(S);
   return u01_53(r.v[0], r.v[1]);
 }
 GSC_HD double rng_normal(Env& S, double mean, double std) {
   if (std == 0.0) return mean;
-  Philox4 r = philox4x32_10(S.h->key0, S.h->key1, S.h->ctr++);
+  Philox4 r = env_philox(S);
   const double u1 = 1.0 - u01_53(r.v[0], r.v[1]);  // (0, 1]
   const double u2 = u01_53(r.v[2], r.v[3]);
   return mean + std * (sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
@@ -986,7 +1010,7 @@ GSC_HD_CALL void write_obs(const Env& S, const SimConst& K, const TopoDev& T, fl
 
 GSC_HD_CALL float compute_reward(Env& S, const SimConst& K, const TopoDev& T) {
   Header* h = S.h;
-  const int succ = h->run_processed, drop = h->run_dropped, Sd = S.d.S, n = T.n;
+  const int succ = h->run_processed, drop = h->run_dropped, Sd = K.S, n = T.n;  // real SF count (dims may be padded)
   double succ_ratio = 0.0, fr = 0.0;
   if (succ + drop > 0) {
     succ_ratio = (double)succ / (succ + drop);
@@ -1004,7 +1028,7 @@ GSC_HD_CALL float compute_reward(Env& S, const SimConst& K, const TopoDev& T) {
   double used = 0.0, inst = 0.0;
   for (int v = 0; v < n; ++v) {
     int cnt = 0;
-    for (int s = 0; s < Sd; ++s) cnt += S.placement[v * Sd + s];
+    for (int s = 0; s < Sd; ++s) cnt += S.placement[v * S.d.S + s];
     inst += cnt;
     if (cnt > 0) used += Sd > 1 ? ((double)(cnt - 1) / (Sd - 1)) * 0.5 + 0.5 : 1.0;
   }

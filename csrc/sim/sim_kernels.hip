@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../common.h"
@@ -262,10 +263,22 @@ __device__ __forceinline__ void rq_merge_inbox(RegQueue<QS>& q, Env& S, int lane
 // Every lane runs the handlers on its own (identical) copy of the header and the same LDS state, so
 // loaded values are wave-uniform and control flow stays scalar; loops over nodes / destinations
 // inside a handler spread over the lanes (sim_core.h wave helpers).
-template <int QS>
+// Layout source of a step kernel: DynLayout = the runtime layout in the kernel arguments; a dims
+// bucket (sim_core.h) = compile-time dims, so every state-blob offset / stride folds to a constant.
+struct DynLayout {};
+template <class B>
+struct BucketLayout {
+  static constexpr Dims D = B::dims();
+  static constexpr Layout L = make_layout(B::dims());
+};
+
+template <class B, int QS, bool PROF>
 __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst& K, char* base, char* topo_lds,
                                                 int env, int lane) {
-  Env S(base, a.L, a.D);
+  Env S = [&] {
+    if constexpr (std::is_same<B, DynLayout>::value) return Env(base, a.L, a.D);
+    else return Env(base, BucketLayout<B>::L, BucketLayout<B>::D);
+  }();
   // Keep the env header in registers for the whole window (written back once at the end).
   Header* const h_mem = S.h;
   Header h_reg = *h_mem;
@@ -282,7 +295,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   schedule_stop(S, K);
   __syncthreads();
   rq_merge_inbox<QS>(q, S, lane);
-  const bool prof = a.prof != nullptr;
+  constexpr bool prof = PROF;  // cycle counters compiled in only for the diagnostic variant
   unsigned long long t_sel = 0, t_hdl = 0, t_mrg = 0, n_ev = 0;
   const unsigned long long t_begin = prof ? __builtin_amdgcn_s_memtime() : 0;
   for (long it = 0;; ++it) {
@@ -318,7 +331,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
         const int ptype = prof ? S.procs[p].type * 4 + (S.procs[p].state < 3 ? S.procs[p].state : 3) : 0;
         dispatch(S, K, T, p);
         ++n_disp;
-        if (a.prof_types && lane == 0) {
+        if (prof && lane == 0) {
           a.prof_types[((long)env * 64 + ptype) * 2] += __builtin_amdgcn_s_memtime() - td;
           a.prof_types[((long)env * 64 + ptype) * 2 + 1] += 1;
         }
@@ -403,7 +416,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   __syncthreads();
 }
 
-template <int QSETS, bool LDS_STATE>
+template <int QSETS, bool LDS_STATE, bool PROF = false, class B = DynLayout>
 __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int env = blockIdx.x;
@@ -414,20 +427,24 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
   else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
   else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
-  // [SimConst][topology tables][state blob (LDS mode)]
-  SimConst* Ks = reinterpret_cast<SimConst*>(smem);
+  constexpr bool STATIC = !std::is_same<B, DynLayout>::value;
+  // LDS: [state blob (LDS mode)][SimConst][topology tables] -- the blob at offset 0, so with a
+  // compile-time layout every state address is a constant
+  long sbytes = a.state_bytes;
+  if constexpr (STATIC) sbytes = BucketLayout<B>::L.total;
+  const long sb = LDS_STATE ? align16((int)sbytes) : 0;
+  SimConst* Ks = reinterpret_cast<SimConst*>(smem + sb);
   if (lane == 0) *Ks = a.K;
-  char* topo_lds = smem + const_stage_bytes();
-  char* state_lds = topo_lds + a.topo_stage;
+  char* topo_lds = smem + sb + const_stage_bytes();
   char* g = a.states + (long)env * a.state_bytes;
   if constexpr (LDS_STATE) {
-    copy16(state_lds, g, a.state_bytes, lane);
+    copy16(smem, g, sbytes, lane);
     __syncthreads();
-    device_step_env<QSETS>(a, *Ks, state_lds, topo_lds, env, lane);
-    copy16(g, state_lds, a.state_bytes, lane);
+    device_step_env<B, QSETS, PROF>(a, *Ks, smem, topo_lds, env, lane);
+    copy16(g, smem, sbytes, lane);
   } else {
     __syncthreads();
-    device_step_env<QSETS>(a, *Ks, g, topo_lds, env, lane);
+    device_step_env<B, QSETS, false>(a, *Ks, g, topo_lds, env, lane);
   }
 }
 
@@ -484,6 +501,12 @@ class SimContext {
     D_.event_cap = dims["event_cap"].cast<int>();
     GSC_CHECK(D_.N <= 256, "at most 256 nodes per topology");
     GSC_CHECK(D_.flow_cap < 32768 && D_.proc_cap < 32768, "pool capacities must be < 32768");
+    // dims that fit a compile-time bucket run padded to it (host and device share the layout)
+    static const bool buckets = getenv("GSC_SIM_BUCKET") ? atoi(getenv("GSC_SIM_BUCKET")) != 0 : true;
+    if (buckets && fits_bucket(D_, DimsBucketAbilene::dims())) {
+      D_ = DimsBucketAbilene::dims();
+      bucket_ = 1;
+    }
     L_ = make_layout(D_);
     fill_const(cfg);
     for (auto item : topos) {
@@ -529,7 +552,11 @@ class SimContext {
             (const void*)sim_step_kernel<1, true>, (const void*)sim_step_kernel<2, true>,
             (const void*)sim_step_kernel<4, true>, (const void*)sim_step_kernel<8, true>,
             (const void*)sim_step_kernel<1, false>, (const void*)sim_step_kernel<2, false>,
-            (const void*)sim_step_kernel<4, false>, (const void*)sim_step_kernel<8, false>};
+            (const void*)sim_step_kernel<4, false>, (const void*)sim_step_kernel<8, false>,
+            (const void*)sim_step_kernel<1, true, true>, (const void*)sim_step_kernel<2, true, true>,
+            (const void*)sim_step_kernel<4, true, true>, (const void*)sim_step_kernel<8, true, true>,
+            (const void*)sim_step_kernel<2, true, false, DimsBucketAbilene>,
+            (const void*)sim_step_kernel<2, true, true, DimsBucketAbilene>};
         for (auto f : fns) GSC_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
       }
     }
@@ -539,6 +566,7 @@ class SimContext {
   }
 
   long state_bytes() const { return L_.total; }
+  int bucket() const { return bucket_; }
   bool use_lds() const { return use_lds_; }
   // LDS bytes one env's workgroup needs on the device (SimConst + topology tables + state blob)
   long lds_per_env() const { return const_stage_bytes() + topo_stage_ + (use_lds_ ? L_.total : 0); }
@@ -568,9 +596,16 @@ class SimContext {
     if (device_) {
       const size_t lds = const_stage_bytes() + topo_stage_ + (use_lds_ ? (size_t)L_.total : 0);
       const hipStream_t st = stream_of(stream);
-#define GSC_LAUNCH_SIM(QS)                                                                       \
-  if (use_lds_) hipLaunchKernelGGL((sim_step_kernel<QS, true>), dim3(E), dim3(64), lds, st, a); \
+#define GSC_LAUNCH_SIM(QS)                                                                             \
+  if (use_lds_ && a.prof) hipLaunchKernelGGL((sim_step_kernel<QS, true, true>), dim3(E), dim3(64), lds, st, a); \
+  else if (use_lds_) hipLaunchKernelGGL((sim_step_kernel<QS, true>), dim3(E), dim3(64), lds, st, a);          \
   else hipLaunchKernelGGL((sim_step_kernel<QS, false>), dim3(E), dim3(64), lds, st, a);
+      if (bucket_ == 1 && use_lds_) {
+        if (a.prof)
+          hipLaunchKernelGGL((sim_step_kernel<2, true, true, DimsBucketAbilene>), dim3(E), dim3(64), lds, st, a);
+        else
+          hipLaunchKernelGGL((sim_step_kernel<2, true, false, DimsBucketAbilene>), dim3(E), dim3(64), lds, st, a);
+      } else
       switch (qsets_) {
         case 1: GSC_LAUNCH_SIM(1) break;
         case 2: GSC_LAUNCH_SIM(2) break;
@@ -618,7 +653,7 @@ class SimContext {
     K.S = c["S"].cast<int>();
     K.F = c["F"].cast<int>();
     GSC_CHECK(K.C <= kMaxC && K.S <= kMaxS && K.F <= kMaxF, "too many SFCs / SFs");
-    GSC_CHECK(K.C == D_.C && K.S == D_.S, "config/dims mismatch");
+    GSC_CHECK(K.C == D_.C && K.S <= D_.S, "config/dims mismatch");  // D_.S may be padded (dims bucket)
     auto chain = c["chain"].cast<std::vector<std::vector<int>>>();
     GSC_CHECK((int)chain.size() == K.C, "chain list size");
     for (int i = 0; i < K.C; ++i) {
@@ -677,6 +712,7 @@ class SimContext {
   }
 
   bool device_;
+  int bucket_ = 0;  // 1: DimsBucketAbilene (compile-time layout kernel)
   int host_threads_;
   bool use_lds_ = false;
   long topo_stage_ = 0;
@@ -695,6 +731,7 @@ void register_sim(py::module_& m) {
       .def_property_readonly("state_bytes", &SimContext::state_bytes)
       .def_property_readonly("use_lds", &SimContext::use_lds)
       .def_property_readonly("lds_per_env", &SimContext::lds_per_env)
+      .def_property_readonly("bucket", &SimContext::bucket)
       .def("reset", &SimContext::reset)
       .def("step", &SimContext::step, py::arg("states"), py::arg("topo_next"), py::arg("seeds"), py::arg("actions"),
            py::arg("action_stride"), py::arg("obs"), py::arg("next_obs"), py::arg("reward"), py::arg("done"),

@@ -13,7 +13,7 @@ def test_tiny_flow_pool_raises(monkeypatch):
     sim = load_batched_from_paths([cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml")],
                                   cfg_path("service_functions", "abc.yaml"),
                                   cfg_path("config", "simulator", "sample_config.yaml"), cfg, 2, device="cpu",
-                                  caps=dict(flow_cap=2, proc_cap=64, event_cap=128), host_threads=1)
+                                  caps=dict(flow_cap=2, proc_cap=64, event_cap=256), host_threads=1)
     sim.reset()
     act = torch.full((2, sim.action_dim), 1.0 / 24)
     for _ in range(3):
@@ -31,7 +31,7 @@ def test_trainer_checks_flags_at_episode_end(monkeypatch):
     sim = load_batched_from_paths([cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml")],
                                   cfg_path("service_functions", "abc.yaml"),
                                   cfg_path("config", "simulator", "sample_config.yaml"), cfg, 2, device="cpu",
-                                  caps=dict(flow_cap=2, proc_cap=64, event_cap=128), host_threads=1)
+                                  caps=dict(flow_cap=2, proc_cap=64, event_cap=256), host_threads=1)
     tr = BatchedTrainer(cfg, sim, TrainerConfig(num_envs=2, batch_size=4, learning_starts=1, check_every=0))
     with pytest.raises(RuntimeError, match="overflow"):
         for _ in range(3):
