@@ -167,18 +167,6 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   return L;
 }
 
-// Compile-time dimension bucket: configurations whose dims fit it use these (padded) dims on the
-// host and the device alike -- same layout, same results (padding rows / SF columns / edges / pool
-// slots stay empty; the reward uses the real SF count K.S) -- and the device kernel specialised on
-// them sees every state-blob offset and stride as a constant (no per-array base registers).
-struct DimsBucketAbilene {  // <= 12 nodes, <= 4 SFs, 1 SFC, <= 16 edges (Abilene + 1 SFC class)
-  static constexpr Dims dims() { return Dims{12, 4, 1, 16, 160, 512, 128}; }
-};
-GSC_HD bool fits_bucket(const Dims& d, const Dims& b) {
-  return d.N <= b.N && d.S <= b.S && d.C == b.C && d.E <= b.E && d.flow_cap <= b.flow_cap &&
-         d.proc_cap <= b.proc_cap && d.event_cap == b.event_cap;
-}
-
 // Typed view of one env's state blob.
 struct Env {
   Header* h;

@@ -264,7 +264,9 @@ __device__ __forceinline__ void rq_merge_inbox(RegQueue<QS>& q, Env& S, int lane
 // loaded values are wave-uniform and control flow stays scalar; loops over nodes / destinations
 // inside a handler spread over the lanes (sim_core.h wave helpers).
 // Layout source of a step kernel: DynLayout = the runtime layout in the kernel arguments; a dims
-// bucket (sim_core.h) = compile-time dims, so every state-blob offset / stride folds to a constant.
+// bucket (struct with a constexpr dims()) = compile-time dims, every state offset / stride a constant.
+// (Measured on MI355X for an Abilene-class bucket: no gain over the runtime layout once the event loop
+// stopped spilling, so no bucket is instantiated; kept as the extension point.)
 struct DynLayout {};
 template <class B>
 struct BucketLayout {
@@ -501,12 +503,6 @@ class SimContext {
     D_.event_cap = dims["event_cap"].cast<int>();
     GSC_CHECK(D_.N <= 256, "at most 256 nodes per topology");
     GSC_CHECK(D_.flow_cap < 32768 && D_.proc_cap < 32768, "pool capacities must be < 32768");
-    // dims that fit a compile-time bucket run padded to it (host and device share the layout)
-    static const bool buckets = getenv("GSC_SIM_BUCKET") ? atoi(getenv("GSC_SIM_BUCKET")) != 0 : true;
-    if (buckets && fits_bucket(D_, DimsBucketAbilene::dims())) {
-      D_ = DimsBucketAbilene::dims();
-      bucket_ = 1;
-    }
     L_ = make_layout(D_);
     fill_const(cfg);
     for (auto item : topos) {
@@ -554,9 +550,7 @@ class SimContext {
             (const void*)sim_step_kernel<1, false>, (const void*)sim_step_kernel<2, false>,
             (const void*)sim_step_kernel<4, false>, (const void*)sim_step_kernel<8, false>,
             (const void*)sim_step_kernel<1, true, true>, (const void*)sim_step_kernel<2, true, true>,
-            (const void*)sim_step_kernel<4, true, true>, (const void*)sim_step_kernel<8, true, true>,
-            (const void*)sim_step_kernel<2, true, false, DimsBucketAbilene>,
-            (const void*)sim_step_kernel<2, true, true, DimsBucketAbilene>};
+            (const void*)sim_step_kernel<4, true, true>, (const void*)sim_step_kernel<8, true, true>};
         for (auto f : fns) GSC_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
       }
     }
@@ -566,7 +560,6 @@ class SimContext {
   }
 
   long state_bytes() const { return L_.total; }
-  int bucket() const { return bucket_; }
   bool use_lds() const { return use_lds_; }
   // LDS bytes one env's workgroup needs on the device (SimConst + topology tables + state blob)
   long lds_per_env() const { return const_stage_bytes() + topo_stage_ + (use_lds_ ? L_.total : 0); }
@@ -600,12 +593,6 @@ class SimContext {
   if (use_lds_ && a.prof) hipLaunchKernelGGL((sim_step_kernel<QS, true, true>), dim3(E), dim3(64), lds, st, a); \
   else if (use_lds_) hipLaunchKernelGGL((sim_step_kernel<QS, true>), dim3(E), dim3(64), lds, st, a);          \
   else hipLaunchKernelGGL((sim_step_kernel<QS, false>), dim3(E), dim3(64), lds, st, a);
-      if (bucket_ == 1 && use_lds_) {
-        if (a.prof)
-          hipLaunchKernelGGL((sim_step_kernel<2, true, true, DimsBucketAbilene>), dim3(E), dim3(64), lds, st, a);
-        else
-          hipLaunchKernelGGL((sim_step_kernel<2, true, false, DimsBucketAbilene>), dim3(E), dim3(64), lds, st, a);
-      } else
       switch (qsets_) {
         case 1: GSC_LAUNCH_SIM(1) break;
         case 2: GSC_LAUNCH_SIM(2) break;
@@ -712,7 +699,6 @@ class SimContext {
   }
 
   bool device_;
-  int bucket_ = 0;  // 1: DimsBucketAbilene (compile-time layout kernel)
   int host_threads_;
   bool use_lds_ = false;
   long topo_stage_ = 0;
@@ -731,7 +717,6 @@ void register_sim(py::module_& m) {
       .def_property_readonly("state_bytes", &SimContext::state_bytes)
       .def_property_readonly("use_lds", &SimContext::use_lds)
       .def_property_readonly("lds_per_env", &SimContext::lds_per_env)
-      .def_property_readonly("bucket", &SimContext::bucket)
       .def("reset", &SimContext::reset)
       .def("step", &SimContext::step, py::arg("states"), py::arg("topo_next"), py::arg("seeds"), py::arg("actions"),
            py::arg("action_stride"), py::arg("obs"), py::arg("next_obs"), py::arg("reward"), py::arg("done"),
