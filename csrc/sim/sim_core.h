@@ -44,8 +44,15 @@ struct alignas(16) Event {  // 16 B
   double t;
   uint32_t key;    // (priority << 31) | event id
   int16_t proc;
-  uint16_t pad;
+  int16_t flow;    // flow of the target process (-1: none): the dispatcher loads the process and its
+                   // flow record concurrently instead of one after the other
 };
+// proc | flow << 16 (the register queue's 32-bit target word)
+GSC_HD int32_t pack_target(int proc, int flow) {
+  return (int32_t)((uint32_t)(uint16_t)proc | ((uint32_t)(uint16_t)flow << 16));
+}
+GSC_HD int target_proc(int32_t t) { return (int)(int16_t)(t & 0xffff); }
+GSC_HD int target_flow(int32_t t) { return (int)(int16_t)((uint32_t)t >> 16); }
 
 struct alignas(16) Proc {  // 32 B
   uint8_t type, state;
@@ -280,7 +287,7 @@ __device__ __forceinline__ double wave_max_f64(double v) {
 // ------------------------------------------------------------------------------------------------
 // Event / process primitives (SimPy contract)
 // ------------------------------------------------------------------------------------------------
-GSC_HD void push_event(Env& S, double t, uint32_t prio, int16_t proc) {
+GSC_HD void push_event(Env& S, double t, uint32_t prio, int16_t proc, int16_t flow) {
   Header* h = S.h;
   const uint32_t key = (prio << 31) | (h->eid & 0x7fffffffu);
   h->eid++;
@@ -289,9 +296,13 @@ GSC_HD void push_event(Env& S, double t, uint32_t prio, int16_t proc) {
   e.t = t;
   e.key = key;
   e.proc = proc;
+  e.flow = flow;
   if (h->n_events > h->max_events) h->max_events = h->n_events;
 }
-GSC_HD void timeout(Env& S, int pid, double delay) { push_event(S, S.h->now + delay, 1u, (int16_t)pid); }
+// yield env.timeout(delay) of process pid (whose flow is `flow`)
+GSC_HD void timeout(Env& S, int pid, int flow, double delay) {
+  push_event(S, S.h->now + delay, 1u, (int16_t)pid, (int16_t)flow);
+}
 
 GSC_HD int alloc_proc(Env& S, uint8_t type, uint8_t state, int flow, int parent) {
   Header* h = S.h;
@@ -308,20 +319,21 @@ GSC_HD int alloc_proc(Env& S, uint8_t type, uint8_t state, int flow, int parent)
 GSC_HD int spawn(Env& S, uint8_t type, uint8_t state, int flow, int parent) {
   const int pid = alloc_proc(S, type, state, flow, parent);
   if (pid < 0) { S.h->eid++; return -1; }
-  push_event(S, S.h->now, 0u, (int16_t)pid);
+  push_event(S, S.h->now, 0u, (int16_t)pid, (int16_t)flow);
   return pid;
 }
 // A process yields env.process(itself-again): re-initialise the same slot (recursive reference generators).
-GSC_HD void respawn_self(Env& S, int pid, uint8_t state) {
+GSC_HD void respawn_self(Env& S, int pid, uint8_t state) {  // writer / MMPP / trace processes (no flow)
   S.procs[pid].state = state;
-  push_event(S, S.h->now, 0u, (int16_t)pid);
+  push_event(S, S.h->now, 0u, (int16_t)pid, (int16_t)-1);
 }
 // Generator return: completion event (NORMAL, delay 0); resumes the waiting parent if any.
-GSC_HD void proc_return(Env& S, int pid, int16_t value) {
-  const int parent = GSC_UNI(S.procs[pid].parent);
+// P = the returning process's record (a parent always serves the same flow as its child).
+GSC_HD void proc_return(Env& S, int pid, const Proc& P, int16_t value) {
+  const int parent = GSC_UNI(P.parent);
   if (parent >= 0) {
     S.procs[parent].ret = value;
-    push_event(S, S.h->now, 1u, (int16_t)parent);
+    push_event(S, S.h->now, 1u, (int16_t)parent, P.flow);
   } else {
     S.h->eid++;
   }
@@ -370,9 +382,8 @@ GSC_HD_CALL void reset_run_metrics(Env& S, const SimConst& K, int n, int l0, int
   (void)K; (void)n;
 }
 
-GSC_HD_CALL void dropped_flow(Env& S, Flow& f, int reason) {
+GSC_HD_CALL void dropped_flow(Env& S, const Flow& f, int reason) {
   Header* h = S.h;
-  f.dropped = 1;
   h->dropped++; h->active--; h->run_dropped++;
   const int sf = f.cur_sf < 0 ? S.d.S : f.cur_sf;
   S.drop_locs[f.node * (S.d.S + 1) + sf]++;
@@ -410,23 +421,23 @@ GSC_HD void add_path_delay(Env& S, double d) {
 // 16-byte LDS loads — and writes back only what it changed before yielding.  A process that
 // returns is freed by proc_return (its record is never written back afterwards).
 // ------------------------------------------------------------------------------------------------
-GSC_HD void end_flow(Env& S, int pid, int fid) {
+GSC_HD void end_flow(Env& S, int pid, const Proc& P, int fid) {
   free_flow(S, fid);
-  proc_return(S, pid, 0);
+  proc_return(S, pid, P, 0);
 }
 
 // FlowSimulator.handle_flow (flowsimulator.py:72-128)
-GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  const Proc P = S.procs[pid];
+// Handlers receive the dispatched process record P and (for flow processes) the flow record f,
+// both loaded by dispatch() concurrently; they write back only what they change.
+GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P, const Flow& f) {
   const int fid = GSC_UNI(P.flow);
-  Flow f = S.flows[fid];
   int state = GSC_UNI(P.state);
   for (;;) {
     switch (state) {
       case H_LOOP:
         if (GSC_UNI(f.departed)) {
           completed_flow(S, f);
-          end_flow(S, pid, fid);
+          end_flow(S, pid, P, fid);
           return;
         }
         S.procs[pid].state = H_AFTER_DECIDE;
@@ -434,14 +445,14 @@ GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid
         return;
       case H_AFTER_DECIDE: {
         const int nxt = GSC_UNI(P.ret);
-        if (nxt < 0) { dropped_flow(S, f, R_DECISION); end_flow(S, pid, fid); return; }
+        if (nxt < 0) { dropped_flow(S, f, R_DECISION); end_flow(S, pid, P, fid); return; }
         S.procs[pid].state = H_AFTER_FWD;
         const int c = spawn(S, P_FORWARD, F_INIT, fid, pid);
         if (c >= 0) S.procs[c].b = (int16_t)nxt;
         return;
       }
       case H_AFTER_FWD:
-        if (!GSC_UNI(P.ret)) { dropped_flow(S, f, R_LINK); end_flow(S, pid, fid); return; }
+        if (!GSC_UNI(P.ret)) { dropped_flow(S, f, R_LINK); end_flow(S, pid, P, fid); return; }
         if (!GSC_UNI(f.fwd_eg)) {
           S.procs[pid].state = H_AFTER_PROC;
           spawn(S, P_PROCESS, PR_INIT, fid, pid);
@@ -450,7 +461,7 @@ GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid
         state = H_LOOP;
         break;
       case H_AFTER_PROC:
-        if (!GSC_UNI(P.ret)) { dropped_flow(S, f, R_NODE); end_flow(S, pid, fid); return; }
+        if (!GSC_UNI(P.ret)) { dropped_flow(S, f, R_NODE); end_flow(S, pid, P, fid); return; }
         state = H_LOOP;
         break;
       default:
@@ -462,20 +473,18 @@ GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid
 }
 
 // DefaultDecisionMaker.decide_next_node (default_decision_maker.py:18-81): weighted round robin.
-GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  const Proc P = S.procs[pid];
+GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P, const Flow& f) {
   if (GSC_UNI(P.state) == D_INIT) {
     S.procs[pid].state = D_RUN;
-    timeout(S, pid, 0.0);
+    timeout(S, pid, P.flow, 0.0);
     return;
   }
   const int fid = GSC_UNI(P.flow);
-  Flow f = S.flows[fid];
-  if (GSC_UNI(f.ttl <= 0)) { proc_return(S, pid, -1); return; }
+  if (GSC_UNI(f.ttl <= 0)) { proc_return(S, pid, P, -1); return; }
   if (GSC_UNI(f.fwd_eg)) {
     const int eg = GSC_UNI(f.egress), node = GSC_UNI(f.node);
     if (eg < 0) S.flows[fid].egress = (int16_t)node;
-    proc_return(S, pid, (int16_t)(eg < 0 ? node : eg));
+    proc_return(S, pid, P, (int16_t)(eg < 0 ? node : eg));
     return;
   }
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = GSC_UNI(T.n);
@@ -517,22 +526,22 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
   }
 #endif
   cnt[best]++;
-  proc_return(S, pid, (int16_t)best);
+  proc_return(S, pid, P, (int16_t)best);
 }
 
 // DefaultFlowForwarder.forward_flow (default_forwarder.py:21-90) + return_link_resources.
-GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  Proc P = S.procs[pid];
+GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P0, const Flow& f0) {
+  Proc P = P0;
   const int fid = GSC_UNI(P.flow);
-  Flow f = S.flows[fid];
+  Flow f = f0;
   const int n = GSC_UNI(T.n);
   const int nxt = GSC_UNI(P.b);
   if (GSC_UNI(P.state) == F_INIT) {
     const int cur = GSC_UNI(f.node);
     const double pd = (cur != nxt) ? T.pdelay[cur * n + nxt] : 0.0;
-    if (GSC_UNI(f.ttl - pd <= 0)) { S.flows[fid].ttl = 0; proc_return(S, pid, 0); return; }
+    if (GSC_UNI(f.ttl - pd <= 0)) { S.flows[fid].ttl = 0; proc_return(S, pid, P, 0); return; }
     if (GSC_UNI(cur == f.egress && f.fwd_eg)) { f.departed = 1; S.flows[fid].departed = 1; }
-    if (cur == nxt) { proc_return(S, pid, 1); return; }
+    if (cur == nxt) { proc_return(S, pid, P, 1); return; }
     P.a = (int16_t)cur;
     P.c = 0;
     P.x = pd;
@@ -552,7 +561,7 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
       fm.node = f.node;
       fm.e2e = f.e2e;
       fm.ttl = f.ttl;
-      proc_return(S, pid, 1);
+      proc_return(S, pid, P, 1);
       return;
     }
   }
@@ -566,7 +575,7 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
   if (GSC_UNI(lrem - f.dr >= 0)) {
     S.link_rem[e] = lrem - f.dr;
   } else {
-    proc_return(S, pid, 0);
+    proc_return(S, pid, P, 0);
     return;
   }
   S.link_passed[e] += f.dr;
@@ -574,41 +583,39 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
   if (GSC_UNI(hop == f.egress && f.fwd_eg)) fm.departed = 1;
   P.state = F_AFTER_HOP;
   S.procs[pid] = P;
-  timeout(S, pid, hd);
+  timeout(S, pid, P.flow, hd);
   (void)K;
 }
 
-GSC_HD_CALL void run_retlink(Env& S, int pid) {
-  const Proc P = S.procs[pid];
+GSC_HD_CALL void run_retlink(Env& S, int pid, const Proc& P) {
   if (GSC_UNI(P.state) == RL_INIT) {
     S.procs[pid].state = RL_AFTER;
-    timeout(S, pid, P.y);
+    timeout(S, pid, -1, P.y);
     return;
   }
   S.link_rem[GSC_UNI(P.a)] += P.x;
-  proc_return(S, pid, 0);
+  proc_return(S, pid, P, 0);
 }
 
 // DefaultFlowProcessor.process_flow (default_processor.py:14-50) + get_processing_delay.
-GSC_HD_CALL void run_process(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  Proc P = S.procs[pid];
+GSC_HD_CALL void run_process(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P0, const Flow& f) {
+  Proc P = P0;
   const int fid = GSC_UNI(P.flow);
   const int Sd = S.d.S;
   const int pstate = GSC_UNI(P.state);
   if (pstate == PR_INIT) {
-    Flow f = S.flows[fid];
     const int node = GSC_UNI(f.node);
     const int sf = GSC_UNI(K.chain[GSC_UNI(f.sfc) * kMaxF + GSC_UNI(f.pos)]);
     Flow& fm = S.flows[fid];
     fm.cur_sf = (int16_t)sf;
-    if (!GSC_UNI(S.placement[node * Sd + sf])) { proc_return(S, pid, 0); return; }
+    if (!GSC_UNI(S.placement[node * Sd + sf])) { proc_return(S, pid, P, 0); return; }
     const double pd = fabs(rng_normal(S, K.pd_mean[sf], K.pd_std[sf]));
-    if (GSC_UNI(f.ttl - pd <= 0)) { fm.ttl = 0; proc_return(S, pid, 0); return; }
+    if (GSC_UNI(f.ttl - pd <= 0)) { fm.ttl = 0; proc_return(S, pid, P, 0); return; }
     S.h->num_proc_delays++;
     S.h->total_proc_delay += pd;
     fm.e2e = f.e2e + pd;
     fm.ttl = f.ttl - pd;
-    if (GSC_UNI(pd == 0.0)) { proc_return(S, pid, 0); return; }  // reference: `if not processing_delay`
+    if (GSC_UNI(pd == 0.0)) { proc_return(S, pid, P, 0); return; }  // reference: `if not processing_delay`
     P.x = pd;
     P.a = (int16_t)node;
     P.b = (int16_t)sf;
@@ -619,30 +626,28 @@ GSC_HD_CALL void run_process(Env& S, const SimConst& K, const TopoDev& T, int pi
     return;
   }
   if (pstate == PR_AFTER_REQ) {
-    if (!GSC_UNI(P.ret)) { proc_return(S, pid, 0); return; }
+    if (!GSC_UNI(P.ret)) { proc_return(S, pid, P, 0); return; }
     S.procs[pid].state = PR_AFTER_WAIT;
-    timeout(S, pid, P.x);
+    timeout(S, pid, P.flow, P.x);
     return;
   }
   // PR_AFTER_WAIT: spawn finish_processing, return True
   const int c = spawn(S, P_FINISH, FI_INIT, fid, -1);
   if (c >= 0) { S.procs[c].a = P.a; S.procs[c].b = P.b; }
-  proc_return(S, pid, 1);
+  proc_return(S, pid, P, 1);
   (void)T;
 }
 
 // BaseFlowProcessor.request_resources (base_processor.py:51-101).
-GSC_HD_CALL void run_request(Env& S, const SimConst& K, int pid) {
-  const Proc P = S.procs[pid];
-  if (GSC_UNI(P.state) == RQ_AFTER) { proc_return(S, pid, 1); return; }
+GSC_HD_CALL void run_request(Env& S, const SimConst& K, int pid, const Proc& P, const Flow& f) {
+  if (GSC_UNI(P.state) == RQ_AFTER) { proc_return(S, pid, P, 1); return; }
   const int fid = GSC_UNI(P.flow);
-  Flow f = S.flows[fid];
   const int node = GSC_UNI(P.a), sf = GSC_UNI(P.b), Sd = S.d.S;
   double demanded = 0.0;
   for (int s = 0; s < Sd; ++s)
     if (GSC_UNI(S.sf_present[node * Sd + s])) demanded += S.sf_load[node * Sd + s] + (s == sf ? f.dr : 0.0);
   const double cap = S.node_cap[node];
-  if (GSC_UNI(!(demanded <= cap))) { proc_return(S, pid, 0); return; }
+  if (GSC_UNI(!(demanded <= cap))) { proc_return(S, pid, P, 0); return; }
   Flow& fm = S.flows[fid];
   fm.proc_idx = f.proc_idx + 1;
   S.proc_traffic[node * Sd + sf] += f.dr;
@@ -652,23 +657,21 @@ GSC_HD_CALL void run_request(Env& S, const SimConst& K, int pid) {
   const double ready = S.sf_start[node * Sd + sf] + K.startup[sf];
   if (GSC_UNI(!(ready <= S.h->now))) {
     const double rem = ready - S.h->now;
-    if (GSC_UNI(f.ttl - rem <= 0)) { fm.ttl = 0; proc_return(S, pid, 0); return; }
+    if (GSC_UNI(f.ttl - rem <= 0)) { fm.ttl = 0; proc_return(S, pid, P, 0); return; }
     fm.e2e = f.e2e + rem;
     fm.ttl = f.ttl - rem;
     S.procs[pid].state = RQ_AFTER;
-    timeout(S, pid, rem);
+    timeout(S, pid, P.flow, rem);
     return;
   }
-  proc_return(S, pid, 1);
+  proc_return(S, pid, P, 1);
 }
 
 // BaseFlowProcessor.finish_processing (base_processor.py:103-135).
-GSC_HD_CALL void run_finish(Env& S, const SimConst& K, int pid) {
-  const Proc P = S.procs[pid];
+GSC_HD_CALL void run_finish(Env& S, const SimConst& K, int pid, const Proc& P, const Flow& f) {
   const int Sd = S.d.S;
   if (GSC_UNI(P.state) == FI_INIT) {
     const int fid = GSC_UNI(P.flow);
-    const Flow f = S.flows[fid];
     Flow& fm = S.flows[fid];
     const int pos = GSC_UNI(f.pos) + 1;
     fm.pos = (int16_t)pos;
@@ -676,7 +679,7 @@ GSC_HD_CALL void run_finish(Env& S, const SimConst& K, int pid) {
     Proc& pm = S.procs[pid];
     pm.x = f.dr;
     pm.state = FI_AFTER;
-    timeout(S, pid, f.duration);
+    timeout(S, pid, P.flow, f.duration);
     return;
   }
   const int node = GSC_UNI(P.a), sf = GSC_UNI(P.b);
@@ -687,14 +690,14 @@ GSC_HD_CALL void run_finish(Env& S, const SimConst& K, int pid) {
   for (int s = 0; s < Sd; ++s)
     if (GSC_UNI(S.sf_present[node * Sd + s])) used += S.sf_load[node * Sd + s];
   S.node_rem[node] = S.node_cap[node] - used;
-  proc_return(S, pid, 0);
+  proc_return(S, pid, P, 0);
 }
 
 // FlowSimulator.init_arrival + DefaultFlowGenerator.generate_flow.
-GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  const int node = GSC_UNI(S.procs[pid].a);
+GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P) {
+  const int node = GSC_UNI(P.a);
   const double mean = S.inter_arr[node];
-  if (GSC_UNI(mean != mean)) { proc_return(S, pid, 0); return; }  // None: arrivals at this node stop
+  if (GSC_UNI(mean != mean)) { proc_return(S, pid, P, 0); return; }  // None: arrivals at this node stop
   Header* h = S.h;
   h->total_flow_count++;
   const double inter = K.det_arrival ? mean : -log(1.0 - rng_u01(S)) * mean;
@@ -731,12 +734,12 @@ GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pi
   } else {
     h->eid++;  // keep event ids aligned with the oracle even on overflow
   }
-  timeout(S, pid, inter);
+  timeout(S, pid, -1, inter);
 }
 
 // ResultWriter.begin_writing / write_network_state: the run-window clock.
-GSC_HD_CALL void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  switch (GSC_UNI(S.procs[pid].state)) {
+GSC_HD_CALL void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P) {
+  switch (GSC_UNI(P.state)) {
     case W_BEGIN:
     case W_AFTER:
       respawn_self(S, pid, W_INIT);
@@ -748,7 +751,7 @@ GSC_HD_CALL void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid
       reset_run_metrics(S, K, T.n, 0, 1);
 #endif
       S.procs[pid].state = W_AFTER;
-      timeout(S, pid, K.run_duration);
+      timeout(S, pid, -1, K.run_duration);
       return;
   }
 }
@@ -758,7 +761,7 @@ GSC_HD_CALL void run_mmpp(Env& S, const SimConst& K, const TopoDev& T, int pid) 
   Proc& P = S.procs[pid];
   if (P.state == M_START) {
     P.state = M_AFTER;
-    timeout(S, pid, K.run_duration);
+    timeout(S, pid, -1, K.run_duration);
     return;
   }
   if (P.state == M_AFTER) {
@@ -773,7 +776,7 @@ GSC_HD_CALL void run_mmpp(Env& S, const SimConst& K, const TopoDev& T, int pid) 
   }
   for (int i = 0; i < T.n_ing; ++i) S.inter_arr[T.ingress[i]] = K.mmpp_mean[S.mmpp_state[T.ingress[i]]];
   P.state = M_AFTER;
-  timeout(S, pid, K.run_duration);
+  timeout(S, pid, -1, K.run_duration);
 }
 
 // TraceProcessor.process_trace.
@@ -784,7 +787,7 @@ GSC_HD_CALL void run_trace(Env& S, const SimConst& K, const TopoDev& T, int pid)
     double w = K.trace_time[i] - S.h->now - 1.0;
     if (w < 0) w = 0;
     P.state = TR_AFTER;
-    timeout(S, pid, w);
+    timeout(S, pid, -1, w);
     return;
   }
   const double mean = K.trace_mean[i];
@@ -805,21 +808,27 @@ GSC_HD_CALL void run_trace(Env& S, const SimConst& K, const TopoDev& T, int pid)
     respawn_self(S, pid, TR_INIT);  // env.process(process_trace()) ...
     S.h->eid++;                     // ... then this generator returns (completion, no waiter)
   } else {
-    proc_return(S, pid, 0);
+    proc_return(S, pid, P, 0);
   }
 }
 
-GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid) {
-  switch (GSC_UNI(S.procs[pid].type)) {
-    case P_HANDLE: run_handle(S, K, T, pid); break;
-    case P_DECIDE: run_decide(S, K, T, pid); break;
-    case P_FORWARD: run_forward(S, K, T, pid); break;
-    case P_PROCESS: run_process(S, K, T, pid); break;
-    case P_REQUEST: run_request(S, K, pid); break;
-    case P_FINISH: run_finish(S, K, pid); break;
-    case P_RETLINK: run_retlink(S, pid); break;
-    case P_ARRIVAL: run_arrival(S, K, T, pid); break;
-    case P_WRITER: run_writer(S, K, T, pid); break;
+// Resume process pid; `fid` = its flow as carried by the event (-1: none).  The process record and
+// the flow record are loaded together (one LDS round trip instead of two dependent ones).
+GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid, int fid) {
+  const Proc P = S.procs[pid];
+  Flow f;
+  if (fid >= 0) f = S.flows[fid];
+  if (GSC_UNI(P.flow) != fid) S.h->flags |= FLAG_BAD_STATE;  // event / process flow mismatch
+  switch (GSC_UNI(P.type)) {
+    case P_HANDLE: run_handle(S, K, T, pid, P, f); break;
+    case P_DECIDE: run_decide(S, K, T, pid, P, f); break;
+    case P_FORWARD: run_forward(S, K, T, pid, P, f); break;
+    case P_PROCESS: run_process(S, K, T, pid, P, f); break;
+    case P_REQUEST: run_request(S, K, pid, P, f); break;
+    case P_FINISH: run_finish(S, K, pid, P, f); break;
+    case P_RETLINK: run_retlink(S, pid, P); break;
+    case P_ARRIVAL: run_arrival(S, K, T, pid, P); break;
+    case P_WRITER: run_writer(S, K, T, pid, P); break;
     case P_MMPP: run_mmpp(S, K, T, pid); break;
     case P_TRACE: run_trace(S, K, T, pid); break;
     default: S.h->flags |= FLAG_BAD_STATE; break;
@@ -896,7 +905,7 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
   const Event ev = S.events[idx];
   remove_event(S, idx);
   h->now = ev.t;
-  if (ev.proc >= 0) dispatch(S, K, T, ev.proc);
+  if (ev.proc >= 0) dispatch(S, K, T, ev.proc, ev.flow);
 }
 
 // SimulatorWrapper.apply (placement derivation) + DurationController.get_next_state prologue.
@@ -945,7 +954,7 @@ GSC_HD_CALL void controller_prologue(Env& S, const SimConst& K, const TopoDev& T
 
 GSC_HD void schedule_stop(Env& S, const SimConst& K) {
   const double T_end = K.run_duration * S.h->run_times;
-  push_event(S, S.h->now + (T_end - S.h->now), 0u, kStopProc);
+  push_event(S, S.h->now + (T_end - S.h->now), 0u, kStopProc, (int16_t)-1);
 }
 
 // Host / serial event loop until the stop event.
@@ -957,7 +966,7 @@ GSC_HD void run_until_stop_serial(Env& S, const SimConst& K, const TopoDev& T) {
     remove_event(S, idx);
     S.h->now = ev.t;
     if (ev.proc == kStopProc) return;
-    dispatch(S, K, T, ev.proc);
+    dispatch(S, K, T, ev.proc, ev.flow);
   }
 }
 

@@ -253,7 +253,7 @@ __device__ __forceinline__ void rq_merge_inbox(RegQueue<QS>& q, Env& S, int lane
   const int nin = __builtin_amdgcn_readfirstlane(S.h->n_events);
   for (int i = 0; i < nin; ++i) {
     const Event e = S.events[i];
-    if (!rq_insert(q, e.t, e.key, e.proc, lane)) S.h->flags |= FLAG_EVENT_OVERFLOW;
+    if (!rq_insert(q, e.t, e.key, pack_target(e.proc, e.flow), lane)) S.h->flags |= FLAG_EVENT_OVERFLOW;
   }
   if (q.n > S.h->max_events) S.h->max_events = q.n;
   S.h->n_events = 0;
@@ -310,7 +310,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     int ep;
     rq_pop(q, et, ep);
     const unsigned long long t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
-    if (ep == kStopProc) {
+    if (target_proc(ep) == kStopProc) {
       S.h->now = et;
       break;
     }
@@ -322,7 +322,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     int n_disp = 0;
     {
       double t = et;
-      int p = ep;
+      int p = target_proc(ep), pf = target_flow(ep);
       // queue head = entry 0 of set 0, held by lane 0
       const double head_t = pack_t((uint32_t)__builtin_amdgcn_readfirstlane((int)q.tlo[0]),
                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)q.thi[0]));
@@ -331,7 +331,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
         S.h->now = t;
         const unsigned long long td = prof ? __builtin_amdgcn_s_memtime() : 0;
         const int ptype = prof ? S.procs[p].type * 4 + (S.procs[p].state < 3 ? S.procs[p].state : 3) : 0;
-        dispatch(S, K, T, p);
+        dispatch(S, K, T, p, pf);
         ++n_disp;
         if (prof && lane == 0) {
           a.prof_types[((long)env * 64 + ptype) * 2] += __builtin_amdgcn_s_memtime() - td;
@@ -351,6 +351,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
         remove_event(S, bi);
         t = m.t;
         p = m.proc;
+        pf = m.flow;
       }
     }
     it += __builtin_amdgcn_readfirstlane(n_disp) - 1;
@@ -382,8 +383,8 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
       Event e;
       e.t = pack_t(q.tlo[s], q.thi[s]);
       e.key = q.key[s];
-      e.proc = (int16_t)q.proc[s];
-      e.pad = 0;
+      e.proc = (int16_t)target_proc(q.proc[s]);
+      e.flow = (int16_t)target_flow(q.proc[s]);
       S.events[idx] = e;
     }
   }
