@@ -174,19 +174,6 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   return L;
 }
 
-// Device event loop inbox: the events a handler chain schedules live in VGPR lanes (lane i = entry i)
-// instead of LDS, so scheduling / reading back / merging an event costs lane moves, not LDS round
-// trips.  Only the device kernel's event loop sets Env::rib; everywhere else events go to LDS.
-struct RegInbox {
-  uint32_t tlo, thi, key;
-  int32_t tgt;  // pack_target(proc, flow)
-};
-constexpr int kRegInboxCap = 48;  // < 64 lanes; the loop merges before the inbox can fill
-#if defined(__HIPCC__)
-// write a wave-uniform value into lane i of a VGPR (v_cmp + v_cndmask)
-__device__ __forceinline__ int lane_put(int old, int v, int i) { return (int)__lane_id() == i ? v : old; }
-#endif
-
 // Typed view of one env's state blob.
 struct Env {
   Header* h;
@@ -199,7 +186,6 @@ struct Env {
   int16_t *flow_free, *proc_free;
   uint8_t *sf_present, *placement;
   Dims d;
-  RegInbox* rib = nullptr;  // device event loop only
 
   GSC_HD Env(char* base, const Layout& L, const Dims& dims) : d(dims) {
     h = (Header*)(base + L.hdr);
@@ -305,19 +291,6 @@ GSC_HD void push_event(Env& S, double t, uint32_t prio, int16_t proc, int16_t fl
   Header* h = S.h;
   const uint32_t key = (prio << 31) | (h->eid & 0x7fffffffu);
   h->eid++;
-#if defined(__HIP_DEVICE_COMPILE__)
-  if (S.rib) {
-    const int i = h->n_events;
-    if (i >= kRegInboxCap) { h->flags |= FLAG_EVENT_OVERFLOW; return; }
-    RegInbox& r = *S.rib;
-    r.tlo = (uint32_t)lane_put((int)r.tlo, __double2loint(t), i);
-    r.thi = (uint32_t)lane_put((int)r.thi, __double2hiint(t), i);
-    r.key = (uint32_t)lane_put((int)r.key, (int)key, i);
-    r.tgt = lane_put(r.tgt, pack_target(proc, flow), i);
-    h->n_events = i + 1;
-    return;
-  }
-#endif
   if (h->n_events >= S.d.event_cap) { h->flags |= FLAG_EVENT_OVERFLOW; return; }
   Event& e = S.events[h->n_events++];
   e.t = t;

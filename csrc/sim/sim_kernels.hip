@@ -247,7 +247,7 @@ __device__ __forceinline__ void rq_pop(RegQueue<QS>& q, double& t, int& proc) {
   q.n--;
 }
 
-// Merge the events appended to S.events (LDS: prologue / persistent queue) into the register queue.
+// Merge the events lane 0's handler appended to S.events (the inbox) into the register queue.
 template <int QS>
 __device__ __forceinline__ void rq_merge_inbox(RegQueue<QS>& q, Env& S, int lane) {
   const int nin = __builtin_amdgcn_readfirstlane(S.h->n_events);
@@ -258,27 +258,6 @@ __device__ __forceinline__ void rq_merge_inbox(RegQueue<QS>& q, Env& S, int lane
   if (q.n > S.h->max_events) S.h->max_events = q.n;
   S.h->n_events = 0;
   __builtin_amdgcn_wave_barrier();
-}
-
-// Entry i of the VGPR-lane inbox (wave-uniform values).
-__device__ __forceinline__ void rib_get(const RegInbox& r, int i, double& t, uint32_t& key, int32_t& tgt) {
-  t = __hiloint2double(__builtin_amdgcn_readlane((int)r.thi, i), __builtin_amdgcn_readlane((int)r.tlo, i));
-  key = (uint32_t)__builtin_amdgcn_readlane((int)r.key, i);
-  tgt = __builtin_amdgcn_readlane(r.tgt, i);
-}
-// Merge the VGPR-lane inbox into the register queue.
-template <int QS>
-__device__ __forceinline__ void rq_merge_regs(RegQueue<QS>& q, Env& S, const RegInbox& r, int lane) {
-  const int nin = S.h->n_events;
-  for (int i = 0; i < nin; ++i) {
-    double t;
-    uint32_t key;
-    int32_t tgt;
-    rib_get(r, i, t, key, tgt);
-    if (!rq_insert(q, t, key, tgt, lane)) S.h->flags |= FLAG_EVENT_OVERFLOW;
-  }
-  if (q.n > S.h->max_events) S.h->max_events = q.n;
-  S.h->n_events = 0;
 }
 
 // Every lane runs the handlers on its own (identical) copy of the header and the same LDS state, so
@@ -318,11 +297,6 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   schedule_stop(S, K);
   __syncthreads();
   rq_merge_inbox<QS>(q, S, lane);
-  // from here on handlers schedule into VGPR lanes
-  RegInbox rib;
-  rib.tlo = rib.thi = rib.key = 0u;
-  rib.tgt = 0;
-  S.rib = &rib;
   constexpr bool prof = PROF;  // cycle counters compiled in only for the diagnostic variant
   unsigned long long t_sel = 0, t_hdl = 0, t_mrg = 0, n_ev = 0;
   const unsigned long long t_begin = prof ? __builtin_amdgcn_s_memtime() : 0;
@@ -340,11 +314,11 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
       S.h->now = et;
       break;
     }
-    // Run the handler, then keep going while the smallest event the handler chain just scheduled
-    // precedes the queue head (entry 0 of set 0): those events -- process initialisations,
-    // completions and zero-delay timeouts at `now` -- are dispatched straight from the VGPR-lane
-    // inbox without a round trip through the register queue.  Popping the minimum of
-    // (queue U inbox) is exactly the full queue's order.
+    // Lane 0 runs the handler, then keeps going while the smallest event the handler chain just
+    // scheduled precedes the queue head (lane 0 holds the head: entry 0 of set 0): those events
+    // -- process initialisations, completions and zero-delay timeouts at `now` -- are dispatched
+    // straight from the inbox without a round trip through the register queue.  Popping the
+    // minimum of (queue U inbox) is exactly the full queue's order.
     int n_disp = 0;
     {
       double t = et;
@@ -366,41 +340,26 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
         const int ni = S.h->n_events;
         // pending-event high-water mark of the full queue (= host path's count after its last push)
         if (q.n + ni > S.h->max_events) S.h->max_events = q.n + ni;
-        if (ni == 0 || n_disp >= 4096 || ni >= kRegInboxCap - 8) break;
+        if (ni == 0 || n_disp >= 4096) break;
         int bi = 0;
-        double mt;
-        uint32_t mk;
-        int32_t mg;
-        rib_get(rib, 0, mt, mk, mg);
+        Event m = S.events[0];
         for (int i = 1; i < ni; ++i) {
-          double ct;
-          uint32_t ck;
-          int32_t cg;
-          rib_get(rib, i, ct, ck, cg);
-          if (ct < mt || (ct == mt && ck < mk)) { mt = ct; mk = ck; mg = cg; bi = i; }
+          const Event c = S.events[i];
+          if (ev_less(c, m)) { m = c; bi = i; }
         }
-        if (!(mt < head_t || (mt == head_t && mk < head_k))) break;
-        // remove entry bi: the last entry takes its lane
-        const int last = ni - 1;
-        if (bi != last) {
-          double lt;
-          uint32_t lk;
-          int32_t lg;
-          rib_get(rib, last, lt, lk, lg);
-          rib.tlo = (uint32_t)lane_put((int)rib.tlo, __double2loint(lt), bi);
-          rib.thi = (uint32_t)lane_put((int)rib.thi, __double2hiint(lt), bi);
-          rib.key = (uint32_t)lane_put((int)rib.key, (int)lk, bi);
-          rib.tgt = lane_put(rib.tgt, lg, bi);
-        }
-        S.h->n_events = last;
-        t = mt;
-        p = target_proc(mg);
-        pf = target_flow(mg);
+        if (!(m.t < head_t || (m.t == head_t && m.key < head_k))) break;
+        remove_event(S, bi);
+        t = m.t;
+        p = m.proc;
+        pf = m.flow;
       }
     }
     it += __builtin_amdgcn_readfirstlane(n_disp) - 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const unsigned long long t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
-    rq_merge_regs<QS>(q, S, rib, lane);
+    rq_merge_inbox<QS>(q, S, lane);
     if (prof) {
       const unsigned long long t3 = __builtin_amdgcn_s_memtime();
       t_sel += t1 - t0;
@@ -416,7 +375,6 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     pr[2] += t_mrg;
     pr[3] += n_ev;
   }
-  S.rib = nullptr;  // epilogue (env_init) schedules into LDS again
   __syncthreads();
   // write the queue back (sorted) as the persistent pending-event array
   for (int s = 0; s < QS; ++s) {
@@ -430,7 +388,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
       S.events[idx] = e;
     }
   }
-  S.h->n_events = q.n;
+  if (lane == 0) S.h->n_events = q.n;
   __syncthreads();
   // epilogue: reward/stats in lane 0, observations lane-parallel (they read only LDS state)
   const long ostride = (long)K.n_pad * K.n_obs;
