@@ -283,6 +283,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   }();
   // Keep the env header in registers for the whole window (written back once at the end).
   Header* const h_mem = S.h;
+  // (measured: header in LDS instead = 2.83 vs 2.30 ms/step for 256 Abilene envs)
   Header h_reg = *h_mem;
   S.h = &h_reg;
   const TopoDev T = a.topo_stage ? stage_topo(a.topos[S.h->topo], topo_lds, lane) : a.topos[S.h->topo];
