@@ -30,6 +30,8 @@
 // as gatv2_dense_reference in gsc_amd/models/gnn.py.  Tests: tests/test_gpu_ops.py (bf16 tolerance).
 #include <pybind11/pybind11.h>
 
+#include <cstdlib>
+
 #include "gnn_cl.h"
 
 namespace gsc {
@@ -558,8 +560,10 @@ __device__ __forceinline__ void mf_layer_bwd(const ClArgs& a, const MfW* wT, con
   }
 }
 
-template <int HPF, bool K2, bool LOADED>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void gnn_mf_bwd_kernel(ClArgs a, MfLayout m) {
+// WPE: waves per SIMD the register budget is sized for (2: 256 registers -- spills to scratch at
+// H = 22; 1: 512 registers, no spills, one wave per SIMD)
+template <int HPF, bool K2, bool LOADED, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void gnn_mf_bwd_kernel(ClArgs a, MfLayout m) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int CG = HPF / 4;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -881,6 +885,7 @@ static void mf_launch_fwd(ClArgs a, hipStream_t st, int cus) {
 
 template <int HPF, bool K2>
 static int mf_launch_bwd(ClArgs a, hipStream_t st, int cus, int max_rows) {
+  static const int wpe = getenv("GSC_GNN_BWD_WPE") ? atoi(getenv("GSC_GNN_BWD_WPE")) : 1;
   GSC_CHECK(a.s_dst != nullptr && a.s_src != nullptr && a.MP >= a.M && a.MP % 16 == 0,
             "MFMA GNN backward needs the one-hot message matrices (GraphSet.s_dst / s_src)");
   const MfLayout m = mf_layout(a, true, HPF);
@@ -893,19 +898,25 @@ static int mf_launch_bwd(ClArgs a, hipStream_t st, int cus, int max_rows) {
   }
   GSC_CHECK(lds <= 160 * 1024, "GNN (MFMA) backward working set exceeds LDS");
   const bool loaded = a.blob != nullptr;
-  const void* fn = loaded ? (const void*)gnn_mf_bwd_kernel<HPF, K2, true> : (const void*)gnn_mf_bwd_kernel<HPF, K2, false>;
+  const void* fns[4] = {(const void*)gnn_mf_bwd_kernel<HPF, K2, true, 1>, (const void*)gnn_mf_bwd_kernel<HPF, K2, false, 1>,
+                        (const void*)gnn_mf_bwd_kernel<HPF, K2, true, 2>, (const void*)gnn_mf_bwd_kernel<HPF, K2, false, 2>};
+  const void* fn = fns[(wpe == 2 ? 2 : 0) + (loaded ? 0 : 1)];
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = (int)((160 * 1024) / lds);
-  if (per_cu * a.waves > 8) per_cu = 8 / a.waves;  // 2 waves/SIMD (VGPR budget)
+  if (per_cu * a.waves > 4 * wpe) per_cu = 4 * wpe / a.waves;  // WPE waves/SIMD (register budget)
+  if (per_cu < 1) per_cu = 1;
   const int need = (a.B + a.waves - 1) / a.waves;
   const int cap = cus * (per_cu > 0 ? per_cu : 1);
   int grid = need < cap ? need : cap;
   if (grid > max_rows) grid = max_rows;
   if (grid < 1) grid = 1;
-  if (loaded)
-    hipLaunchKernelGGL((gnn_mf_bwd_kernel<HPF, K2, true>), dim3(grid), dim3(64 * a.waves), lds, st, a, m);
-  else
-    hipLaunchKernelGGL((gnn_mf_bwd_kernel<HPF, K2, false>), dim3(grid), dim3(64 * a.waves), lds, st, a, m);
+  if (wpe == 2) {
+    if (loaded) hipLaunchKernelGGL((gnn_mf_bwd_kernel<HPF, K2, true, 2>), dim3(grid), dim3(64 * a.waves), lds, st, a, m);
+    else hipLaunchKernelGGL((gnn_mf_bwd_kernel<HPF, K2, false, 2>), dim3(grid), dim3(64 * a.waves), lds, st, a, m);
+  } else {
+    if (loaded) hipLaunchKernelGGL((gnn_mf_bwd_kernel<HPF, K2, true, 1>), dim3(grid), dim3(64 * a.waves), lds, st, a, m);
+    else hipLaunchKernelGGL((gnn_mf_bwd_kernel<HPF, K2, false, 1>), dim3(grid), dim3(64 * a.waves), lds, st, a, m);
+  }
   check_launch();
   return grid;
 }
