@@ -1,0 +1,313 @@
+// Layer-wise GATv2 for graphs too large for the fused per-graph kernels (e.g. the 200-node
+// synthetic topologies of BASELINE config 5: a graph's working set exceeds one CU's LDS).
+//
+// One conv = three stages over the whole batch (rows = B graphs x P node slots):
+//   node linears   [x_l | x_r] = h W^T + b          MFMA GEMM engine (csrc/ops/mlp.hip), K = Fi
+//   attention      per target node: scores att . LeakyReLU(x_l[j] + x_r[i]) over its in-messages
+//                  (CSR), PyG segment softmax, mean aggregation, bias, ReLU        (this file)
+//   mean pool      per graph, fixed order                                        (this file)
+// and the backward mirrors it: attention backward per target node (softmax / score / scatter
+// terms; d x_r gathered per target, d x_l gathered per source through the source-sorted CSR -- no
+// atomics), weight gradients dW = dX^T h and input gradients dX W on the GEMM engine, vector
+// gradients by deterministic two-phase column sums.
+//
+// Lanes: a 32-lane half-wave owns one (graph, node) with lane c = channel (H <= 32); message scores
+// reduce over the half-wave with xor shuffles.  Reference: PyG GATv2Conv as gatv2_dense_reference
+// (gsc_amd/models/gnn.py) -- reference repo src/rlsp/agents/models.py:10-53.
+#include <pybind11/pybind11.h>
+
+#include "../common.h"
+
+namespace py = pybind11;
+
+namespace gsc {
+
+constexpr float kLwSlope = 0.2f;
+
+struct LwGraph {
+  const int32_t* topo;     // [B]
+  const int32_t* nnodes;   // [T]
+  const int32_t* in_ptr;   // [T, P+1]  messages into each node (target-sorted order)
+  const int32_t* in_src;   // [T, M]    source of the q-th target-sorted message
+  const int32_t* out_ptr;  // [T, P+1]  messages out of each node
+  const int32_t* out_q;    // [T, M]    target-sorted position of the source-sorted messages
+  const float* deg;        // [T, P]
+  int B, P, M, H;
+};
+
+__device__ __forceinline__ float lw_sum32(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+  return v;
+}
+
+__device__ __forceinline__ float leaky(float z) { return z > 0.f ? z : kLwSlope * z; }
+
+// ---- forward attention + aggregation ---------------------------------------------------------------
+// h_out[b,i,:] = act( sum_q alpha_q x_l[b,j_q,:] / deg_i + bias ),  alpha_q saved as [B, M]
+__global__ __launch_bounds__(256) void lw_attn_fwd_kernel(LwGraph g, const float* __restrict__ xl,
+                                                          const float* __restrict__ xr, const float* __restrict__ att,
+                                                          const float* __restrict__ bias, int relu,
+                                                          float* __restrict__ h_out, float* __restrict__ alpha) {
+  const long node = (long)blockIdx.x * 8 + (threadIdx.x >> 5);  // 8 nodes per block
+  const int c = threadIdx.x & 31;
+  if (node >= (long)g.B * g.P) return;
+  const int b = (int)(node / g.P), i = (int)(node - (long)b * g.P);
+  const int t = g.topo[b];
+  const int H = g.H;
+  float* out = h_out + node * H;
+  if (i >= g.nnodes[t]) {
+    if (c < H) out[c] = 0.f;
+    return;
+  }
+  const int q0 = g.in_ptr[(long)t * (g.P + 1) + i], q1 = g.in_ptr[(long)t * (g.P + 1) + i + 1];
+  const int32_t* src = g.in_src + (long)t * g.M;
+  const float* xlb = xl + (long)b * g.P * H;
+  const float xri = c < H ? xr[node * H + c] : 0.f;
+  const float ac = c < H ? att[c] : 0.f;
+  float* al = alpha + (long)b * g.M;
+  // three passes over the in-messages (scores recomputed: no cross-lane traffic through memory):
+  // max, softmax denominator, then alpha (saved) and the aggregation
+  auto score = [&](int q, float& xlj) {
+    xlj = c < H ? xlb[(long)src[q] * H + c] : 0.f;
+    return lw_sum32(ac * leaky(xlj + xri));
+  };
+  float mx = -__builtin_inff(), xlj;
+  for (int q = q0; q < q1; ++q) {
+    const float s = score(q, xlj);
+    mx = s > mx ? s : mx;
+  }
+  float den = 0.f;
+  for (int q = q0; q < q1; ++q) den += __expf(score(q, xlj) - mx);
+  float acc = 0.f;
+  for (int q = q0; q < q1; ++q) {
+    const float a = __expf(score(q, xlj) - mx) / (den + 1e-16f);
+    acc += a * xlj;
+    if (c == 0) al[q] = a;
+  }
+  if (c < H) {
+    float y = acc / g.deg[(long)t * g.P + i] + bias[c];
+    if (relu) y = y > 0.f ? y : 0.f;
+    out[c] = y;
+  }
+}
+
+// emb[b,:] = mean over the graph's real nodes of h[b,:,:]
+__global__ __launch_bounds__(256) void lw_pool_kernel(LwGraph g, const float* __restrict__ h, float* __restrict__ emb) {
+  const long b = (long)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int c = threadIdx.x & 31;
+  if (b >= g.B || c >= g.H) return;
+  const int n = g.nnodes[g.topo[b]];
+  const float* hb = h + b * g.P * g.H;
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) s += hb[(long)i * g.H + c];
+  emb[b * g.H + c] = s / (float)n;
+}
+
+// d h_last[b,i,:] = demb[b,:] / n for real nodes, 0 for padding
+__global__ __launch_bounds__(256) void lw_pool_bwd_kernel(LwGraph g, const float* __restrict__ demb, float* __restrict__ dh) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)g.B * g.P * g.H;
+  if (idx >= total) return;
+  const long node = idx / g.H;
+  const int c = (int)(idx - node * g.H);
+  const int b = (int)(node / g.P), i = (int)(node - (long)b * g.P);
+  const int n = g.nnodes[g.topo[b]];
+  dh[idx] = i < n ? demb[(long)b * g.H + c] / (float)n : 0.f;
+}
+
+// ---- backward, per target node ---------------------------------------------------------------------
+// In:  dh (gradient at this conv's output; overwritten by dY = dh * relu'(h_out)), h_out (null: no
+//      ReLU), x_l, x_r, alpha.  Out: dxr[b,i,:] (gathered), per-message x_l gradients msg[b,q,:]
+//      = alpha_q dY_i / deg_i + dz_q, per-node d att partials datt[b,i,:].
+__global__ __launch_bounds__(256) void lw_attn_bwd_kernel(LwGraph g, float* __restrict__ dh,
+                                                          const float* __restrict__ h_out, const float* __restrict__ xl,
+                                                          const float* __restrict__ xr,
+                                                          const float* __restrict__ alpha, const float* __restrict__ att,
+                                                          float* __restrict__ dxr, float* __restrict__ msg,
+                                                          float* __restrict__ datt) {
+  const long node = (long)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int c = threadIdx.x & 31;
+  if (node >= (long)g.B * g.P) return;
+  const int b = (int)(node / g.P), i = (int)(node - (long)b * g.P);
+  const int t = g.topo[b];
+  const int H = g.H;
+  const bool ch = c < H;
+  if (i >= g.nnodes[t]) {
+    if (ch) {
+      dh[node * H + c] = 0.f;
+      dxr[node * H + c] = 0.f;
+      datt[node * H + c] = 0.f;
+    }
+    return;
+  }
+  float dy = ch ? dh[node * H + c] : 0.f;
+  if (h_out && ch && !(h_out[node * H + c] > 0.f)) dy = 0.f;
+  if (ch) dh[node * H + c] = dy;
+  const float gc = dy / g.deg[(long)t * g.P + i];
+  const int q0 = g.in_ptr[(long)t * (g.P + 1) + i], q1 = g.in_ptr[(long)t * (g.P + 1) + i + 1];
+  const int32_t* src = g.in_src + (long)t * g.M;
+  const float* xlb = xl + (long)b * g.P * H;
+  const float* al = alpha + (long)b * g.M;
+  float* mb = msg + (long)b * g.M * H;
+  const float xri = ch ? xr[node * H + c] : 0.f;
+  const float ac = ch ? att[c] : 0.f;
+  // sum_q' alpha_q' dalpha_q'
+  float sad = 0.f;
+  for (int q = q0; q < q1; ++q) {
+    const int j = src[q];
+    const float da = lw_sum32(ch ? gc * xlb[(long)j * H + c] : 0.f);
+    sad += al[q] * da;
+  }
+  float dxr_acc = 0.f, datt_acc = 0.f;
+  for (int q = q0; q < q1; ++q) {
+    const int j = src[q];
+    const float xlj = ch ? xlb[(long)j * H + c] : 0.f;
+    const float da = lw_sum32(gc * xlj);
+    const float de = al[q] * (da - sad);
+    const float z = xlj + xri;
+    datt_acc += de * leaky(z);
+    const float dz = de * ac * (z > 0.f ? 1.f : kLwSlope);
+    dxr_acc += dz;
+    if (ch) mb[(long)q * H + c] = al[q] * gc + dz;
+  }
+  if (ch) {
+    dxr[node * H + c] = dxr_acc;
+    datt[node * H + c] = datt_acc;
+  }
+}
+
+// dxl[b,j,:] = sum over messages out of j of msg[b,q,:]   (source-sorted CSR; no atomics)
+__global__ __launch_bounds__(256) void lw_src_gather_kernel(LwGraph g, const float* __restrict__ msg, float* __restrict__ dxl) {
+  const long node = (long)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int c = threadIdx.x & 31;
+  if (node >= (long)g.B * g.P || c >= g.H) return;
+  const int b = (int)(node / g.P), j = (int)(node - (long)b * g.P);
+  const int t = g.topo[b];
+  float s = 0.f;
+  if (j < g.nnodes[t]) {
+    const int p0 = g.out_ptr[(long)t * (g.P + 1) + j], p1 = g.out_ptr[(long)t * (g.P + 1) + j + 1];
+    const int32_t* oq = g.out_q + (long)t * g.M;
+    const float* mb = msg + (long)b * g.M * g.H;
+    for (int p = p0; p < p1; ++p) s += mb[(long)oq[p] * g.H + c];
+  }
+  dxl[node * g.H + c] = s;
+}
+
+// dh[r, :] *= (h[r, :] > 0)  (ReLU of the layer below; h = that layer's output)
+__global__ __launch_bounds__(256) void lw_relu_mask_kernel(float* dh, const float* h, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !(h[i] > 0.f)) dh[i] = 0.f;
+}
+
+// Deterministic column sums of x [R, C] (row stride ldx): phase 1 -- block k sums rows
+// [k*chunk, (k+1)*chunk) in order into part[k][C]; phase 2 -- part rows summed in order into out[C]
+// (+= when accumulate).
+__global__ __launch_bounds__(256) void lw_colsum_p1_kernel(const float* __restrict__ x, long R, int C, long ldx, long chunk,
+                                                           float* __restrict__ part) {
+  const long r0 = (long)blockIdx.x * chunk;
+  const long r1 = r0 + chunk < R ? r0 + chunk : R;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (long r = r0; r < r1; ++r) s += x[r * ldx + c];
+    part[(long)blockIdx.x * C + c] = s;
+  }
+}
+__global__ __launch_bounds__(64) void lw_colsum_p2_kernel(const float* __restrict__ part, int K, int C, float* out,
+                                                          int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += part[(long)k * C + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ---------------------------------------------------------------------------------------------------
+static LwGraph lw_graph(py::dict t, uintptr_t topo, int B, int P, int H) {
+  LwGraph g{};
+  g.topo = ptr<const int32_t>(topo);
+  g.nnodes = ptr<const int32_t>(t["nnodes"].cast<uintptr_t>());
+  g.in_ptr = ptr<const int32_t>(t["in_ptr"].cast<uintptr_t>());
+  g.in_src = ptr<const int32_t>(t["in_src"].cast<uintptr_t>());
+  g.out_ptr = ptr<const int32_t>(t["out_ptr"].cast<uintptr_t>());
+  g.out_q = ptr<const int32_t>(t["out_q"].cast<uintptr_t>());
+  g.deg = ptr<const float>(t["deg"].cast<uintptr_t>());
+  g.M = t["M"].cast<int>();
+  g.B = B;
+  g.P = P;
+  g.H = H;
+  GSC_CHECK(H <= 32, "layer-wise GATv2: at most 32 channels");
+  return g;
+}
+
+static dim3 node_grid(const LwGraph& g) { return dim3((unsigned)(((long)g.B * g.P + 7) / 8)); }
+
+void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t xl, uintptr_t xr, uintptr_t att,
+                 uintptr_t bias, int relu, uintptr_t h_out, uintptr_t alpha, uintptr_t stream) {
+  const LwGraph g = lw_graph(tables, topo, B, P, H);
+  hipLaunchKernelGGL(lw_attn_fwd_kernel, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<const float>(xl),
+                     ptr<const float>(xr), ptr<const float>(att), ptr<const float>(bias), relu, ptr<float>(h_out),
+                     ptr<float>(alpha));
+  check_launch();
+}
+
+void lw_pool(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t h, uintptr_t emb, uintptr_t stream) {
+  const LwGraph g = lw_graph(tables, topo, B, P, H);
+  hipLaunchKernelGGL(lw_pool_kernel, dim3((B + 7) / 8), dim3(256), 0, stream_of(stream), g, ptr<const float>(h),
+                     ptr<float>(emb));
+  check_launch();
+}
+
+void lw_pool_bwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t demb, uintptr_t dh, uintptr_t stream) {
+  const LwGraph g = lw_graph(tables, topo, B, P, H);
+  const long total = (long)B * P * H;
+  hipLaunchKernelGGL(lw_pool_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream_of(stream), g,
+                     ptr<const float>(demb), ptr<float>(dh));
+  check_launch();
+}
+
+void lw_attn_bwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t dh, uintptr_t h_out, uintptr_t xl,
+                 uintptr_t xr, uintptr_t alpha, uintptr_t att, uintptr_t dxr, uintptr_t msg, uintptr_t datt,
+                 uintptr_t stream) {
+  const LwGraph g = lw_graph(tables, topo, B, P, H);
+  hipLaunchKernelGGL(lw_attn_bwd_kernel, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<float>(dh),
+                     ptr<const float>(h_out), ptr<const float>(xl), ptr<const float>(xr), ptr<const float>(alpha),
+                     ptr<const float>(att), ptr<float>(dxr), ptr<float>(msg), ptr<float>(datt));
+  check_launch();
+}
+
+void lw_src_gather(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t msg, uintptr_t dxl, uintptr_t stream) {
+  const LwGraph g = lw_graph(tables, topo, B, P, H);
+  hipLaunchKernelGGL(lw_src_gather_kernel, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<const float>(msg),
+                     ptr<float>(dxl));
+  check_launch();
+}
+
+void lw_relu_mask(uintptr_t dh, uintptr_t h, long n, uintptr_t stream) {
+  hipLaunchKernelGGL(lw_relu_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream_of(stream),
+                     ptr<float>(dh), ptr<const float>(h), n);
+  check_launch();
+}
+
+// part must hold >= min(R, 1024) x C floats
+void lw_colsum(uintptr_t x, long R, int C, long ldx, uintptr_t part, uintptr_t out, int accumulate, uintptr_t stream) {
+  const long chunk = R <= 1024 ? 1 : (R + 1023) / 1024;
+  const int K = (int)((R + chunk - 1) / chunk);
+  hipLaunchKernelGGL(lw_colsum_p1_kernel, dim3(K), dim3(64), 0, stream_of(stream), ptr<const float>(x), R, C, ldx, chunk,
+                     ptr<float>(part));
+  hipLaunchKernelGGL(lw_colsum_p2_kernel, dim3((C + 63) / 64), dim3(64), 0, stream_of(stream), ptr<const float>(part), K,
+                     C, ptr<float>(out), accumulate);
+  check_launch();
+}
+
+void register_gnn_lw(py::module_& m) {
+  m.def("lw_attn_fwd", &lw_attn_fwd, "layer-wise GATv2: attention + aggregation (+ReLU), alpha saved");
+  m.def("lw_pool", &lw_pool, "layer-wise GATv2: mean pool over real nodes");
+  m.def("lw_pool_bwd", &lw_pool_bwd, "layer-wise GATv2: mean-pool backward");
+  m.def("lw_attn_bwd", &lw_attn_bwd, "layer-wise GATv2: attention backward per target node");
+  m.def("lw_src_gather", &lw_src_gather, "layer-wise GATv2: d x_l gathered per source node");
+  m.def("lw_relu_mask", &lw_relu_mask, "dh *= (h > 0)");
+  m.def("lw_colsum", &lw_colsum, "deterministic column sums (two phases)");
+}
+
+}  // namespace gsc

@@ -8,6 +8,7 @@ void register_optim(py::module_& m);
 void register_mlp(py::module_& m);
 void register_streams(py::module_& m);
 void register_replay(py::module_& m);
+void register_gnn_lw(py::module_& m);
 void register_ops(py::module_& m) {
   register_explore(m);
   register_gnn(m);
@@ -15,5 +16,6 @@ void register_ops(py::module_& m) {
   register_mlp(m);
   register_streams(m);
   register_replay(m);
+  register_gnn_lw(m);
 }
 }  // namespace gsc

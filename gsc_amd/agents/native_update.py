@@ -32,7 +32,7 @@ from typing import List, Optional
 import torch
 
 from gsc_amd.native import load as load_native
-from gsc_amd.ops.gnn import _layer_of, _tables
+from gsc_amd.ops.gnn import _layer_of, _tables, gnn_fits
 from gsc_amd.ops.mlp import gemm
 
 BF16 = torch.bfloat16
@@ -137,10 +137,19 @@ class NativeDDPGUpdate:
         nat = self.nat
         Fin = L.actor.embedder.input_dim
         self.Fin = Fin
-        sb = nat.gnn_saved_bytes(self.tables, self.P, Fin, H, self.layer_of)
-        self.blob = {k: torch.empty(B * sb, device=dev, dtype=torch.uint8) for k in ("a", "c")}
-        self.gnn_rows = 1024
         ne = sum(p.numel() for p in L.actor.embedder.flat_parameters())
+        self.ne = ne
+        # graphs whose per-graph working set exceeds LDS (e.g. 200 nodes): layer-wise GNN kernels, one
+        # workspace per saved forward ("a", "c") plus one for forwards without a backward
+        self.layerwise = not gnn_fits(L.actor.embedder, L.graphs, self.P, Fin)
+        if self.layerwise:
+            from gsc_amd.ops.gnn_lw import LayerwiseGAT
+            self.lwo = {k: LayerwiseGAT(self.tables, B, self.P, Fin, H, self.layer_of, dev) for k in ("a", "c", "-")}
+            self.blob = {"a": None, "c": None}
+        else:
+            sb = nat.gnn_saved_bytes(self.tables, self.P, Fin, H, self.layer_of)
+            self.blob = {k: torch.empty(B * sb, device=dev, dtype=torch.uint8) for k in ("a", "c")}
+        self.gnn_rows = 1024
         self.gnn_partials = torch.empty(self.gnn_rows, ne, device=dev, dtype=F32)
         self.gnn_grad = mk(ne)
         self.topo32 = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -149,13 +158,20 @@ class NativeDDPGUpdate:
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.dev).cuda_stream
 
-    def _gnn_fwd(self, net: _Net, x: torch.Tensor, out: torch.Tensor, save: Optional[torch.Tensor]) -> None:
+    def _gnn_fwd(self, net: _Net, x: torch.Tensor, out: torch.Tensor, save: Optional[torch.Tensor],
+                 key: str = "-") -> None:
+        if self.layerwise:
+            self.lwo[key].forward(net.fp.flat[:self.ne], x, self.topo32, out)
+            return
         self.nat.gnn_forward(self.tables, net.emb_ptr(), x.data_ptr(), self.topo32.data_ptr(), out.data_ptr(), self.B,
                              self.P, self.Fin, self.H, self.layer_of, self._stream(),
                              save.data_ptr() if save is not None else 0)
 
-    def _gnn_bwd(self, net: _Net, x: torch.Tensor, demb: torch.Tensor, blob: torch.Tensor) -> None:
+    def _gnn_bwd(self, net: _Net, x: torch.Tensor, demb: torch.Tensor, blob: torch.Tensor, key: str = "-") -> None:
         # the embedder gradient is the first run of the network's flat gradient buffer
+        if self.layerwise:
+            self.lwo[key].backward(net.fp.flat[:self.ne], demb, net.fp.grad[:self.ne])
+            return
         self.nat.gnn_backward(self.tables, net.emb_ptr(), x.data_ptr(), self.topo32.data_ptr(), demb.data_ptr(),
                               self.gnn_partials.data_ptr(), self.gnn_rows, net.fp.grad.data_ptr(), self.B, self.P,
                               self.Fin, self.H, self.layer_of, self._stream(), blob.data_ptr())
@@ -266,7 +282,7 @@ class NativeDDPGUpdate:
         self._hidden_fwd(tc, self.hid_c)
         self._critic_tail(tc, self.hid_c, 0, None, b)
         # critic on (s, a): loss + gradients
-        self._gnn_fwd(c, b.obs, self.emb["c"], self.blob["c"])
+        self._gnn_fwd(c, b.obs, self.emb["c"], self.blob["c"], key="c")
         self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], extra=b.actions, wa=self._wa(c, "c"))
         self._hidden_fwd(c, self.hid_c)
         C = c.width(c.nh - 1)
@@ -275,12 +291,12 @@ class NativeDDPGUpdate:
         self._head_reduce(c, C, 1)
         dh0 = self._hidden_bwd(c, self.hid_c, dh, grads=True)
         self._first_bwd(c, self.emb["c"], dh0, extra=b.actions)
-        self._gnn_bwd(c, b.obs, self.demb, self.blob["c"])
+        self._gnn_bwd(c, b.obs, self.demb, self.blob["c"], key="c")
 
     def stage_actor_fwd(self, b) -> None:
         """Actor embedding + hidden layers on s (independent of the critic step: overlaps its all-reduce)."""
         a = self.actor
-        self._gnn_fwd(a, b.obs, self.emb["a"], self.blob["a"])
+        self._gnn_fwd(a, b.obs, self.emb["a"], self.blob["a"], key="a")
         self._first(a, self.emb["a"], self._rowtab(a, "a"), self.hid_a[0])
         self._hidden_fwd(a, self.hid_a)
 
@@ -328,7 +344,7 @@ class NativeDDPGUpdate:
             gemm(self.dact, a.w16(last), "nn", out16=dz, gate=hl)
         dh0a = self._hidden_bwd(a, self.hid_a, dz, grads=True)
         self._first_bwd(a, self.emb["a"], dh0a)
-        self._gnn_bwd(a, b.obs, self.demb, self.blob["a"])
+        self._gnn_bwd(a, b.obs, self.demb, self.blob["a"], key="a")
 
     def last_metrics(self) -> dict:
         m = self.metrics
@@ -358,6 +374,11 @@ class NativeAct:
         self.rowtab = torch.zeros(self.T, n.width(0), device=dev)
         self.out = torch.zeros(E, self.A, device=dev)
         self.topo32 = torch.zeros(E, dtype=torch.int32, device=dev)
+        self.lw = None
+        if not gnn_fits(L.actor.embedder, L.graphs, self.P, self.Fin):
+            from gsc_amd.ops.gnn_lw import LayerwiseGAT
+            self.lw = LayerwiseGAT(self.tables, E, self.P, self.Fin, self.H, self.layer_of, dev)
+            self.ne = sum(p.numel() for p in L.actor.embedder.flat_parameters())
 
     @staticmethod
     def supported(learner) -> bool:
@@ -367,8 +388,11 @@ class NativeAct:
         n, s = self.net, torch.cuda.current_stream(self.L.device).cuda_stream
         assert obs.shape[0] == self.E and obs.is_contiguous() and obs.dtype == F32
         self.topo32.copy_(topo)
-        self.nat.gnn_forward(self.tables, n.emb_ptr(), obs.data_ptr(), self.topo32.data_ptr(), self.emb.data_ptr(),
-                             self.E, self.P, self.Fin, self.H, self.layer_of, s, 0)
+        if self.lw is not None:
+            self.lw.forward(n.fp.flat[:self.ne], obs, self.topo32, self.emb)
+        else:
+            self.nat.gnn_forward(self.tables, n.emb_ptr(), obs.data_ptr(), self.topo32.data_ptr(), self.emb.data_ptr(),
+                                 self.E, self.P, self.Fin, self.H, self.layer_of, s, 0)
         w = n.w16(0)
         self.nat.rowdot(self.masks.data_ptr(), self.masks.stride(0), self.T, w.data_ptr() + 2 * self.H, w.stride(0),
                         n.width(0), self.A, self.rowtab.data_ptr(), self.rowtab.stride(0), s)

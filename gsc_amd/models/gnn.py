@@ -14,7 +14,8 @@ convolutions (ReLU between, none after the last) and a mean pool over each graph
 Two implementations with identical semantics:
 * :func:`gatv2_dense_reference` — vectorised PyTorch (CPU path, autograd reference, tests);
 * ``gsc_amd.ops.gnn`` — one fused HIP kernel per direction (whole embedder per graph in LDS),
-  used automatically for CUDA tensors.
+  used automatically for CUDA tensors; graphs too large for LDS run the layer-wise native kernels
+  (``gsc_amd/ops/gnn_lw.py``: MFMA GEMM node linears + per-node attention kernels).
 """
 from __future__ import annotations
 
@@ -120,10 +121,11 @@ class GNNEmbedder(nn.Module):
         if use_native is None:
             use_native = x.is_cuda and _NATIVE_GNN
         if use_native:
-            from gsc_amd.ops.gnn import gnn_embed, gnn_fits
+            from gsc_amd.ops.gnn import gnn_embed, gnn_embed_layerwise, gnn_fits
             if gnn_fits(self, graphs, x.shape[1], x.shape[2]):
                 return gnn_embed(self, x, topo, graphs)
-            # graphs whose per-graph working set exceeds LDS (e.g. 200 nodes): PyTorch path
+            # graphs whose per-graph working set exceeds LDS (e.g. 200 nodes): layer-wise native kernels
+            return gnn_embed_layerwise(self, x, topo, graphs)
         return self.forward_reference(x, topo, graphs)
 
     def forward_reference(self, x, topo, graphs: GraphSet):

@@ -1,4 +1,6 @@
-"""Autograd wrapper around the fused HIP GATv2 embedder kernels (``csrc/ops/gnn.hip``)."""
+"""Autograd wrappers around the native GATv2 embedder kernels: the fused per-graph kernels
+(``csrc/ops/gnn.hip`` / ``gnn_mf.hip``) and, for graphs whose working set exceeds LDS, the
+layer-wise kernels (``gsc_amd/ops/gnn_lw.py``)."""
 from __future__ import annotations
 
 import os
@@ -114,3 +116,53 @@ def gnn_fits(embedder, graphs, P: int, Fin: int) -> bool:
 def gnn_embed(embedder, x: torch.Tensor, topo: torch.Tensor, graphs) -> torch.Tensor:
     params = embedder.flat_parameters()
     return _GnnEmbed.apply(x, topo, graphs, (embedder.hidden_dim, _layer_of(embedder), torch.is_grad_enabled()), *params)
+
+
+_LW_CACHE = {}
+
+
+def _lw(graphs, B: int, P: int, Fin: int, H: int, layer_of, dev, fresh: bool):
+    from .gnn_lw import LayerwiseGAT
+    if fresh:
+        return LayerwiseGAT(_tables(graphs), B, P, Fin, H, layer_of, dev)
+    key = (id(graphs), B, P, Fin, H, tuple(layer_of), str(dev))
+    lw = _LW_CACHE.get(key)
+    if lw is None:
+        lw = _LW_CACHE[key] = LayerwiseGAT(_tables(graphs), B, P, Fin, H, layer_of, dev)
+    return lw
+
+
+class _GnnEmbedLW(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, topo, graphs, meta, *params):
+        H, layer_of, grad_mode = meta
+        B, P, Fin = x.shape
+        flat = _flat(list(params)).contiguous()
+        x = x.contiguous().float()
+        topo32 = topo.to(torch.int32).contiguous()
+        need = grad_mode and any(ctx.needs_input_grad[4:])
+        lw = _lw(graphs, B, P, Fin, H, layer_of, x.device, fresh=need)
+        emb = torch.empty(B, H, device=x.device, dtype=torch.float32)
+        lw.forward(flat, x, topo32, emb)
+        ctx.lw, ctx.flat, ctx.shapes = lw, flat, [p.shape for p in params]
+        ctx.keep = (x, topo32)  # the saved forward references them
+        return emb
+
+    @staticmethod
+    def backward(ctx, demb):
+        grad = torch.empty_like(ctx.flat)
+        ctx.lw.backward(ctx.flat, demb.contiguous().float(), grad)
+        out, off = [], 0
+        for sh in ctx.shapes:
+            n = 1
+            for d in sh:
+                n *= d
+            out.append(grad[off:off + n].view(sh))
+            off += n
+        return (None, None, None, None, *out)
+
+
+def gnn_embed_layerwise(embedder, x: torch.Tensor, topo: torch.Tensor, graphs) -> torch.Tensor:
+    params = embedder.flat_parameters()
+    return _GnnEmbedLW.apply(x, topo, graphs, (embedder.hidden_dim, _layer_of(embedder), torch.is_grad_enabled()),
+                             *params)

@@ -1,0 +1,122 @@
+"""Layer-wise GATv2 embedder on native kernels, for graphs too large for the fused per-graph
+kernels (``gnn_fits`` false: e.g. the 200-node synthetic topologies of BASELINE config 5).
+
+Per conv (``csrc/ops/gnn_lw.hip``): node linears ``x_l = h W_l^T + b_l``, ``x_r = h W_r^T + b_r`` on
+the MFMA GEMM engine over all ``B x P`` node rows; attention + segment softmax + mean aggregation
+(+ bias, ReLU) per target node; mean pool per graph.  Backward: attention backward per target node
+(``d x_r`` gathered per target, ``d x_l`` per source through the source-sorted CSR), weight
+gradients ``dW = dX^T h`` (split-K GEMM, deterministic reduction), input gradients ``dX W`` (GEMM),
+vector gradients by deterministic column sums.  Same semantics as ``gatv2_dense_reference``
+(reference ``src/rlsp/agents/models.py:10-53``).
+
+A :class:`LayerwiseGAT` owns the workspaces of one batch size; ``forward(..., save=True)`` keeps
+every conv's inputs / ``x_l`` / ``x_r`` / attention weights for the following ``backward``.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from gsc_amd.native import load as load_native
+from .mlp import gemm
+
+
+def _block_size(Fi: int, H: int) -> int:
+    return 2 * H * Fi + 4 * H
+
+
+def _block_offset(b: int, Fin: int, H: int) -> int:
+    return 0 if b == 0 else _block_size(Fin, H) + (b - 1) * _block_size(H, H)
+
+
+class LayerwiseGAT:
+    def __init__(self, tables: dict, B: int, P: int, Fin: int, H: int, layer_of: List[int], device):
+        self.nat = load_native()
+        self.tables = tables
+        self.B, self.P, self.Fin, self.H = int(B), int(P), int(Fin), int(H)
+        self.layer_of = list(layer_of)
+        self.L = len(self.layer_of)
+        dev = torch.device(device)
+        self.dev = dev
+        R = self.B * self.P
+        M = int(tables["M"])
+        mk = lambda *s: torch.zeros(*s, device=dev, dtype=torch.float32)
+        self.xl = [mk(R, H) for _ in range(self.L)]
+        self.xr = [mk(R, H) for _ in range(self.L)]
+        self.alpha = [mk(self.B, M) for _ in range(self.L)]
+        self.hout = [mk(R, H) for _ in range(self.L)]
+        self.x = None                      # layer-0 input of the saved forward
+        # backward scratch
+        self.dh = [mk(R, H), mk(R, H)]
+        self.dxl, self.dxr, self.datt = mk(R, H), mk(R, H), mk(R, H)
+        self.msg = mk(self.B * M, H)
+        self.part = mk(1024 * max(H, 32))
+        self.slabs = mk(max(4 << 20, 64 * H * max(H, Fin)))
+        self.topo32 = None
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def _params(self, flat: torch.Tensor, blk: int):
+        H, Fin = self.H, self.Fin
+        Fi = Fin if blk == 0 else H
+        o = _block_offset(blk, Fin, H)
+        Wl = flat[o:o + H * Fi].view(H, Fi)
+        o += H * Fi
+        bl = flat[o:o + H]
+        o += H
+        Wr = flat[o:o + H * Fi].view(H, Fi)
+        o += H * Fi
+        br = flat[o:o + H]
+        o += H
+        att = flat[o:o + H]
+        o += H
+        bias = flat[o:o + H]
+        return Fi, Wl, bl, Wr, br, att, bias
+
+    def forward(self, flat: torch.Tensor, x: torch.Tensor, topo32: torch.Tensor, emb: torch.Tensor) -> None:
+        """flat: fp32 embedder parameters (module order); x [B, P, Fin] fp32; topo32 [B] int32; emb [B, H]."""
+        B, P, H = self.B, self.P, self.H
+        assert x.shape == (B, P, self.Fin) and x.is_contiguous() and x.dtype == torch.float32
+        assert topo32.dtype == torch.int32 and topo32.numel() == B
+        nat, s, t = self.nat, self._stream(), self.tables
+        self.x, self.topo32 = x, topo32
+        h = x.view(B * P, self.Fin)
+        for l, blk in enumerate(self.layer_of):
+            Fi, Wl, bl, Wr, br, att, bias = self._params(flat, blk)
+            gemm(h, Wl, "nt", out32=self.xl[l], bias=bl)
+            gemm(h, Wr, "nt", out32=self.xr[l], bias=br)
+            nat.lw_attn_fwd(t, topo32.data_ptr(), B, P, H, self.xl[l].data_ptr(), self.xr[l].data_ptr(),
+                            att.data_ptr(), bias.data_ptr(), int(l + 1 < self.L), self.hout[l].data_ptr(),
+                            self.alpha[l].data_ptr(), s)
+            h = self.hout[l]
+        nat.lw_pool(t, topo32.data_ptr(), B, P, H, self.hout[self.L - 1].data_ptr(), emb.data_ptr(), s)
+
+    def backward(self, flat: torch.Tensor, demb: torch.Tensor, grad: torch.Tensor) -> None:
+        """Gradients of the last ``forward`` into ``grad`` (fp32, module order; overwritten)."""
+        B, P, H, R = self.B, self.P, self.H, self.B * self.P
+        nat, s, t = self.nat, self._stream(), self.tables
+        tp = self.topo32.data_ptr()
+        cur, nxt = self.dh
+        nat.lw_pool_bwd(t, tp, B, P, H, demb.contiguous().data_ptr(), cur.data_ptr(), s)
+        seen = set()
+        for l in range(self.L - 1, -1, -1):
+            blk = self.layer_of[l]
+            Fi, Wl, bl, Wr, br, att, bias = self._params(flat, blk)
+            _, gWl, gbl, gWr, gbr, gatt, gbias = self._params(grad, blk)
+            acc = blk in seen
+            seen.add(blk)
+            hin = self.x.view(R, self.Fin) if l == 0 else self.hout[l - 1]
+            nat.lw_attn_bwd(t, tp, B, P, H, cur.data_ptr(), self.hout[l].data_ptr() if l + 1 < self.L else 0,
+                            self.xl[l].data_ptr(), self.xr[l].data_ptr(), self.alpha[l].data_ptr(), att.data_ptr(),
+                            self.dxr.data_ptr(), self.msg.data_ptr(), self.datt.data_ptr(), s)
+            nat.lw_src_gather(t, tp, B, P, H, self.msg.data_ptr(), self.dxl.data_ptr(), s)
+            gemm(self.dxl, hin, "tn", out32=gWl, splits=None, slabs=self.slabs, accumulate=acc)
+            gemm(self.dxr, hin, "tn", out32=gWr, splits=None, slabs=self.slabs, accumulate=acc)
+            for src, dst in ((self.dxl, gbl), (self.dxr, gbr), (self.datt, gatt), (cur, gbias)):
+                nat.lw_colsum(src.data_ptr(), R, H, H, self.part.data_ptr(), dst.data_ptr(), int(acc), s)
+            if l > 0:
+                gemm(self.dxl, Wl, "nn", out32=nxt)
+                gemm(self.dxr, Wr, "nn", out32=nxt, accumulate=True)
+                cur, nxt = nxt, cur

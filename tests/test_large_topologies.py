@@ -67,8 +67,15 @@ def test_syn200_sim_and_scheduler():
     sim.check_flags()
 
 
-def test_gnn_falls_back_for_graphs_beyond_lds():
+def test_gnn_native_path_for_graphs_beyond_lds():
+    """50-node graphs fit the fused per-graph kernels; 200-node graphs do not and run the layer-wise
+    native kernels (gsc_amd/ops/gnn_lw.py) -- no PyTorch GNN on the GPU (GPU numerics:
+    tests/test_gpu_gnn_lw.py)."""
+    import inspect
+    from gsc_amd.models import gnn as gnn_mod
     from gsc_amd.ops.gnn import gnn_fits
     e = GNNEmbedder(3, 22, 2, "mean", 2)
     assert gnn_fits(e, GraphSet([load_topology(SYN50)], 50, "cpu"), 50, 3)
     assert not gnn_fits(e, GraphSet([load_topology(SYN200[0])], 200, "cpu"), 200, 3)
+    src = inspect.getsource(gnn_mod.GNNEmbedder.forward)
+    assert "gnn_embed_layerwise" in src
