@@ -55,6 +55,10 @@ class LayerwiseGAT:
         self.slabs = mk(max(4 << 20, 64 * H * max(H, Fin)))
         self.topo32 = None
 
+    def _relu(self, l: int) -> bool:
+        # ReLU after every conv but the last -- and after a single conv (GNNEmbedder.forward_reference)
+        return l + 1 < self.L or self.L == 1
+
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.dev).cuda_stream
 
@@ -88,7 +92,7 @@ class LayerwiseGAT:
             gemm(h, Wl, "nt", out32=self.xl[l], bias=bl)
             gemm(h, Wr, "nt", out32=self.xr[l], bias=br)
             nat.lw_attn_fwd(t, topo32.data_ptr(), B, P, H, self.xl[l].data_ptr(), self.xr[l].data_ptr(),
-                            att.data_ptr(), bias.data_ptr(), int(l + 1 < self.L), self.hout[l].data_ptr(),
+                            att.data_ptr(), bias.data_ptr(), int(self._relu(l)), self.hout[l].data_ptr(),
                             self.alpha[l].data_ptr(), s)
             h = self.hout[l]
         nat.lw_pool(t, topo32.data_ptr(), B, P, H, self.hout[self.L - 1].data_ptr(), emb.data_ptr(), s)
@@ -108,7 +112,7 @@ class LayerwiseGAT:
             acc = blk in seen
             seen.add(blk)
             hin = self.x.view(R, self.Fin) if l == 0 else self.hout[l - 1]
-            nat.lw_attn_bwd(t, tp, B, P, H, cur.data_ptr(), self.hout[l].data_ptr() if l + 1 < self.L else 0,
+            nat.lw_attn_bwd(t, tp, B, P, H, cur.data_ptr(), self.hout[l].data_ptr() if self._relu(l) else 0,
                             self.xl[l].data_ptr(), self.xr[l].data_ptr(), self.alpha[l].data_ptr(), att.data_ptr(),
                             self.dxr.data_ptr(), self.msg.data_ptr(), self.datt.data_ptr(), s)
             nat.lw_src_gather(t, tp, B, P, H, self.msg.data_ptr(), self.dxl.data_ptr(), s)
