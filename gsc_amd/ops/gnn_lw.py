@@ -9,8 +9,9 @@ gradients ``dW = dX^T h`` (split-K GEMM, deterministic reduction), input gradien
 vector gradients by deterministic column sums.  Same semantics as ``gatv2_dense_reference``
 (reference ``src/rlsp/agents/models.py:10-53``).
 
-A :class:`LayerwiseGAT` owns the workspaces of one batch size; ``forward(..., save=True)`` keeps
-every conv's inputs / ``x_l`` / ``x_r`` / attention weights for the following ``backward``.
+A :class:`LayerwiseGAT` owns the workspaces of one batch size; ``forward`` keeps every conv's
+output / ``x_l`` / ``x_r`` / attention weights (and a reference to its input) for the following
+``backward``.
 """
 from __future__ import annotations
 
