@@ -32,7 +32,7 @@ from typing import List, Optional
 import torch
 
 from gsc_amd.native import load as load_native
-from gsc_amd.ops.gnn import _layer_of, _tables, gnn_fits
+from gsc_amd.ops.gnn import _layer_of, _tables, gnn_use_fused
 from gsc_amd.ops.mlp import gemm
 
 BF16 = torch.bfloat16
@@ -139,9 +139,9 @@ class NativeDDPGUpdate:
         self.Fin = Fin
         ne = sum(p.numel() for p in L.actor.embedder.flat_parameters())
         self.ne = ne
-        # graphs whose per-graph working set exceeds LDS (e.g. 200 nodes): layer-wise GNN kernels, one
+        # large graphs (beyond LDS, e.g. 200 nodes, or >= GSC_GNN_LW_MIN_NODES): layer-wise GNN kernels, one
         # workspace per saved forward ("a", "c") plus one for forwards without a backward
-        self.layerwise = not gnn_fits(L.actor.embedder, L.graphs, self.P, Fin)
+        self.layerwise = not gnn_use_fused(L.actor.embedder, L.graphs, self.P, Fin)
         if self.layerwise:
             from gsc_amd.ops.gnn_lw import LayerwiseGAT
             self.lwo = {k: LayerwiseGAT(self.tables, B, self.P, Fin, H, self.layer_of, dev) for k in ("a", "c", "-")}
@@ -375,7 +375,7 @@ class NativeAct:
         self.out = torch.zeros(E, self.A, device=dev)
         self.topo32 = torch.zeros(E, dtype=torch.int32, device=dev)
         self.lw = None
-        if not gnn_fits(L.actor.embedder, L.graphs, self.P, self.Fin):
+        if not gnn_use_fused(L.actor.embedder, L.graphs, self.P, self.Fin):
             from gsc_amd.ops.gnn_lw import LayerwiseGAT
             self.lw = LayerwiseGAT(self.tables, E, self.P, self.Fin, self.H, self.layer_of, dev)
             self.ne = sum(p.numel() for p in L.actor.embedder.flat_parameters())

@@ -121,10 +121,10 @@ class GNNEmbedder(nn.Module):
         if use_native is None:
             use_native = x.is_cuda and _NATIVE_GNN
         if use_native:
-            from gsc_amd.ops.gnn import gnn_embed, gnn_embed_layerwise, gnn_fits
-            if gnn_fits(self, graphs, x.shape[1], x.shape[2]):
+            from gsc_amd.ops.gnn import gnn_embed, gnn_embed_layerwise, gnn_use_fused
+            if gnn_use_fused(self, graphs, x.shape[1], x.shape[2]):
                 return gnn_embed(self, x, topo, graphs)
-            # graphs whose per-graph working set exceeds LDS (e.g. 200 nodes): layer-wise native kernels
+            # large graphs (beyond LDS, or >= GSC_GNN_LW_MIN_NODES nodes): layer-wise native kernels
             return gnn_embed_layerwise(self, x, topo, graphs)
         return self.forward_reference(x, topo, graphs)
 

@@ -103,6 +103,11 @@ class _GnnEmbed(torch.autograd.Function):
         return (None, None, None, None, *out)
 
 
+# graphs with at least this many nodes take the layer-wise kernels even when the fused per-graph
+# kernels would fit (GSC_GNN_LW_MIN_NODES; syn50 measured equal: 3981 vs 3977 env-steps/s, so off by default)
+_LW_MIN_NODES = int(os.environ.get("GSC_GNN_LW_MIN_NODES", "100000"))
+
+
 def gnn_fits(embedder, graphs, P: int, Fin: int) -> bool:
     """Fused kernels handle these graph sizes (per-graph working set fits one CU's LDS)."""
     key = ("_gnn_fits", embedder.hidden_dim, tuple(_layer_of(embedder)), P, Fin)
@@ -111,6 +116,11 @@ def gnn_fits(embedder, graphs, P: int, Fin: int) -> bool:
         cache[key] = bool(load_native().gnn_fused_fits(int(graphs.M), int(graphs.max_nodes), int(P), int(Fin),
                                                        int(embedder.hidden_dim), _layer_of(embedder)))
     return cache[key]
+
+
+def gnn_use_fused(embedder, graphs, P: int, Fin: int) -> bool:
+    """Fused per-graph kernels (small graphs) or the layer-wise kernels (large graphs)."""
+    return gnn_fits(embedder, graphs, P, Fin) and int(graphs.max_nodes) < _LW_MIN_NODES
 
 
 def gnn_embed(embedder, x: torch.Tensor, topo: torch.Tensor, graphs) -> torch.Tensor:
