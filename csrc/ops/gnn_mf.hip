@@ -392,166 +392,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 }
 
 // ---------------------------------------------------------------------------------------------
-// Packed forward: two graphs of <= 16 nodes per wave (rows 0-15 graph A, 16-31 graph B of every
-// 32x32 tile), so each latency-bound phase (linears, softmax passes, aggregation) serves two graphs.
-// The message lists are concatenated (B's node ids + 16): E stays block-diagonal, the per-message
-// loops cover both graphs, and the mean pool splits by row half.
-// ---------------------------------------------------------------------------------------------
-struct MfRows {  // valid node rows of a packed tile
-  int n0, n1;
-  __device__ __forceinline__ bool ok(int row) const { return row < n0 || (row >= 16 && row - 16 < n1); }
-};
-
-__device__ __forceinline__ void mf_load_pair(MfTopo& T, const ClArgs& a, int t0, int t1, int n1g, int lane, int& last0,
-                                             int& last1) {
-  const int m0 = a.nmsgs[t0], m1 = n1g ? a.nmsgs[t1] : 0;
-  T.m = m0 + m1;
-  if (last0 == t0 && last1 == (n1g ? t1 : -1)) return;
-  last0 = t0;
-  last1 = n1g ? t1 : -1;
-  const long o0 = (long)t0 * a.M, o1 = (long)t1 * a.M;
-  for (int i = lane; i < m0 + m1; i += 64) {
-    if (i < m0) {
-      T.isrc[i] = a.in_src[o0 + i];
-      T.idst[i] = a.in_dst[o0 + i];
-    } else {
-      T.isrc[i] = a.in_src[o1 + i - m0] + 16;
-      T.idst[i] = a.in_dst[o1 + i - m0] + 16;
-    }
-  }
-  if (lane < 32) {
-    const int v = lane & 15;
-    const int t = lane < 16 ? t0 : t1;
-    T.deg[lane] = (lane < 16 || n1g) && v < a.P ? a.deg[(long)t * a.P + v] : 1.f;
-  }
-  cl_wave_sync();
-}
-
-template <int HPF>
-__device__ __forceinline__ void mf_store_rows2(const f32x16& acc, const MfRows& R, float* img, int lane) {
-  const int r = lane & 31, hh = lane >> 5;
-  float* base = img + 4 * hh * HPF + r;
-  if (r < HPF) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int ro = (i & 3) + 8 * (i >> 2);
-      if (R.ok(ro + 4 * hh)) base[ro * HPF] = acc[i];
-    }
-  }
-}
-
-// One packed GATv2 layer (forward only).  LAST: returns this lane's partial pools of graph A (.x)
-// and graph B (.y); otherwise writes the ReLU output image.
-template <int HPF, bool K2, bool LAST>
-__device__ __forceinline__ float2 mf_layer2(const MfW& w, const float* vec, const MfTopo& T, const MfRows& R,
-                                            const __bf16* hin, float* xl, float* xr, float* alpha, int* mx, float* sm,
-                                            __bf16* E, __bf16* hout, int NVS, int H, int lane) {
-  const int r = lane & 31, hh = lane >> 5;
-  f32x16 al, ar;
-  mf_linear<K2>(w, vec, hin, 32, lane, al, ar);
-  mf_store_rows2<HPF>(al, R, xl, lane);
-  mf_store_rows2<HPF>(ar, R, xr, lane);
-  if (lane < 32) {
-    mx[lane] = kMfKeyNegInf;
-    sm[lane] = 0.f;
-  }
-  cl_wave_sync();
-  mf_softmax<HPF>(vec, T, xl, xr, alpha, mx, sm, E, NVS, true, lane);
-  const f32x16 y = mf_aggregate(al, vec, E, 32, NVS, lane);
-  if (LAST) {
-    float pa = 0.f, pb = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-      if (row < 16) pa += row < R.n0 ? y[i] : 0.f;
-      else pb += row - 16 < R.n1 ? y[i] : 0.f;
-    }
-    return make_float2(pa, pb);
-  }
-  __bf16* hb = hout + 4 * hh * kMfRS + r;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int ro = (i & 3) + 8 * (i >> 2);
-    hb[ro * kMfRS] = (__bf16)((R.ok(ro + 4 * hh) && r < H) ? fmaxf(y[i], 0.f) : 0.f);
-  }
-  cl_wave_sync();
-  return make_float2(0.f, 0.f);
-}
-
-template <int HPF, bool K2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gnn_mf_fwd2_kernel(ClArgs a, MfLayout m) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  mf_stage_vec(a, lds);
-  const bf16x8* frags = reinterpret_cast<const bf16x8*>(lds + mf_vec_floats(a.n_blocks));
-  mf_stage_frags(a, reinterpret_cast<bf16x8*>(lds + mf_vec_floats(a.n_blocks)), 2);
-  __syncthreads();
-  char* const W0 = reinterpret_cast<char*>(lds + mf_vec_floats(a.n_blocks) + 2 * kMfFragSet);
-  int woff = wave * m.per_wave;
-  const int half = lane >> 5, c = lane & 31;
-  int last0 = -1, last1 = -2;
-  const int pairs = (a.B + 1) >> 1;
-  for (int pr = blockIdx.x * a.waves + wave; pr < pairs; pr += gridDim.x * a.waves) {
-    asm volatile("" : "+v"(woff));  // see gnn_mf_bwd_kernel
-    char* W = W0 + woff;
-    __bf16* hA = reinterpret_cast<__bf16*>(W + m.hR[0]);
-    __bf16* hB = reinterpret_cast<__bf16*>(W + m.hR[1]);
-    float* xl = reinterpret_cast<float*>(W + m.xl);
-    float* xr = reinterpret_cast<float*>(W + m.xr);
-    float* al = reinterpret_cast<float*>(W + m.al[0]);
-    __bf16* E = reinterpret_cast<__bf16*>(W + m.E);
-    int* mx = reinterpret_cast<int*>(W + m.mx);
-    float* sm = reinterpret_cast<float*>(W + m.sm);
-    MfTopo T;
-    T.isrc = reinterpret_cast<int*>(W + m.topo);
-    T.idst = T.isrc + 2 * a.M;
-    T.deg = reinterpret_cast<float*>(T.idst + 2 * a.M);
-    const int g0 = 2 * pr, g1 = g0 + 1;
-    const int has1 = g1 < a.B;
-    const int t0 = a.topo[g0], t1 = has1 ? a.topo[g1] : t0;
-    mf_load_pair(T, a, t0, t1, has1, lane, last0, last1);
-    MfRows R{a.nnodes[t0], has1 ? a.nnodes[t1] : 0};
-    // both graphs' inputs -> rows 0-15 / 16-31 of the bf16 image; clear E (block-diagonal per pair)
-    for (int i = lane; i < 32 * 32; i += 64) {
-      const int v = i >> 5, k = i & 31;
-      const int gi = v >> 4, vv = v & 15;
-      const int n = gi ? R.n1 : R.n0;
-      const float* xg = a.x + (long)(gi ? g1 : g0) * a.P * a.Fin;
-      hA[v * kMfRS + k] = (__bf16)((vv < n && k < a.Fin) ? xg[vv * a.Fin + k] : 0.f);
-    }
-    for (int i = lane; i < 32 * m.NVS / 8; i += 64) reinterpret_cast<uint4*>(E)[i] = make_uint4(0, 0, 0, 0);
-    cl_wave_sync();
-    __bf16* hin = hA;
-    __bf16* hout = hB;
-    float2 pool = make_float2(0.f, 0.f);
-    for (int l = 0; l < a.L; ++l) {
-      const float* vec = lds + (l == 0 ? 0 : kMfVec);
-      if (l + 1 < a.L) {
-        if (l == 0)
-          mf_layer2<HPF, false, false>(mf_frags(frags, 0, lane), vec, T, R, hin, xl, xr, al, mx, sm, E, hout, m.NVS,
-                                       a.H, lane);
-        else
-          mf_layer2<HPF, K2, false>(mf_frags(frags, 1, lane), vec, T, R, hin, xl, xr, al, mx, sm, E, hout, m.NVS, a.H,
-                                    lane);
-        __bf16* t = hin;
-        hin = hout;
-        hout = t;
-      } else {
-        pool = mf_layer2<HPF, K2, true>(mf_frags(frags, 1, lane), vec, T, R, hin, xl, xr, al, mx, sm, E, nullptr,
-                                        m.NVS, a.H, lane);
-      }
-    }
-    pool.x += __shfl_xor(pool.x, 32);
-    pool.y += __shfl_xor(pool.y, 32);
-    if (half == 0 && c < a.H) {
-      a.emb[(long)g0 * a.H + c] = pool.x / (float)R.n0;
-      if (has1) a.emb[(long)g1 * a.H + c] = pool.y / (float)R.n1;
-    }
-    cl_wave_sync();
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ void mf_zero(f32x16& t) {
@@ -1022,55 +862,8 @@ bool gnn_mf_supported(int Fin, int H, int NM, int L, int n_blocks, const int* la
   return true;
 }
 
-static MfLayout mf_layout_pair(const ClArgs& a, int HPF) {
-  MfLayout m{};
-  m.NV = 32;
-  m.NVS = 40;
-  int o = 0;
-  auto take = [&](int bytes) {
-    const int at = o;
-    o += (bytes + 15) & ~15;
-    return at;
-  };
-  const int hRb = 32 * kMfRS * 2, fb = 32 * HPF * 4;
-  m.hR[0] = take(hRb);
-  m.hR[1] = take(hRb);
-  m.al[0] = take(((2 * a.M + 3) & ~3) * 4);
-  m.xl = take(fb);
-  m.xr = take(fb);
-  m.E = take(32 * m.NVS * 2);
-  m.mx = take(32 * 4);
-  m.sm = take(32 * 4);
-  m.topo = take((4 * a.M + 32) * 4);
-  m.per_wave = (o + 15) & ~15;
-  return m;
-}
-
-template <int HPF, bool K2>
-static void mf_launch_fwd_pair(ClArgs a, hipStream_t st, int cus) {
-  const MfLayout m = mf_layout_pair(a, HPF);
-  a.waves = 4;
-  const size_t lds = sizeof(float) * (mf_vec_floats(a.n_blocks) + 2 * kMfFragSet) + (size_t)a.waves * m.per_wave;
-  GSC_CHECK(lds <= 160 * 1024, "GNN (MFMA, packed) forward working set exceeds LDS");
-  const void* fn = (const void*)gnn_mf_fwd2_kernel<HPF, K2>;
-  if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  int per_cu = (int)((160 * 1024) / lds);
-  if (per_cu > 4) per_cu = 4;  // 4 waves/SIMD (VGPR budget)
-  const int pairs = (a.B + 1) / 2;
-  const int need = (pairs + a.waves - 1) / a.waves;
-  const int cap = cus * (per_cu > 0 ? per_cu : 1);
-  const int grid = need < cap ? need : cap;
-  hipLaunchKernelGGL((gnn_mf_fwd2_kernel<HPF, K2>), dim3(grid > 0 ? grid : 1), dim3(64 * a.waves), lds, st, a, m);
-  check_launch();
-}
-
 template <int HPF, bool K2>
 static void mf_launch_fwd(ClArgs a, hipStream_t st, int cus) {
-  static const bool pack = getenv("GSC_GNN_PACK") ? atoi(getenv("GSC_GNN_PACK")) != 0 : true;
-  if (pack && a.blob == nullptr && a.NM <= 16) {
-    mf_launch_fwd_pair<HPF, K2>(a, st, cus);
-    return;
-  }
   const bool save = a.blob != nullptr;
   const MfLayout m = mf_layout(a, save, HPF);
   a.waves = 4;

@@ -69,25 +69,6 @@ def test_gnn_mfma_matches_reference(layers, iters, hidden):
         nat.gnn_set_path(old)
 
 
-@pytest.mark.parametrize("layers,iters,hidden", [(2, 2, 22), (2, 2, 16), (2, 2, 32), (1, 1, 22), (3, 1, 22)])
-def test_gnn_mfma_packed_forward_matches_reference(layers, iters, hidden):
-    """Two graphs per wave (<= 16 nodes each: Abilene + triangle, mixed per pair, odd batch so the
-    last wave holds one graph) -- the default forward for Abilene-sized graphs."""
-    gs = GraphSet([load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml")),
-                   load_topology(cfg_path("networks", "triangle", "triangle-in1-cap10-delay10.graphml"))], 24, DEV)
-    assert gs.max_nodes <= 16
-    _check_gnn(layers, iters, hidden, gs=gs, bf16=True)
-    # the packed forward of one graph equals its forward inside any pair
-    torch.manual_seed(1)
-    emb = GNNEmbedder(3, hidden, layers, "mean", iters).to(DEV)
-    topo = torch.randint(0, 2, (65,), device=DEV)
-    x = torch.rand(65, 24, 3, device=DEV) * gs.node_mask[topo].unsqueeze(-1)
-    with torch.no_grad():
-        full = emb(x, topo, gs, use_native=True)
-        single = torch.cat([emb(x[i:i + 1], topo[i:i + 1], gs, use_native=True) for i in (0, 1, 64)])
-    assert torch.equal(full[[0, 1, 64]], single)
-
-
 def test_gnn_mfma_is_default_and_deterministic():
     """The default path is the MFMA one for GSC shapes, and its gradients are bitwise reproducible."""
     from gsc_amd.native import load
