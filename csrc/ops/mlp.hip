@@ -66,6 +66,7 @@ struct Epilogue {
   const float* rowscale;  // [M]: multiply row m
   int relu, clamp, accumulate;
   int single_topo;       // rowtab / colmask have one row (every topo[m] == 0): no per-row gathers
+  int vec16;             // c16 base 16-byte aligned and ldc16 % 8 == 0: staged 16-byte row stores
   float lo, hi;
   float* c32;            // fp32 out (or split-K slabs)
   long ldc32;
@@ -254,6 +255,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   float* c32 = e.c32 ? e.c32 + (split ? (long)blockIdx.z * g.slab : 0) : nullptr;
   const int col_l = lane & 31, hh = lane >> 5;
   const bool per_row_topo = (e.rowtab || e.colmask) && !e.single_topo;
+  // bf16 output through LDS (per-wave sub-tile, padded rows) when the output rows are 16-byte aligned
+  constexpr int LDT = 32 * RN + 8;
+  static_assert(4 * (32 * RM) * LDT <= 2 * (A_ELEMS + B_ELEMS), "epilogue staging tile exceeds the LDS buffers");
+  const bool stage16 = !split && e.c16 && e.vec16;
+  short* stile = smem + wave * (32 * RM) * LDT;
+  if (stage16) __syncthreads();  // every wave is done reading the operand tiles
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
     // topology of this lane's 16 rows, loaded once per row block (all gathers issued up front)
@@ -308,7 +315,29 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         if (e.rowscale) v *= e.rowscale[m];
         if (e.clamp) v = fminf(fmaxf(v, e.lo), e.hi);
         if (c32) c32[m * e.ldc32 + n] = v;
-        if (e.c16) e.c16[m * e.ldc16 + n] = __float2bfloat16(v);
+        if (e.c16) {
+          if (stage16) stile[(32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh) * LDT + 32 * j + col_l] = f2bf(v);
+          else e.c16[m * e.ldc16 + n] = __float2bfloat16(v);
+        }
+      }
+    }
+  }
+  if (stage16) {
+    // bf16 output staged through LDS: each lane stores 16 contiguous bytes of a row (full-line
+    // writes instead of 2-byte column scatters)
+    __builtin_amdgcn_wave_barrier();
+    constexpr int CPR = 32 * RN / 8;  // 16-byte chunks per sub-tile row
+    const long mb = m0 + wm * 32 * RM, nb = n0 + wn * 32 * RN;
+    for (int idx = lane; idx < 32 * RM * CPR; idx += 64) {
+      const int row = idx / CPR, ch = idx % CPR;
+      const long m = mb + row, n = nb + 8 * ch;
+      if (m >= g.M) continue;
+      const short* src = stile + row * LDT + 8 * ch;
+      if (n + 8 <= g.N) {
+        *reinterpret_cast<s16x8*>(reinterpret_cast<short*>(e.c16) + m * e.ldc16 + n) =
+            *reinterpret_cast<const s16x8*>(src);
+      } else {
+        for (int k = 0; k < 8 && n + k < g.N; ++k) reinterpret_cast<short*>(e.c16)[m * e.ldc16 + n + k] = src[k];
       }
     }
   }
@@ -606,6 +635,7 @@ void gemm(int layout, int M, int N, int K, uintptr_t a, long lda, int adt, uintp
   e.ldc32 = gl("ldc32", N);
   e.c16 = ptr<__hip_bfloat16>(gp("c16"));
   e.ldc16 = gl("ldc16", N);
+  e.vec16 = e.c16 && (gp("c16") % 16 == 0) && (e.ldc16 % 8 == 0);
   const int tile = ep.contains("tile") ? ep["tile"].cast<int>() : 0;
   int splits = ep.contains("splits") ? ep["splits"].cast<int>() : 1;
   constexpr int BK = 32;
