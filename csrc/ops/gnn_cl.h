@@ -18,6 +18,7 @@ struct ClClock {
     if (on) last = __builtin_amdgcn_s_memtime();
   }
   __device__ __forceinline__ void mark(int k) {
+    if (__builtin_constant_p(on) && !on) return;
     if (on) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
       acc[k] += t - last;

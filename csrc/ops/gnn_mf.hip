@@ -591,8 +591,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (int k = 0; k < CG; ++k) gattE[k] = gattP[k] = 0.f;
   const int NV = m.NV, NVS = m.NVS;
   int woff = wave * m.per_wave;
+  // phase counters compiled out (a runtime-enabled clock pinned 26 registers for the whole loop and
+  // pushed the kernel into scratch spills); gnn_bench's phase profile uses the channel-lane kernels
   ClClock ck;
-  ck.start(a.prof != nullptr);
+  ck.start(false);
   for (int g = blockIdx.x * a.waves + wave; g < a.B; g += gridDim.x * a.waves) {
     // opaque per-iteration base: stops LICM from materialising (and spilling) dozens of per-lane
     // LDS addresses for the whole loop; they are cheap to recompute
