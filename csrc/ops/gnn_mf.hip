@@ -92,6 +92,13 @@ __device__ __forceinline__ int mf_key(float f) {
   return k >= 0 ? k : k ^ 0x7fffffff;
 }
 __device__ __forceinline__ float mf_unkey(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff); }
+// lane id through an opaque asm: lane-derived LDS addresses are recomputed where they are used instead
+// of being hoisted out of the graph / layer loops, where they exceed the register budget and spill
+__device__ __forceinline__ int mf_lane() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 
 // 8 weights as one bf16 fragment: W is [H][Fi] fp32 (module layout).  !trans: W[row][col0 + j]
 // (B operand of X = h W^T); trans: W[col0 + j][row] (B operand of dh = dX W).
@@ -600,6 +607,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // LDS addresses for the whole loop; they are cheap to recompute
     asm volatile("" : "+v"(woff));
     W = W0 + woff;
+    const int lane = mf_lane(), c = lane & 31, half = lane >> 5;
     float* xl = reinterpret_cast<float*>(W + m.xl);
     float* xr = reinterpret_cast<float*>(W + m.xr);
     float* dy = reinterpret_cast<float*>(W + m.dy);
@@ -625,6 +633,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // forward recompute: keep each conv's input (both bf16 images) and alpha; the last conv's
     // output is not needed (its gradient comes from the mean pool)
     for (int l = 0; !LOADED && l < a.L; ++l) {
+      const int lane = mf_lane();
       const float* vec = lds + (l == 0 ? 0 : kMfVec);
       const __bf16* hin = reinterpret_cast<const __bf16*>(W + m.hR[l]);
       float* al = reinterpret_cast<float*>(W + m.al[l]);
@@ -651,6 +660,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       mf_store_rows<HPF>(dyt, n, dy, lane);
     }
     for (int l = a.L - 1; l >= 0; --l) {
+      const int lane = mf_lane(), r = lane & 31, hh = lane >> 5;
       const float* vec = lds + (l == 0 ? 0 : kMfVec);
       const __bf16* hin = reinterpret_cast<const __bf16*>(W + m.hR[l]);
       const __bf16* hT = reinterpret_cast<const __bf16*>(W + m.hT[l]);
