@@ -165,6 +165,9 @@ __device__ __forceinline__ MfW mf_frags(const bf16x8* img, int b, int lane) {
 }
 
 __host__ __device__ __forceinline__ int mf_vec_floats(int n_blocks) { return n_blocks * kMfVec; }
+// fp32 [node][channel] row stride (x_l, x_r, dy images): HPF + 4 floats = 16 B x odd, so the per-message
+// row gathers (ds_read_b128 / b64 at different nodes) of up to 16 distinct rows hit distinct banks
+__host__ __device__ constexpr int mf_xs(int HPF) { return HPF + 4; }
 
 // X_l, X_r = h W^T + b: D[v][c] with lane column c and node rows in the 16 accumulators.
 template <bool K2>
@@ -193,13 +196,13 @@ template <int HPF>
 __device__ __forceinline__ void mf_store_rows(const f32x16& acc, int n, float* img, int lane) {
   // one base address + compile-time row offsets (immediate ds_write offsets, no per-row registers)
   const int r = lane & 31, hh = lane >> 5;
-  float* base = img + 4 * hh * HPF + r;
+  float* base = img + 4 * hh * mf_xs(HPF) + r;
   const int nn = n - 4 * hh;
   if (r < HPF) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ro = (i & 3) + 8 * (i >> 2);
-      if (ro < nn) base[ro * HPF] = acc[i];
+      if (ro < nn) base[ro * mf_xs(HPF)] = acc[i];
     }
   }
 }
@@ -214,8 +217,8 @@ __device__ __forceinline__ void mf_softmax(const float* vec, const MfTopo& T, co
   asm volatile("" ::: "memory");  // att is re-read from LDS per layer rather than held in VGPRs
   for (int q = lane; q < m; q += 64) {
     const int i = T.idst[q];
-    const float* xj = xl + T.isrc[q] * HPF;
-    const float* xi = xr + i * HPF;
+    const float* xj = xl + T.isrc[q] * mf_xs(HPF);
+    const float* xi = xr + i * mf_xs(HPF);
     float s = 0.f;
 #pragma unroll 2
     for (int k4 = 0; k4 < HPF / 4; ++k4) {
@@ -452,8 +455,8 @@ __device__ __forceinline__ void mf_layer_bwd(const ClArgs& a, const MfW* wT, con
   // p_q = alpha_q (dy[i] . x_l[j]) / deg_i ; ssum_i = sum_{q -> i} p_q ; E^T[j][i] = alpha_q / deg_i
   for (int q = lane; q < m; q += 64) {
     const int i = T.idst[q], j = T.isrc[q];
-    const float* gi = dy + i * HPF;
-    const float* xj = xl + j * HPF;
+    const float* gi = dy + i * mf_xs(HPF);
+    const float* xj = xl + j * mf_xs(HPF);
     float s = 0.f;
 #pragma unroll 2
     for (int k4 = 0; k4 < HPF / 4; ++k4) {
@@ -479,8 +482,8 @@ __device__ __forceinline__ void mf_layer_bwd(const ClArgs& a, const MfW* wT, con
 #pragma unroll
     for (int k2 = 0; k2 < CG / 2; ++k2) {
       const int cx = c0 + 2 * k2;
-      const float2 l2 = *reinterpret_cast<const float2*>(xl + j * HPF + cx);
-      const float2 r2 = *reinterpret_cast<const float2*>(xr + i * HPF + cx);
+      const float2 l2 = *reinterpret_cast<const float2*>(xl + j * mf_xs(HPF) + cx);
+      const float2 r2 = *reinterpret_cast<const float2*>(xr + i * mf_xs(HPF) + cx);
       const float2 t2 = *reinterpret_cast<const float2*>(vec + 64 + cx);
       const float z0 = l2.x + r2.x, z1 = l2.y + r2.y;
       gatt[2 * k2] = fmaf(de, z0 > 0.f ? z0 : kClSlope * z0, gatt[2 * k2]);
@@ -824,7 +827,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 static MfLayout mf_layout(const ClArgs& a, bool bwd, int HPF) {
   MfLayout m{};
   m.NV = a.NM <= 16 ? 16 : 32;
-  m.NVS = m.NV + 8;
+  m.NVS = m.NV + 4;  // [k][node] rows: NV + 4 bf16 keeps b64 row reads / writes of 16-32 rows conflict-free
   m.MS = a.MP + 8;
   int o = 0;
   auto take = [&](int bytes) {
@@ -834,7 +837,7 @@ static MfLayout mf_layout(const ClArgs& a, bool bwd, int HPF) {
   };
   m.hTrows0 = (a.Fin + 3) & ~3;
   m.hTrows = HPF;
-  const int hRb = m.NV * kMfRS * 2, M4b = ((a.M + 3) & ~3) * 4, fb = a.NM * HPF * 4;
+  const int hRb = m.NV * kMfRS * 2, M4b = ((a.M + 3) & ~3) * 4, fb = a.NM * mf_xs(HPF) * 4;
   const int Nb = ((a.NM + 3) & ~3) * 4;
   if (bwd) {
     for (int l = 0; l < a.L; ++l) {
