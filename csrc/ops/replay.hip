@@ -11,8 +11,11 @@
 // with u the 32-bit Philox4x32-10 word (key = (seed, "repl"), counter = (draw << 32) | b / 4, word
 // b % 4) -- independent of launch shape, identical on the host path (CPU training, tests).
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <cstring>
+#include <tuple>
+#include <vector>
 
 #include "../common.h"
 #include "../sim/philox.h"
@@ -66,6 +69,66 @@ __global__ __launch_bounds__(256) void insert_rows_kernel(const ReplayState* __r
     if constexpr (KIND == 0) reinterpret_cast<G*>(dst)[d] = reinterpret_cast<const G*>(src)[i];
     if constexpr (KIND == 1) reinterpret_cast<__bf16*>(dst)[d] = (__bf16)reinterpret_cast<const float*>(src)[i];
     if constexpr (KIND == 2) reinterpret_cast<float*>(dst)[d] = (float)reinterpret_cast<const uint8_t*>(src)[i];
+  }
+}
+
+// ---- every column of a sample / insert in one launch ----------------------------------------------
+// A column is a [rows, row_g granules] tensor; granules of gsz bytes (16/8/4/2/1).  Gather kinds:
+// 0 copy, 3 int64 -> int32 (topology ids straight into the learner's int32 buffer).  Insert kinds as
+// insert_rows_kernel (0 copy, 1 f32 -> bf16, 2 u8 -> f32); row_g counts elements for kinds 1 / 2.
+constexpr int kMaxCols = 8;
+struct RCol {
+  const char* src;
+  char* dst;
+  long row_g;
+  int gsz, kind;
+};
+struct RCols {
+  RCol c[kMaxCols];
+  long start[kMaxCols + 1];  // prefix sums of rows * row_g (work items per column)
+  int n;
+};
+
+__device__ __forceinline__ void copy_granule(const char* s, char* d, int gsz) {
+  switch (gsz) {
+    case 16: *reinterpret_cast<int4*>(d) = *reinterpret_cast<const int4*>(s); break;
+    case 8: *reinterpret_cast<int2*>(d) = *reinterpret_cast<const int2*>(s); break;
+    case 4: *reinterpret_cast<int*>(d) = *reinterpret_cast<const int*>(s); break;
+    case 2: *reinterpret_cast<short*>(d) = *reinterpret_cast<const short*>(s); break;
+    default: *d = *s; break;
+  }
+}
+
+// dst_c[b] = src_c[idx[b]] for every column; block 0 also advances the draw counter (the index
+// kernel that consumed it has completed)
+__global__ __launch_bounds__(256) void gather_cols_kernel(RCols cs, const int32_t* __restrict__ idx, int B,
+                                                          ReplayState* st) {
+  if (st != nullptr && blockIdx.x == 0 && threadIdx.x == 0) st->draws += 1;
+  const long total = cs.start[cs.n];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c = 0;
+    while (i >= cs.start[c + 1]) ++c;
+    const RCol& col = cs.c[c];
+    const long j = i - cs.start[c], b = j / col.row_g, k = j - b * col.row_g;
+    const long sr = (long)idx[b] * col.row_g + k;
+    if (col.kind == 3) reinterpret_cast<int32_t*>(col.dst)[j] = (int32_t)reinterpret_cast<const long long*>(col.src)[sr];
+    else copy_granule(col.src + sr * col.gsz, col.dst + j * col.gsz, col.gsz);
+  }
+  (void)B;
+}
+
+__global__ __launch_bounds__(256) void insert_cols_kernel(RCols cs, const ReplayState* __restrict__ st, long long cap) {
+  const long long pos = st->pos;
+  const long total = cs.start[cs.n];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    int c = 0;
+    while (i >= cs.start[c + 1]) ++c;
+    const RCol& col = cs.c[c];
+    const long j = i - cs.start[c], e = j / col.row_g, k = j - e * col.row_g;
+    const long d = ((pos + e) % cap) * col.row_g + k;
+    if (col.kind == 1) reinterpret_cast<__bf16*>(col.dst)[d] = (__bf16)reinterpret_cast<const float*>(col.src)[j];
+    else if (col.kind == 2) reinterpret_cast<float*>(col.dst)[d] = (float)reinterpret_cast<const uint8_t*>(col.src)[j];
+    else copy_granule(col.src + j * col.gsz, col.dst + d * col.gsz, col.gsz);
   }
 }
 
@@ -167,6 +230,57 @@ void replay_insert(bool device, uintptr_t state, uintptr_t src, uintptr_t dst, i
   check_launch();
 }
 
+static int granule_of(long bytes, uintptr_t a, uintptr_t b) {
+  const uintptr_t al = a | b | (uintptr_t)bytes;
+  return al % 16 == 0 ? 16 : al % 8 == 0 ? 8 : al % 4 == 0 ? 4 : al % 2 == 0 ? 2 : 1;
+}
+
+// One sample: Philox indices (as replay_sample_indices) then every column gathered by one kernel.
+// cols: (src, dst, row_bytes, kind) with kind 0 copy / 3 int64 -> int32 (row_bytes = 8).
+void replay_sample_cols(bool device, uintptr_t state, uint32_t seed, int B, long long cap, uintptr_t idx,
+                        const std::vector<std::tuple<uintptr_t, uintptr_t, long, int>>& cols, uintptr_t stream) {
+  GSC_CHECK(!cols.empty() && (int)cols.size() <= kMaxCols, "replay_sample_cols: 1..8 columns");
+  if (!device) {
+    host_indices(ptr<ReplayState>(state), seed, B, cap, ptr<int32_t>(idx));
+    const int32_t* ix = ptr<int32_t>(idx);
+    for (const auto& c : cols) {
+      const uintptr_t src = std::get<0>(c), dst = std::get<1>(c);
+      const long rb = std::get<2>(c);
+      for (int b = 0; b < B; ++b) {
+        if (std::get<3>(c) == 3) ptr<int32_t>(dst)[b] = (int32_t)ptr<const long long>(src)[ix[b]];
+        else std::memcpy(ptr<char>(dst) + (long)b * rb, ptr<char>(src) + (long)ix[b] * rb, rb);
+      }
+    }
+    return;
+  }
+  RCols cs{};
+  cs.n = (int)cols.size();
+  cs.start[0] = 0;
+  for (int i = 0; i < cs.n; ++i) {
+    const auto& c = cols[i];
+    RCol& r = cs.c[i];
+    r.src = ptr<const char>(std::get<0>(c));
+    r.dst = ptr<char>(std::get<1>(c));
+    r.kind = std::get<3>(c);
+    const long rb = std::get<2>(c);
+    GSC_CHECK(r.kind == 0 || (r.kind == 3 && rb == 8), "replay_sample_cols: kind 0 or 3 (int64 rows)");
+    r.gsz = r.kind == 3 ? 8 : granule_of(rb, std::get<0>(c), std::get<1>(c));
+    r.row_g = rb / r.gsz;
+    cs.start[i + 1] = cs.start[i] + (long)B * r.row_g;
+  }
+  const hipStream_t s = stream_of(stream);
+  hipLaunchKernelGGL(replay_index_kernel, dim3((B + 255) / 256), dim3(256), 0, s, ptr<const ReplayState>(state), seed,
+                     B, cap, ptr<int32_t>(idx));
+  hipLaunchKernelGGL(gather_cols_kernel, dim3(grid_for(cs.start[cs.n])), dim3(256), 0, s, cs, ptr<const int32_t>(idx), B,
+                     ptr<ReplayState>(state));
+  check_launch();
+}
+
+// One insert of E rows at the cursor for every column, then the cursor advance.
+// cols: (src, dst, row_n, kind) as replay_insert.
+void replay_insert_cols(bool device, uintptr_t state, int E, long long cap,
+                        const std::vector<std::tuple<uintptr_t, uintptr_t, long, int>>& cols, uintptr_t stream);
+
 void replay_advance(bool device, uintptr_t state, int E, long long cap, uintptr_t stream) {
   if (!device) {
     ReplayState* st = ptr<ReplayState>(state);
@@ -217,6 +331,37 @@ void step_metrics(bool device, uintptr_t stats, int nstats, uintptr_t ep_return,
   check_launch();
 }
 
+void replay_insert_cols(bool device, uintptr_t state, int E, long long cap,
+                        const std::vector<std::tuple<uintptr_t, uintptr_t, long, int>>& cols, uintptr_t stream) {
+  GSC_CHECK(!cols.empty() && (int)cols.size() <= kMaxCols, "replay_insert_cols: 1..8 columns");
+  if (!device) {
+    for (const auto& c : cols)
+      replay_insert(false, state, std::get<0>(c), std::get<1>(c), E, std::get<2>(c), cap, std::get<3>(c), 0);
+    replay_advance(false, state, E, cap, 0);
+    return;
+  }
+  RCols cs{};
+  cs.n = (int)cols.size();
+  cs.start[0] = 0;
+  for (int i = 0; i < cs.n; ++i) {
+    const auto& c = cols[i];
+    RCol& r = cs.c[i];
+    r.src = ptr<const char>(std::get<0>(c));
+    r.dst = ptr<char>(std::get<1>(c));
+    r.kind = std::get<3>(c);
+    const long rn = std::get<2>(c);
+    GSC_CHECK(r.kind >= 0 && r.kind <= 2, "replay_insert_cols: kind 0..2");
+    r.gsz = r.kind == 0 ? granule_of(rn, std::get<0>(c), std::get<1>(c)) : 1;
+    r.row_g = r.kind == 0 ? rn / r.gsz : rn;
+    cs.start[i + 1] = cs.start[i] + (long)E * r.row_g;
+  }
+  const hipStream_t s = stream_of(stream);
+  hipLaunchKernelGGL(insert_cols_kernel, dim3(grid_for(cs.start[cs.n])), dim3(256), 0, s, cs,
+                     ptr<const ReplayState>(state), cap);
+  hipLaunchKernelGGL(replay_advance_kernel, dim3(1), dim3(1), 0, s, ptr<ReplayState>(state), E, cap);
+  check_launch();
+}
+
 int replay_index_host(uint32_t seed, long long draw, int b, long long pos, long long full, long long cap) {
   return replay_index(seed, draw, b, pos, full, cap);
 }
@@ -226,6 +371,8 @@ void register_replay(py::module_& m) {
   m.def("replay_gather", &replay_gather);
   m.def("replay_insert", &replay_insert);
   m.def("replay_advance", &replay_advance);
+  m.def("replay_sample_cols", &replay_sample_cols, "Philox indices + every column gathered in one kernel");
+  m.def("replay_insert_cols", &replay_insert_cols, "every column inserted in one kernel + cursor advance");
   m.def("replay_index", &replay_index_host, "one sampled index (host; for tests)");
   m.def("step_metrics", &step_metrics, "trainer metric accumulators (succ, drop, finished return, finished)");
 }

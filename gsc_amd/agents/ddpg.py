@@ -88,6 +88,7 @@ class DDPGLearner:
         self.native_ok = (self.device.type == "cuda" and self.amp and not self.actor.squash and self.actor.graph_mode
                           and os.environ.get("GSC_NATIVE_LEARNER", "1") != "0")
         self._native = None
+        self._topo_ready = False
         self._act_native = None
 
     def _autocast(self):
@@ -179,6 +180,11 @@ class DDPGLearner:
             self._native = NativeDDPGUpdate(self, batch_size)
         return self._native
 
+    def topo32_buffer(self, batch_size: int) -> Optional[torch.Tensor]:
+        """The int32 topology-id buffer the native update reads (a replay sampler can gather into it
+        directly, see ``update_graphed(topo_ready=True)``), or None off the native path."""
+        return self.native_update(batch_size).topo32 if self.native_ok else None
+
     def update(self, b: Batch) -> None:
         """One DDPG update, eager.
 
@@ -207,8 +213,11 @@ class DDPGLearner:
         if self.native_ok:
             nu = self.native_update(b.obs.shape[0])
 
+            topo_ready = self._topo_ready
+
             def s1():
-                nu.prepare(b)
+                if not topo_ready:   # else the replay sampler gathered the int32 ids itself
+                    nu.prepare(b)
                 nu.stage_critic(b)
 
             def s3():
@@ -224,14 +233,16 @@ class DDPGLearner:
             return self._native.last_metrics()
         return {"qf1_loss": self._lq, "actor_loss": self._la, "qf1_values": self._qv}
 
-    def update_graphed(self, b: Batch, warmup: int = 2, pre=None) -> None:
+    def update_graphed(self, b: Batch, warmup: int = 2, pre=None, topo_ready: bool = False) -> None:
         """Same update, replayed from captured HIP graphs (``b`` must be the same static buffers on
         every call).  One process: one graph for the whole update.  Data parallel: four graphs with
         the gradient all-reduces issued eagerly between them (collectives stay out of capture); the
         critic all-reduce overlaps the actor-forward graph.  The first ``warmup`` calls run eagerly
         (they are real updates) on a side stream.  ``pre`` (e.g. the replay sampler filling ``b``)
-        runs first and is captured with the update."""
+        runs first and is captured with the update; ``topo_ready``: ``pre`` also fills
+        :meth:`topo32_buffer`."""
         inv_world = 1.0 / self.dist.world_size
+        self._topo_ready = bool(topo_ready and pre is not None)
         if self._graphs is None:
             if self._graph_warm < warmup:
                 s = torch.cuda.Stream(self.device)
@@ -371,6 +382,7 @@ class BatchedTrainer:
         self.episode_returns: List[float] = []
         self.graphed = bool(tcfg.cuda_graphs and self.device.type == "cuda")
         self._batch = None
+        self._topo_sink = None
         self.sim_stream = self.learn_stream = None
         self.sim_cus = 0
         if self.device.type == "cuda" and tcfg.overlap_sim:
@@ -517,8 +529,9 @@ class BatchedTrainer:
                 if self._batch is None:
                     self._batch = self.replay.empty_batch(self.batch_size)
                     B, out = self.batch_size, self._batch
-                    self._sampler = lambda: self.replay.sample(B, out=out)
-                self.learner.update_graphed(self._batch, pre=self._sampler)
+                    sink = self._topo_sink = self.learner.topo32_buffer(B)
+                    self._sampler = lambda: self.replay.sample(B, out=out, topo32=sink)
+                self.learner.update_graphed(self._batch, pre=self._sampler, topo_ready=self._topo_sink is not None)
             else:
                 self.learner.update(self.replay.sample(self.batch_size))
 

@@ -75,33 +75,33 @@ class DeviceReplay:
         topo = topo.to(torch.int64).contiguous()
         rewards = rewards.contiguous().float()
         ob = obs[0].numel() * 4
-        nat.replay_insert(dev, st, obs.data_ptr(), self.obs.data_ptr(), E, ob, cap, 0, s)
-        nat.replay_insert(dev, st, next_obs.data_ptr(), self.next_obs.data_ptr(), E, ob, cap, 0, s)
-        nat.replay_insert(dev, st, topo.data_ptr(), self.topo.data_ptr(), E, 8, cap, 0, s)
-        nat.replay_insert(dev, st, rewards.data_ptr(), self.rewards.data_ptr(), E, 4, cap, 0, s)
+        cols = [(obs.data_ptr(), self.obs.data_ptr(), ob, 0), (next_obs.data_ptr(), self.next_obs.data_ptr(), ob, 0),
+                (topo.data_ptr(), self.topo.data_ptr(), 8, 0), (rewards.data_ptr(), self.rewards.data_ptr(), 4, 0)]
         A = self.actions.shape[1]
         if self.actions.dtype == torch.bfloat16 and actions.dtype == torch.float32:
             a = actions.contiguous()
-            nat.replay_insert(dev, st, a.data_ptr(), self.actions.data_ptr(), E, A, cap, 1, s)
+            cols.append((a.data_ptr(), self.actions.data_ptr(), A, 1))
         else:
             a = actions.to(self.actions.dtype).contiguous()
-            nat.replay_insert(dev, st, a.data_ptr(), self.actions.data_ptr(), E, A * a.element_size(), cap, 0, s)
+            cols.append((a.data_ptr(), self.actions.data_ptr(), A * a.element_size(), 0))
         if dones.dtype in (torch.uint8, torch.bool):
             d = dones.contiguous().view(torch.uint8)
-            nat.replay_insert(dev, st, d.data_ptr(), self.dones.data_ptr(), E, 1, cap, 2, s)
+            cols.append((d.data_ptr(), self.dones.data_ptr(), 1, 2))
         else:
             d = dones.contiguous().float()
-            nat.replay_insert(dev, st, d.data_ptr(), self.dones.data_ptr(), E, 4, cap, 0, s)
-        nat.replay_advance(dev, st, E, cap, s)
+            cols.append((d.data_ptr(), self.dones.data_ptr(), 4, 0))
+        # every column in one kernel, then the cursor advance (csrc/ops/replay.hip insert_cols_kernel)
+        nat.replay_insert_cols(dev, st, E, cap, cols, s)
         new = self.pos + E
         if new >= self.capacity:
             self.full = True
         self.pos = new % self.capacity
 
     @torch.no_grad()
-    def sample(self, batch_size: int, out: Optional[Batch] = None) -> Batch:
+    def sample(self, batch_size: int, out: Optional[Batch] = None, topo32: Optional[torch.Tensor] = None) -> Batch:
         """Uniform sample (reference buffer.py:56-62); with ``out`` the rows are gathered into those
-        (static) buffers -- graph-capturable."""
+        (static) buffers -- graph-capturable.  ``topo32`` (int32 [B]) also receives the sampled
+        topology ids (the native learner's kernels take int32)."""
         if len(self) == 0:
             raise RuntimeError("cannot sample from an empty replay buffer")
         B = int(batch_size)
@@ -111,10 +111,15 @@ class DeviceReplay:
         if out is None:
             out = self.empty_batch(B)
         nat, s, dev = self.nat, self._stream(), self.is_dev
-        nat.replay_sample_indices(dev, self.state.data_ptr(), self.seed, B, self.capacity, idx.data_ptr(), s)
+        cols = []
         for src, dst in zip((self.obs, self.topo, self.actions, self.rewards, self.next_obs, self.dones), out):
             assert dst.is_contiguous() and dst.shape[0] == B and dst.dtype == src.dtype
-            nat.replay_gather(dev, src.data_ptr(), dst.data_ptr(), idx.data_ptr(), B, src[0].numel() * src.element_size(), s)
+            cols.append((src.data_ptr(), dst.data_ptr(), src[0].numel() * src.element_size(), 0))
+        if topo32 is not None:
+            assert topo32.dtype == torch.int32 and topo32.is_contiguous() and topo32.numel() == B
+            cols.append((self.topo.data_ptr(), topo32.data_ptr(), 8, 3))
+        # Philox indices, then every column in one gather kernel (csrc/ops/replay.hip gather_cols_kernel)
+        nat.replay_sample_cols(dev, self.state.data_ptr(), self.seed, B, self.capacity, idx.data_ptr(), cols, s)
         return out
 
     def last_indices(self, batch_size: int) -> torch.Tensor:

@@ -19,8 +19,11 @@ def test_device_replay_matches_host():
         for r in rs:
             d = r.device
             r.add(obs.to(d), topo.to(d), act.to(d), rew.to(d), nxt.to(d), done.to(d))
-        bs = [r.sample(3000) for r in rs]
+        t32 = [torch.zeros(3000, dtype=torch.int32, device=r.device) for r in rs]
+        bs = [r.sample(3000, topo32=t) for r, t in zip(rs, t32)]
         torch.cuda.synchronize()
+        assert torch.equal(t32[1].cpu(), bs[1].topo.cpu().to(torch.int32))
+        assert torch.equal(t32[0], bs[0].topo.to(torch.int32))
         assert torch.equal(rs[0].last_indices(3000), rs[1].last_indices(3000).cpu())
         for a, b in zip(*bs):
             assert torch.equal(a, b.cpu())

@@ -87,3 +87,14 @@ def test_rng_state_roundtrip():
     _fill(q, 2)
     q.set_rng_state(st)
     assert torch.equal(q.sample(10).obs, a)
+
+
+def test_fused_sample_writes_int32_topology_ids():
+    r = DeviceReplay(50, 4, 3, 6, "cpu", seed=3)
+    topo = torch.arange(20) % 5
+    r.add(torch.rand(20, 4, 3), topo, torch.rand(20, 6), torch.rand(20), torch.rand(20, 4, 3),
+          torch.zeros(20, dtype=torch.uint8))
+    t32 = torch.full((64,), -1, dtype=torch.int32)
+    b = r.sample(64, topo32=t32)
+    assert torch.equal(t32, b.topo.to(torch.int32))
+    assert torch.equal(b.topo, topo[r.last_indices(64).long()])
