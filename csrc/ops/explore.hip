@@ -100,6 +100,67 @@ __global__ __launch_bounds__(64) void explore_postprocess_kernel(const float* __
     if (i < P) out[base + i] = (float)w[i];
 }
 
+// Lane-parallel variant for n_pad <= 32 (the common case): 32 lanes per slice (one weight per lane,
+// two slices per wave), fp64 sums by cross-lane reductions and the residual's target element by a
+// ballot -- the serial kernel above is one latency-bound thread per slice.  Same noise stream; the
+// fp64 sums associate differently (results agree to float32 rounding).
+__device__ __forceinline__ double half_sum(double v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void explore_postprocess_lanes_kernel(const float* __restrict__ mu,
+                                                                       const float* __restrict__ mask,
+                                                                       const long long* __restrict__ topo,
+                                                                       float* __restrict__ out, int E, int A, int P,
+                                                                       int warmup, float rand_mu, float rand_sigma,
+                                                                       uint32_t seed, uint32_t step, double thr,
+                                                                       int passes) {
+  const int R = A / P;
+  const long slice = (long)blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
+  const int i = threadIdx.x & 31;
+  if (slice >= (long)E * R) return;  // whole 32-lane halves exit together
+  const long base = slice * P;
+  const bool on = i < P;
+  const float* mrow = topo ? mask + topo[slice / R] * (long)A + (slice % R) * P : mask + base;
+  double w = 0.0;
+  if (on) {
+    const int i0 = i & ~1;
+    const Philox4 r = philox4x32_10(seed, step, (uint64_t)(base + i0));
+    const float u0 = (float)(r.v[0] >> 8) * (1.0f / 16777216.0f);
+    const float u1 = (float)(r.v[1] >> 8) * (1.0f / 16777216.0f);
+    float a;
+    if (warmup) {
+      a = (i & 1 ? u1 : u0) * mrow[i];
+    } else {
+      const float rad = sqrtf(-2.0f * __logf(1.0f - u0));
+      float sn, cs;
+      __sincosf(6.283185307179586f * u1, &sn, &cs);
+      const float sv = 2.0f * mu[base + i] - 1.0f + rand_mu + rand_sigma * (rad * (i & 1 ? sn : cs));
+      a = 0.5f * (sv + 1.0f);
+      a = a < 0.f ? 0.f : (a > 1.f ? 1.f : a);
+    }
+    w = (double)a;
+  }
+  const double acc = 1.4901161193847656e-08;  // sqrt(float64 eps)
+  const unsigned long long half_mask = (threadIdx.x & 32) ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+  const int half_base = threadIdx.x & 32;
+  for (int pass = 0; pass < passes; ++pass) {
+    w = on && w >= thr ? w : 0.0;
+    const double s = half_sum(w);
+    if (s == 0.0) w = on ? round10(1.0 / P) : 0.0;
+    else if (fabs(1.0 - s) > acc && on) w = round10(w / s);
+    const double r = 1.0 - half_sum(w);
+    if (r != 0.0) {
+      // first element that can absorb the residual (the last one otherwise)
+      const unsigned long long b = __ballot(on && (i == P - 1 || w + r >= 0)) & half_mask;
+      if (b != 0 && (__ffsll((long long)b) - 1 - half_base) == i) w += r;
+    }
+  }
+  if (on) out[base + i] = (float)w;
+}
+
 void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t out, int E, int A, int P, int warmup, float rand_mu,
                          float rand_sigma, uint32_t seed, uint32_t step, double thr, int passes, uintptr_t stream) {
   GSC_CHECK(A % P == 0, "action dim must be a multiple of n_pad");
@@ -111,7 +172,12 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t
                        ptr<const float>(mask), ptr<const long long>(topo), ptr<float>(out), E, A, P, warmup, rand_mu, rand_sigma, seed, step,
                        thr, passes);
   };
-  if (P <= 32) go(explore_postprocess_kernel<32>);
+  if (P <= 32) {
+    const int sl_per_block = 8;
+    hipLaunchKernelGGL(explore_postprocess_lanes_kernel, dim3((int)((slices + sl_per_block - 1) / sl_per_block)), dim3(256), 0,
+                       stream_of(stream), ptr<const float>(mu), ptr<const float>(mask), ptr<const long long>(topo),
+                       ptr<float>(out), E, A, P, warmup, rand_mu, rand_sigma, seed, step, thr, passes);
+  } else if (P <= 32) go(explore_postprocess_kernel<32>);
   else if (P <= 64) go(explore_postprocess_kernel<64>);
   else if (P <= 128) go(explore_postprocess_kernel<128>);
   else if (P <= 256) go(explore_postprocess_kernel<256>);

@@ -378,6 +378,7 @@ class NativeAct:
         self.rowtab = torch.zeros(self.T, n.width(0), device=dev)
         self.out = torch.zeros(E, self.A, device=dev)
         self.topo32 = torch.zeros(E, dtype=torch.int32, device=dev)
+        self._topo_ref, self._topo_ver = None, -1
         self.lw = None
         if not gnn_use_fused(L.actor.embedder, L.graphs, self.P, self.Fin):
             from gsc_amd.ops.gnn_lw import LayerwiseGAT
@@ -391,7 +392,11 @@ class NativeAct:
     def __call__(self, obs: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:
         n, s = self.net, torch.cuda.current_stream(self.L.device).cuda_stream
         assert obs.shape[0] == self.E and obs.is_contiguous() and obs.dtype == F32
-        self.topo32.copy_(topo)
+        # topology ids change at episode ends only: convert once per tensor (the reference held
+        # keeps its storage from being reused by another tensor)
+        if topo is not self._topo_ref or topo._version != self._topo_ver:
+            self.topo32.copy_(topo)
+            self._topo_ref, self._topo_ver = topo, topo._version
         if self.lw is not None:
             self.lw.forward(n.fp.flat[:self.ne], obs, self.topo32, self.emb)
         else:
