@@ -107,7 +107,7 @@ def main():
                                   seed=args.seed * 1000 + info.rank)
     tcfg = TrainerConfig(num_envs=args.envs, batch_size=args.batch_size, updates_per_step=args.updates_per_step,
                          learning_starts=1, seed=args.seed + 17 * info.rank, check_every=0,
-                         overlap_sim=not args.no_overlap, sim_cus=args.sim_cus)
+                         overlap_sim=not args.no_overlap, sim_cus=args.sim_cus, lazy_handoff=True)
     trainer = BatchedTrainer(cfg, sim, tcfg, info, network_schedule=list(range(len(networks))),
                              period=pre["period"])
 

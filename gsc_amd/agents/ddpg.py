@@ -328,6 +328,11 @@ class TrainerConfig:
     cuda_graphs: bool = True                # replay the DDPG update from captured HIP graphs (GPU only)
     amp_bf16: Optional[bool] = None         # None: bf16 GEMM operands on the GPU, fp32 on CPU; False: fp32
                                             # autograd learner everywhere (learning checks)
+    lazy_handoff: bool = False              # overlap mode: hand work between the caller's stream and the
+                                            # trainer's streams only at the trainer's read/write points
+                                            # (metrics/flush/state_dict/load_state_dict/reseed), not around every
+                                            # step -- saves two cross-stream event hops per step; the caller must
+                                            # not touch trainer tensors between steps without those (or a device sync)
 
 
 class BatchedTrainer:
@@ -383,6 +388,7 @@ class BatchedTrainer:
         self.graphed = bool(tcfg.cuda_graphs and self.device.type == "cuda")
         self._batch = None
         self._topo_sink = None
+        self._handoff = True
         self.sim_stream = self.learn_stream = None
         self.sim_cus = 0
         if self.device.type == "cuda" and tcfg.overlap_sim:
@@ -458,8 +464,15 @@ class BatchedTrainer:
             p, self._pending = self._pending, None
             self._record(*p)
 
+    def _join(self) -> None:
+        """Caller's stream waits for the trainer's streams; the next step re-syncs in the other direction."""
+        if self.learn_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.learn_stream)
+            self._handoff = True
+
     def flush(self) -> None:
         """Complete the deferred replay insert / metrics of the last step (before reading them)."""
+        self._join()
         if self._pending is not None:
             if self.learn_stream is not None:
                 self.learn_stream.wait_stream(torch.cuda.current_stream(self.device))
@@ -471,10 +484,14 @@ class BatchedTrainer:
 
     def step(self) -> None:
         if self.learn_stream is not None:
-            self.learn_stream.wait_stream(torch.cuda.current_stream(self.device))
+            cur = torch.cuda.current_stream(self.device)
+            if self._handoff or not self.t.lazy_handoff:
+                self.learn_stream.wait_stream(cur)
+                self._handoff = False
             with torch.cuda.stream(self.learn_stream):
                 self._step()
-            torch.cuda.current_stream(self.device).wait_stream(self.learn_stream)
+            if not self.t.lazy_handoff:
+                cur.wait_stream(self.learn_stream)
         else:
             self._step()
 
@@ -564,6 +581,7 @@ class BatchedTrainer:
         return sd
 
     def load_state_dict(self, sd: dict) -> None:
+        self._join()
         self.learner.load_state_dict(sd["learner"])
         self.global_step = int(sd["global_step"])
         self.episode = int(sd["episode"])
@@ -582,6 +600,7 @@ class BatchedTrainer:
     def reseed(self, seed: int) -> None:
         """Fresh rank-local randomness (resume of a checkpoint without this rank's state): new
         simulator Philox keys (all envs restart their episode) and a new replay sampler stream."""
+        self._join()
         g = np.random.default_rng(seed)
         self.sim.seeds.copy_(torch.from_numpy(g.integers(1, 2**31 - 1, size=self.E).astype(np.uint32)
                                               .view(np.int32)).to(self.device))
