@@ -101,6 +101,7 @@ class SimpleDDPG(RLSPAgent):
                                                device=self.device, seed=seed * 1000 + self.dist.rank,
                                                same_seed_every_episode=overrides.pop("same_seed_every_episode",
                                                                                      False))
+            overrides.setdefault("lazy_handoff", True)   # joins at metrics / checkpoints / after training
             tcfg = TrainerConfig(num_envs=self.num_envs, seed=seed + 17 * self.dist.rank, **overrides)
             self.trainer = BatchedTrainer(self.cfg, self.sim, tcfg, self.dist,
                                           network_schedule=list(range(len(self.train_files))), period=self.period)
@@ -245,6 +246,7 @@ class SimpleDDPG(RLSPAgent):
                 info = {"charts/success_ratio": m["success_ratio"], "charts/episodes_finished": m["episodes"]}
                 info.update({f"losses/{k}": m[k] for k in ("qf1_loss", "actor_loss", "qf1_values") if k in m})
                 self._episode_end(m["mean_episode_return"], info)
+        tr.flush()   # the caller's stream waits for the trainer's streams before anything reads their results
         self.sim.check_flags()
         return {"steps": self.global_step - start, "episodes": self.episode, "best_return": self.best_return}
 
@@ -279,6 +281,8 @@ class SimpleDDPG(RLSPAgent):
         d = torch.load(path, map_location="cpu", weights_only=True)
         if d.get("format") != ckpt.ACTOR_FORMAT:
             raise ValueError(f"{path}: not an actor file")
+        if self.backend == "batched":
+            self.trainer.flush()  # in-flight steps finish before the weights change; the next step re-syncs
         self.actor.load_state_dict(d["state_dict"])
         self.learner.target_actor.load_state_dict(d["state_dict"])
         self.learner.refresh_shadows()
