@@ -48,6 +48,7 @@ struct SimArgs {
   unsigned long long* prof;  // optional [E, 4] cycle counters: select, dispatch, merge, events (diagnostic)
   int prio;                  // wave priority of the step kernel (s_setprio), see sim_step_kernel
   unsigned long long* prof_types;  // optional [E, 64, 2] dispatch cycles / count per (process type, state)
+  int32_t* topo_cur;         // optional [E]: topology each env runs now (updated where an env was reset)
 };
 
 GSC_HD void step_epilogue(Env& S, const SimArgs& a, const SimConst& K, int env) {
@@ -64,6 +65,7 @@ GSC_HD void step_epilogue(Env& S, const SimArgs& a, const SimConst& K, int env) 
     a.done[env] = 1;
     a.ep_return[env] = (float)S.h->episode_return;
     const int topo = a.topo_next[env];
+    if (a.topo_cur) a.topo_cur[env] = topo;
     const int ep = S.h->episode + 1;
     env_init(S, K, a.topos[topo], topo, a.seeds[env], ep);
     write_obs(S, K, a.topos[topo], a.obs + env * ostride);
@@ -411,6 +413,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     __syncthreads();
     {  // every lane (wave-uniform header copies), init loops spread over the lanes
       const int topo = a.topo_next[env];
+      if (a.topo_cur && lane == 0) a.topo_cur[env] = topo;
       env_init(S, K, a.topos[topo], topo, a.seeds[env], S.h->episode + 1, lane, 64);
     }
     __syncthreads();
@@ -581,9 +584,10 @@ class SimContext {
 
   void step(uintptr_t states, uintptr_t topo_next, uintptr_t seeds, uintptr_t actions, long action_stride,
             uintptr_t obs, uintptr_t next_obs, uintptr_t reward, uintptr_t done, uintptr_t stats,
-            uintptr_t ep_return, int E, uintptr_t stream, uintptr_t prof) {
+            uintptr_t ep_return, int E, uintptr_t stream, uintptr_t prof, uintptr_t topo_cur) {
     SimArgs a = args(states, topo_next, seeds, actions, action_stride, obs, next_obs, reward, done, stats,
                      ep_return, E);
+    a.topo_cur = ptr<int32_t>(topo_cur);
     a.prof = ptr<unsigned long long>(prof);
     a.prof_types = prof ? ptr<unsigned long long>(prof) + (long)E * 4 : nullptr;
     static const int prio = getenv("GSC_SIM_PRIO") ? atoi(getenv("GSC_SIM_PRIO")) : 3;
@@ -722,7 +726,8 @@ void register_sim(py::module_& m) {
       .def("reset", &SimContext::reset)
       .def("step", &SimContext::step, py::arg("states"), py::arg("topo_next"), py::arg("seeds"), py::arg("actions"),
            py::arg("action_stride"), py::arg("obs"), py::arg("next_obs"), py::arg("reward"), py::arg("done"),
-           py::arg("stats"), py::arg("ep_return"), py::arg("E"), py::arg("stream"), py::arg("prof") = 0);
+           py::arg("stats"), py::arg("ep_return"), py::arg("E"), py::arg("stream"), py::arg("prof") = 0,
+           py::arg("topo_cur") = 0);
   m.attr("SIM_NUM_STATS") = kNumStats;
   m.attr("SIM_HEADER_BYTES") = (int)sizeof(Header);
 }

@@ -370,11 +370,12 @@ class BatchedTrainer:
         self.schedule = list(network_schedule) if network_schedule else [0]
         self.period = int(period) if period else 0
         self.sim.set_topologies(self.schedule[0])
-        # acting observations and actions are double-buffered by step parity: with the simulator
-        # overlapped, step t's replay insert runs after step t+1's simulator launch (off the
-        # sim -> act -> sim critical path) and still reads step t's buffers
-        self._obs_bufs = [self.sim.reset().clone(), None]
-        self._obs_bufs[1] = torch.empty_like(self._obs_bufs[0])
+        # acting actions are double-buffered by step parity and observations triple-buffered: with the
+        # simulator overlapped, step t's replay insert runs after step t+1's simulator launch (off the
+        # sim -> act -> sim critical path) and still reads step t's buffers, while the simulator writes
+        # the observations of step t+2 straight into the third buffer (no copy on the critical path)
+        first = self.sim.reset().clone()
+        self._obs_bufs = [first, torch.empty_like(first), torch.empty_like(first)]
         self.topo = self.sim.topo_cur.to(torch.int64).clone()
         self.masks = self.learner.masks
         self._act_bufs = [torch.empty(self.E, sim.action_dim, device=self.device) for _ in range(2)]
@@ -443,7 +444,7 @@ class BatchedTrainer:
     @property
     def obs(self) -> torch.Tensor:
         """Observation the next step acts on."""
-        return self._obs_bufs[self.global_step & 1]
+        return self._obs_bufs[self.global_step % 3]
 
     @property
     def act_buf(self) -> torch.Tensor:
@@ -498,7 +499,8 @@ class BatchedTrainer:
     def _step(self) -> None:
         warm = self.global_step < self.learning_starts
         k = self.global_step & 1
-        obs, topo = self._obs_bufs[k], self.topo
+        obs, topo = self._obs_bufs[self.global_step % 3], self.topo
+        obs_next = self._obs_bufs[(self.global_step + 1) % 3]
         with trace_range("act"):
             mu = self.learner.act(obs, topo)
         with trace_range("explore"):
@@ -513,7 +515,7 @@ class BatchedTrainer:
             main = torch.cuda.current_stream(self.device)
             self.sim_stream.wait_stream(main)
             with torch.cuda.stream(self.sim_stream):
-                out = self.sim.step(act, buffer_set=k)
+                out = self.sim.step(act, buffer_set=k, obs_out=obs_next)
             self._flush_pending()
             with trace_range("learn"):
                 self._learn()
@@ -522,12 +524,11 @@ class BatchedTrainer:
         else:
             self._flush_pending()
             with trace_range("sim"):
-                out = self.sim.step(act, buffer_set=k)
+                out = self.sim.step(act, buffer_set=k, obs_out=obs_next)
             self._record(obs, topo, act, out)
             if train:
                 with trace_range("learn"):
                     self._learn()
-        self._obs_bufs[k ^ 1].copy_(out.obs)
         episode_end = (self.global_step + 1) % self.sim.episode_steps == 0
         if episode_end:
             self.episode += 1
@@ -605,5 +606,5 @@ class BatchedTrainer:
         self.sim.seeds.copy_(torch.from_numpy(g.integers(1, 2**31 - 1, size=self.E).astype(np.uint32)
                                               .view(np.int32)).to(self.device))
         self.sim.set_topologies(self.topo.to(torch.int32))
-        self._obs_bufs[self.global_step & 1].copy_(self.sim.reset())
+        self._obs_bufs[self.global_step % 3].copy_(self.sim.reset())
         self.replay.reseed(int(seed) * 7919 + self.global_step)

@@ -237,19 +237,25 @@ class BatchedSimulator:
         then [E, 64, 2] handler cycles / dispatches per (process type, resume state)."""
         self.prof = torch.zeros(self.E * 4 + self.E * 128, dtype=torch.int64, device=self.device) if on else None
 
-    def step(self, actions: torch.Tensor, buffer_set: int = 0) -> SimStepOut:
+    def step(self, actions: torch.Tensor, buffer_set: int = 0, obs_out: Optional[torch.Tensor] = None) -> SimStepOut:
+        """One lockstep step of every env.  ``obs_out``: write the next action's observations there
+        instead of the buffer set's own ``obs`` (the trainer's rotating observation buffers)."""
         if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
             actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
         if actions.dim() != 2 or actions.shape[0] != self.E or actions.shape[1] < self.action_dim:
             raise ValueError(f"actions must be [E={self.E}, >= {self.action_dim}], got {tuple(actions.shape)}")
         obs, next_obs, reward, done_u8, stats, ep_return = self._out_sets[buffer_set]
+        if obs_out is not None:
+            assert obs_out.shape == obs.shape and obs_out.dtype == obs.dtype and obs_out.is_contiguous()
+            assert obs_out.device == self.device
+            obs = obs_out
+        # envs that finish are reset onto their scheduled topology: the kernel updates topo_cur there
         self.ctx.step(self.states.data_ptr(), self.topo_next.data_ptr(), self.seeds.data_ptr(), actions.data_ptr(),
                       actions.shape[1], obs.data_ptr(), next_obs.data_ptr(), reward.data_ptr(),
                       done_u8.data_ptr(), stats.data_ptr(), ep_return.data_ptr(), self.E, self._stream(),
-                      self.prof.data_ptr() if (self.prof is not None and self.is_device) else 0)
+                      self.prof.data_ptr() if (self.prof is not None and self.is_device) else 0,
+                      self.topo_cur.data_ptr())
         done = done_u8.view(torch.bool)  # 0/1 bytes: zero-copy
-        # envs that finished were reset onto their scheduled topology
-        torch.where(done, self.topo_next, self.topo_cur, out=self.topo_cur)
         return SimStepOut(obs, next_obs, reward, done, stats, ep_return)
 
     def check_flags(self) -> int:

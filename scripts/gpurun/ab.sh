@@ -4,7 +4,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest $R/tests/test_gpu_ops.py $R/tests/test_gpu_learner.py $R/tests/test_gpu_replay.py $R/tests/test_gpu_graphs.py -x -q --timeout 200 --timeout-method thread > $OUT/ab_tests.log 2>&1 &&
+timeout -k 10 300 python -u -m pytest $R/tests/test_gpu_ops.py $R/tests/test_gpu_learner.py $R/tests/test_gpu_replay.py $R/tests/test_gpu_graphs.py $R/tests/test_gpu_sim.py -x -q --timeout 200 --timeout-method thread > $OUT/ab_tests.log 2>&1 &&
 : > $OUT/ab.txt &&
 timeout -k 10 120 python $R/scripts/gnn_bench.py >> $OUT/ab.txt 2>&1 &&
 for i in 1 2 3; do
