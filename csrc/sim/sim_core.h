@@ -912,6 +912,47 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
 // The schedule table S.sched must already hold this step's action.
 GSC_HD_CALL void controller_prologue(Env& S, const SimConst& K, const TopoDev& T) {
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // lane-parallel over destination nodes: the frontier walk reads each source row with one load per
+  // lane, and the next frontier is the ballot of positive weights (== the serial loops below)
+  {
+    const int lane = wave_lane();
+    for (int i = lane; i < N * Sd; i += 64) S.placement[i] = 0;
+    lanes_sync(64);
+    for (int c = 0; c < K.C; ++c) {
+      uint64_t f[4] = {0, 0, 0, 0};  // node bitset (n <= 256)
+      for (int i = 0; i < T.n_ing; ++i) {
+        const int v = GSC_UNI(T.ingress[i]);
+        if (GSC_UNI(S.inter_arr[v] == S.inter_arr[v])) f[v >> 6] |= 1ull << (v & 63);
+      }
+      for (int k = 0; k < K.chain_len[c]; ++k) {
+        const int sf = K.chain[c * kMaxF + k];
+        uint64_t nf[4] = {0, 0, 0, 0};
+        for (int src = 0; src < n; ++src) {
+          if (!((f[src >> 6] >> (src & 63)) & 1)) continue;
+          const double* row = S.sched + ((src * C + c) * Sd + sf) * N;
+          for (int d0 = 0; d0 < n; d0 += 64) {
+            const int dst = d0 + lane;
+            const bool pos = dst < n && row[dst] > 0;
+            if (pos) S.placement[dst * Sd + sf] = 1;
+            nf[d0 >> 6] |= (uint64_t)__ballot(pos);
+          }
+        }
+        for (int j = 0; j < 4; ++j) f[j] = nf[j];
+      }
+    }
+    lanes_sync(64);
+    // available_sf rebuild: keep SFs that still carry load, (re)create placed ones
+    const double now = S.h->now;
+    for (int i = lane; i < n * Sd; i += 64) {
+      if (S.sf_present[i] && S.sf_load[i] != 0.0) continue;
+      if (S.placement[i]) { S.sf_present[i] = 1; S.sf_load[i] = 0.0; S.sf_start[i] = now; }
+      else S.sf_present[i] = 0;
+    }
+    lanes_sync(64);
+    return;
+  }
+#endif
   for (int i = 0; i < N * Sd; ++i) S.placement[i] = 0;
   // follow positive weights from every active ingress along each chain (add_placement_recursive)
   for (int c = 0; c < K.C; ++c) {

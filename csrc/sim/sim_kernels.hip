@@ -153,7 +153,21 @@ __device__ __forceinline__ TopoDev stage_topo(const TopoDev& g, char* dst, int l
   auto put = [&](const void* src, int bytes) -> char* {
     char* d = p;
     const int w = bytes >> 1;  // 16-bit granules (every table is 2- or 8-byte typed)
-    for (int i = lane; i < w; i += 64) reinterpret_cast<int16_t*>(d)[i] = reinterpret_cast<const int16_t*>(src)[i];
+    const int16_t* s16 = reinterpret_cast<const int16_t*>(src);
+    int16_t* d16 = reinterpret_cast<int16_t*>(d);
+    for (int i0 = 0; i0 < w; i0 += 64 * 8) {  // 8 loads in flight per lane (one HBM/L2 latency per 512 granules)
+      int16_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + 64 * j + lane;
+        v[j] = i < w ? s16[i] : (int16_t)0;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + 64 * j + lane;
+        if (i < w) d16[i] = v[j];
+      }
+    }
     p += align16(bytes);
     return d;
   };
@@ -279,6 +293,7 @@ struct BucketLayout {
 template <class B, int QS, bool PROF>
 __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst& K, char* base, char* topo_lds,
                                                 int env, int lane) {
+  const unsigned long long t_entry = PROF ? __builtin_amdgcn_s_memtime() : 0;
   Env S = [&] {
     if constexpr (std::is_same<B, DynLayout>::value) return Env(base, a.L, a.D);
     else return Env(base, BucketLayout<B>::L, BucketLayout<B>::D);
@@ -371,12 +386,15 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
       n_ev += __builtin_amdgcn_readfirstlane(n_disp);
     }
   }
+  const unsigned long long t_loop_end = prof ? __builtin_amdgcn_s_memtime() : 0;
   if (prof && lane == 0) {
     unsigned long long* pr = a.prof + (long)env * 4;
     pr[0] += t_sel;
     pr[1] += t_hdl;
     pr[2] += t_mrg;
     pr[3] += n_ev;
+    a.prof_types[((long)env * 64 + 62) * 2] += t_begin - t_entry;  // prologue (topology stage, action, inbox)
+    a.prof_types[((long)env * 64 + 62) * 2 + 1] += 1;
   }
   __syncthreads();
   // write the queue back (sorted) as the persistent pending-event array
@@ -421,6 +439,10 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   }
   if (lane == 0) *h_mem = h_reg;
   __syncthreads();
+  if (PROF && lane == 0) {  // epilogue (queue write-back, reward, stats, observations, resets)
+    a.prof_types[((long)env * 64 + 63) * 2] += __builtin_amdgcn_s_memtime() - t_loop_end;
+    a.prof_types[((long)env * 64 + 63) * 2 + 1] += 1;
+  }
 }
 
 template <int QSETS, bool LDS_STATE, bool PROF = false, class B = DynLayout>
@@ -445,10 +467,19 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   char* topo_lds = smem + sb + const_stage_bytes();
   char* g = a.states + (long)env * a.state_bytes;
   if constexpr (LDS_STATE) {
+    const unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
     copy16(smem, g, sbytes, lane);
     __syncthreads();
+    const unsigned long long t1 = PROF ? __builtin_amdgcn_s_memtime() : 0;
     device_step_env<B, QSETS, PROF>(a, *Ks, smem, topo_lds, env, lane);
+    const unsigned long long t2 = PROF ? __builtin_amdgcn_s_memtime() : 0;
     copy16(g, smem, sbytes, lane);
+    if (PROF && lane == 0) {  // state blob HBM -> LDS / LDS -> HBM
+      a.prof_types[((long)env * 64 + 60) * 2] += t1 - t0;
+      a.prof_types[((long)env * 64 + 60) * 2 + 1] += 1;
+      a.prof_types[((long)env * 64 + 61) * 2] += __builtin_amdgcn_s_memtime() - t2;
+      a.prof_types[((long)env * 64 + 61) * 2 + 1] += 1;
+    }
   } else {
     __syncthreads();
     device_step_env<B, QSETS, false>(a, *Ks, g, topo_lds, env, lane);
