@@ -146,9 +146,10 @@ class NativeDDPGUpdate:
             from gsc_amd.ops.gnn_lw import LayerwiseGAT
             self.lwo = {k: LayerwiseGAT(self.tables, B, self.P, Fin, H, self.layer_of, dev) for k in ("a", "c", "-")}
             self.blob = {"a": None, "c": None}
-        elif os.environ.get("GSC_GNN_SAVE", "0") == "0":
-            # the backward recomputes the forward (measured on MI355X, 256 Abilene envs: 88.2k vs 86.7k
-            # env-steps/s with the forward saving its per-layer images for the backward)
+        elif os.environ.get("GSC_GNN_SAVE", "1") == "0":
+            # GSC_GNN_SAVE=0: the backward recomputes the forward in LDS.  Default: the forward saves its
+            # per-layer images for the backward (measured on MI355X, 256 Abilene envs, after the backward
+            # stopped spilling: 101.9k vs 101.2k env-steps/s; recompute had won before, 88.2k vs 86.7k)
             self.blob = {"a": None, "c": None}
         else:
             sb = nat.gnn_saved_bytes(self.tables, self.P, Fin, H, self.layer_of)
