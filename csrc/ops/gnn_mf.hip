@@ -625,9 +625,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     mf_load_topo(T, a, a.topo[g], lane);
     const int n = T.n;
     if (LOADED) {
-      // the forward saved every conv's input images and alpha: one bulk copy instead of a recompute
-      const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.blob) + (long)g * m.blob);
-      for (int i = lane; i < m.blob / 16; i += 64) reinterpret_cast<uint4*>(W)[i] = src[i];
+      // the forward saved every conv's input images and alpha: one bulk copy instead of a recompute,
+      // as direct global -> LDS loads (1 KiB per wave instruction, all in flight together, no VGPRs)
+      const char* src = reinterpret_cast<const char*>(a.blob) + (long)g * m.blob;
+      for (int o = 0; o < m.blob; o += 1024)
+        if (o + 16 * lane < m.blob)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + o + 16 * lane),
+                                           (__attribute__((address_space(3))) void*)(W + o), 16, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       cl_wave_sync();
     } else {
       mf_load_x<true>(a, g, n, reinterpret_cast<__bf16*>(W + m.hR[0]), reinterpret_cast<__bf16*>(W + m.hT[0]), E, NV,
