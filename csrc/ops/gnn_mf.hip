@@ -829,7 +829,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-static MfLayout mf_layout(const ClArgs& a, bool bwd, int HPF) {
+// kind 0: forward; 1: forward that saves its per-layer images (the blob region, laid out exactly as
+// the backward's, then the forward's scratch -- none of the backward's buffers, so more waves fit);
+// 2: backward
+enum { kMfLayFwd = 0, kMfLaySave = 1, kMfLayBwd = 2 };
+static MfLayout mf_layout(const ClArgs& a, int kind, int HPF) {
+  const bool bwd = kind == kMfLayBwd, blob = kind != kMfLayFwd;
   MfLayout m{};
   m.NV = a.NM <= 16 ? 16 : 32;
   m.NVS = m.NV + 4;  // [k][node] rows: NV + 4 bf16 keeps b64 row reads / writes of 16-32 rows conflict-free
@@ -844,17 +849,19 @@ static MfLayout mf_layout(const ClArgs& a, bool bwd, int HPF) {
   m.hTrows = HPF;
   const int hRb = m.NV * kMfRS * 2, M4b = ((a.M + 3) & ~3) * 4, fb = a.NM * mf_xs(HPF) * 4;
   const int Nb = ((a.NM + 3) & ~3) * 4;
-  if (bwd) {
+  if (blob) {
     for (int l = 0; l < a.L; ++l) {
       m.hR[l] = take(hRb);
       m.hT[l] = take((l == 0 ? m.hTrows0 : m.hTrows) * m.NVS * 2);
       m.al[l] = take(M4b);
     }
     m.blob = o;
-    m.dy = take(fb);
-    const int gt = HPF * m.MS * 2, dx = 2 * hRb;
-    m.U = take(gt > dx ? gt : dx);
-    m.da = take(M4b);
+    if (bwd) {
+      m.dy = take(fb);
+      const int gt = HPF * m.MS * 2, dx = 2 * hRb;
+      m.U = take(gt > dx ? gt : dx);
+      m.da = take(M4b);
+    }
   } else {
     m.hR[0] = take(hRb);
     m.hR[1] = take(hRb);
@@ -885,7 +892,7 @@ bool gnn_mf_supported(int Fin, int H, int NM, int L, int n_blocks, const int* la
 template <int HPF, bool K2>
 static void mf_launch_fwd(ClArgs a, hipStream_t st, int cus) {
   const bool save = a.blob != nullptr;
-  const MfLayout m = mf_layout(a, save, HPF);
+  const MfLayout m = mf_layout(a, save ? kMfLaySave : kMfLayFwd, HPF);
   a.waves = 4;
   const size_t lds = sizeof(float) * (mf_vec_floats(a.n_blocks) + 2 * kMfFragSet) + (size_t)a.waves * m.per_wave;
   GSC_CHECK(lds <= 160 * 1024, "GNN (MFMA) forward working set exceeds LDS");
@@ -908,7 +915,7 @@ static int mf_launch_bwd(ClArgs a, hipStream_t st, int cus, int max_rows) {
   static const int wpe = getenv("GSC_GNN_BWD_WPE") ? atoi(getenv("GSC_GNN_BWD_WPE")) : 2;  // measured: 336 vs 469 us (WPE 1)
   GSC_CHECK(a.s_dst != nullptr && a.s_src != nullptr && a.MP >= a.M && a.MP % 16 == 0,
             "MFMA GNN backward needs the one-hot message matrices (GraphSet.s_dst / s_src)");
-  const MfLayout m = mf_layout(a, true, HPF);
+  const MfLayout m = mf_layout(a, kMfLayBwd, HPF);
   a.waves = 4;
   size_t lds = 0;
   for (;;) {
@@ -950,7 +957,7 @@ void gnn_mf_forward(const void* args_generic, uintptr_t stream, int cus) {
 
 int gnn_mf_saved_bytes(const void* args_generic) {
   const ClArgs& a = *reinterpret_cast<const ClArgs*>(args_generic);
-  return mf_layout(a, true, a.H <= 24 ? 24 : 32).blob;
+  return mf_layout(a, kMfLayBwd, a.H <= 24 ? 24 : 32).blob;
 }
 
 int gnn_mf_backward(const void* args_generic, uintptr_t stream, int cus, int max_rows) {
