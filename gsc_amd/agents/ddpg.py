@@ -403,11 +403,11 @@ class BatchedTrainer:
                 self.sim_cus = k
                 self.sim_stream = torch.cuda.ExternalStream(nat.create_cu_masked_stream(list(range(k))),
                                                             device=self.device)
-                # The learner stream stays unmasked: while the simulator runs, its CUs' LDS is full so
-                # learner blocks land on the other CUs anyway, and once the sim step ends the learner
-                # also fills the freed CUs (57.2k vs 52.4k env-steps/s with a masked learner stream).
-                # GSC_LEARNER_MASK=1 restricts the learner to the complement.
-                if os.environ.get("GSC_LEARNER_MASK", "0") == "0":
+                # The learner stream is restricted to the complement, so no learner wave shares a SIMD
+                # with a simulator wave (the simulator is the critical path and the learner has slack:
+                # 103.6k vs 102.3k env-steps/s unmasked, 256 Abilene envs; when the learner was the longer
+                # chain the unmasked stream won, 57.2k vs 52.4k).  GSC_LEARNER_MASK=0 leaves it unmasked.
+                if os.environ.get("GSC_LEARNER_MASK", "1") == "0":
                     self.learn_stream = torch.cuda.Stream(self.device)
                 else:
                     self.learn_stream = torch.cuda.ExternalStream(
