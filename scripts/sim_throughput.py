@@ -22,6 +22,7 @@ ap.add_argument("--device", default="cuda")
 ap.add_argument("--net", default="configs/networks/abilene/abilene-in4-rand-cap1-2.graphml")
 ap.add_argument("--profile", action="store_true")
 ap.add_argument("--simcfg", default="configs/config/simulator/sample_config.yaml")
+ap.add_argument("--cus", type=int, default=0, help="run on a stream CU-masked to this many CUs (0: all)")
 args = ap.parse_args()
 cfg = yaml.safe_load(open("configs/config/agent/sample_agent.yaml"))
 sim = load_batched_from_paths([args.net], "configs/service_functions/abc.yaml", args.simcfg, cfg, args.envs,
@@ -32,6 +33,9 @@ a = np.zeros((24, 1, 3, 24))
 a[:n, :, :, :n] = rng.random((n, 1, 3, n))
 a = threshold_normalize(a.reshape(-1), 24, 0.1, 2).astype(np.float32)
 A = torch.from_numpy(np.tile(a, (args.envs, 1))).to(args.device)
+if args.cus:
+    stream = torch.cuda.ExternalStream(sim.native.create_cu_masked_stream(list(range(args.cus))))
+    torch.cuda.set_stream(stream)
 sim.reset()
 for _ in range(5):
     sim.step(A)
@@ -47,7 +51,7 @@ if args.device == "cuda":
     torch.cuda.synchronize()
 dt = time.perf_counter() - t
 sim.check_flags()
-print(f"envs={args.envs} steps={args.steps} state_bytes={sim.state_bytes} lds={sim.ctx.use_lds} "
+print(f"cus={args.cus or 'all'} envs={args.envs} steps={args.steps} state_bytes={sim.state_bytes} lds={sim.ctx.use_lds} "
       f"env_steps_per_s={args.envs * args.steps / dt:.1f} ms_per_step={dt / args.steps * 1e3:.3f}")
 if args.profile:
     pr = sim.prof.double().cpu()
