@@ -247,7 +247,7 @@ class BatchedSimulator:
         obs, next_obs, reward, done_u8, stats, ep_return = self._out_sets[buffer_set]
         if obs_out is not None:
             assert obs_out.shape == obs.shape and obs_out.dtype == obs.dtype and obs_out.is_contiguous()
-            assert obs_out.device == self.device
+            assert obs_out.device.type == self.device.type
             obs = obs_out
         # envs that finish are reset onto their scheduled topology: the kernel updates topo_cur there
         self.ctx.step(self.states.data_ptr(), self.topo_next.data_ptr(), self.seeds.data_ptr(), actions.data_ptr(),
