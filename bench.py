@@ -119,6 +119,11 @@ def main():
         trainer.step()
     sync()
     trainer.metrics(reset=True)
+    # diagnostics only (GSC_SIM_PROFILE=1, never for reported numbers): the simulator runs its cycle-counting
+    # variant and the effective engine clock while it runs beside the learner is printed to stderr
+    diag = os.environ.get("GSC_SIM_PROFILE") == "1" and device.type == "cuda"
+    if diag:
+        sim.enable_profiling()
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -129,6 +134,10 @@ def main():
     dt = time.perf_counter() - t0
     sim.check_flags()
     m = trainer.metrics(reset=True)
+    if diag:
+        ty = sim.prof[sim.E * 4:].view(sim.E, 64, 2).sum(0).double().cpu()
+        print(f"diag: sim cycles/env-step={ty[58, 0] / max(float(ty[58, 1]), 1):.0f} "
+              f"effective engine clock {ty[58, 0] / max(float(ty[59, 0]), 1) * 100:.0f} MHz", file=sys.stderr)
 
     if args.check_replicas and info.enabled:
         import torch.distributed as dist

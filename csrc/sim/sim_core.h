@@ -93,6 +93,7 @@ struct TopoDev {
   const double* pdelay;     // [n*n]
   const int16_t* plen;      // [n*n]
   const int16_t* pnodes;    // [n*n*H]
+  const int16_t* pedges;    // [n*n*H] edge id of each path hop (from the previous path node)
   const int16_t* edge_id;   // [n*n]
   const double* edge_cap;   // [E]
   const int16_t* ingress;   // [n_ing]
@@ -266,6 +267,9 @@ __device__ __forceinline__ uint32_t dpp_red_u32(uint32_t v, uint32_t ident, OP o
 __device__ __forceinline__ int wave_sum_i32(int v) {
   return (int)dpp_red_u32((uint32_t)v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
 }
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
 // max of a double over the wave (exact), broadcast to every lane
 __device__ __forceinline__ double wave_max_f64(double v) {
   const int ilo = 0, ihi = (int)0xFFF00000u;  // -inf
@@ -292,11 +296,12 @@ GSC_HD void push_event(Env& S, double t, uint32_t prio, int16_t proc, int16_t fl
   const uint32_t key = (prio << 31) | (h->eid & 0x7fffffffu);
   h->eid++;
   if (h->n_events >= S.d.event_cap) { h->flags |= FLAG_EVENT_OVERFLOW; return; }
-  Event& e = S.events[h->n_events++];
+  Event e;
   e.t = t;
   e.key = key;
   e.proc = proc;
   e.flow = flow;
+  S.events[h->n_events++] = e;
   if (h->n_events > h->max_events) h->max_events = h->n_events;
 }
 // yield env.timeout(delay) of process pid (whose flow is `flow`)
@@ -547,8 +552,10 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
     P.x = pd;
   } else {  // F_AFTER_HOP
     const int pa = GSC_UNI(P.a), pc = GSC_UNI(P.c);
-    const int hop = GSC_UNI(T.pnodes[(pa * n + nxt) * T.H + pc]);
-    const int e = GSC_UNI(T.edge_id[GSC_UNI(f.node) * n + hop]);
+    // the hop just taken and its edge were kept in the record (ret / pad: a forwarder has no
+    // children) when it was scheduled: no dependent path-table / edge-table lookups here
+    const int hop = GSC_UNI(P.ret);
+    const int e = GSC_UNI(P.pad);
     const int c = spawn(S, P_RETLINK, RL_INIT, -1, -1);
     if (c >= 0) { S.procs[c].a = (int16_t)e; S.procs[c].x = f.dr; S.procs[c].y = f.duration; }
     f.node = (int16_t)hop;
@@ -566,9 +573,10 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
     }
   }
   // next hop
-  const int hop = GSC_UNI(T.pnodes[(GSC_UNI(P.a) * n + nxt) * T.H + GSC_UNI(P.c)]);
+  const int pidx = (GSC_UNI(P.a) * n + nxt) * T.H + GSC_UNI(P.c);
+  const int hop = GSC_UNI(T.pnodes[pidx]);
   const int cur = GSC_UNI(f.node);
-  const int e = GSC_UNI(T.edge_id[cur * n + hop]);
+  const int e = GSC_UNI(T.pedges[pidx]);  // == edge_id[cur * n + hop]
   Flow& fm = S.flows[fid];
   fm.node = f.node;
   const double lrem = S.link_rem[e];
@@ -582,6 +590,8 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
   const double hd = T.pdelay[cur * n + hop];
   if (GSC_UNI(hop == f.egress && f.fwd_eg)) fm.departed = 1;
   P.state = F_AFTER_HOP;
+  P.ret = (int16_t)hop;
+  P.pad = (int16_t)e;
   S.procs[pid] = P;
   timeout(S, pid, P.flow, hd);
   (void)K;
@@ -644,8 +654,19 @@ GSC_HD_CALL void run_request(Env& S, const SimConst& K, int pid, const Proc& P, 
   const int fid = GSC_UNI(P.flow);
   const int node = GSC_UNI(P.a), sf = GSC_UNI(P.b), Sd = S.d.S;
   double demanded = 0.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  {  // the node's SF rows loaded by one lane each (one LDS round trip), summed in the serial order
+    const int lane = wave_lane();
+    int pres = 0;
+    double ld = 0.0;
+    if (lane < Sd) { pres = S.sf_present[node * Sd + lane]; ld = S.sf_load[node * Sd + lane]; }
+    for (int s = 0; s < Sd; ++s)
+      if (__builtin_amdgcn_readlane(pres, s)) demanded += readlane_f64(ld, s) + (s == sf ? f.dr : 0.0);
+  }
+#else
   for (int s = 0; s < Sd; ++s)
     if (GSC_UNI(S.sf_present[node * Sd + s])) demanded += S.sf_load[node * Sd + s] + (s == sf ? f.dr : 0.0);
+#endif
   const double cap = S.node_cap[node];
   if (GSC_UNI(!(demanded <= cap))) { proc_return(S, pid, P, 0); return; }
   Flow& fm = S.flows[fid];
@@ -687,8 +708,19 @@ GSC_HD_CALL void run_finish(Env& S, const SimConst& K, int pid, const Proc& P, c
   S.sf_load[node * Sd + sf] = load;
   if (GSC_UNI(load == 0.0 && !S.placement[node * Sd + sf])) S.sf_present[node * Sd + sf] = 0;
   double used = 0.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  {  // as in run_request: one lane per SF row, serial-order sum
+    const int lane = wave_lane();
+    int pres = 0;
+    double ld = 0.0;
+    if (lane < Sd) { pres = S.sf_present[node * Sd + lane]; ld = S.sf_load[node * Sd + lane]; }
+    for (int s = 0; s < Sd; ++s)
+      if (__builtin_amdgcn_readlane(pres, s)) used += readlane_f64(ld, s);
+  }
+#else
   for (int s = 0; s < Sd; ++s)
     if (GSC_UNI(S.sf_present[node * Sd + s])) used += S.sf_load[node * Sd + s];
+#endif
   S.node_rem[node] = S.node_cap[node] - used;
   proc_return(S, pid, P, 0);
 }

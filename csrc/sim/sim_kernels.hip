@@ -141,7 +141,7 @@ __device__ __forceinline__ int argmin_event_wave(const Env& S, int lane) {
 __host__ __device__ inline long topo_stage_bytes(const Dims& D, int H) {
   const long n2 = (long)D.N * D.N;
   return align16(sizeof(TopoDev)) + align16((int)(8 * D.N)) + align16((int)(8 * n2)) + align16((int)(2 * n2)) +
-         align16((int)(2 * n2 * H)) + align16((int)(2 * n2)) + align16((int)(8 * D.E)) + 2 * align16(2 * D.N);
+         2 * align16((int)(2 * n2 * H)) + align16((int)(2 * n2)) + align16((int)(8 * D.E)) + 2 * align16(2 * D.N);
 }
 __host__ __device__ inline long const_stage_bytes() { return align16(sizeof(SimConst)); }
 
@@ -175,6 +175,7 @@ __device__ __forceinline__ TopoDev stage_topo(const TopoDev& g, char* dst, int l
   t.pdelay = (const double*)put(g.pdelay, 8 * n2);
   t.plen = (const int16_t*)put(g.plen, 2 * n2);
   t.pnodes = (const int16_t*)put(g.pnodes, 2 * n2 * g.H);
+  t.pedges = (const int16_t*)put(g.pedges, 2 * n2 * g.H);
   t.edge_id = (const int16_t*)put(g.edge_id, 2 * n2);
   t.edge_cap = (const double*)put(g.edge_cap, 8 * (g.E > 0 ? g.E : 1));
   t.ingress = (const int16_t*)put(g.ingress, 2 * (g.n_ing > 0 ? g.n_ing : 1));
@@ -360,6 +361,8 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
         if (q.n + ni > S.h->max_events) S.h->max_events = q.n + ni;
         if (ni == 0 || n_disp >= 4096) break;
         int bi = 0;
+        // (measured: keeping the last pushed event in registers to skip this LDS read when the
+        // handler pushed exactly one event cost 44 VGPRs and was slower, 100.0k vs 104.0k env-steps/s)
         Event m = S.events[0];
         for (int i = 1; i < ni; ++i) {
           const Event c = S.events[i];
@@ -466,6 +469,10 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   if (lane == 0) *Ks = a.K;
   char* topo_lds = smem + sb + const_stage_bytes();
   char* g = a.states + (long)env * a.state_bytes;
+  // diagnostic variant: shader-clock cycles and 100 MHz wall ticks over the whole workgroup (slots
+  // 58 / 59) -> the effective engine clock while the simulator runs (e.g. beside the learner)
+  const unsigned long long c_begin = PROF ? __builtin_amdgcn_s_memtime() : 0;
+  const unsigned long long r_begin = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
   if constexpr (LDS_STATE) {
     const unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
     copy16(smem, g, sbytes, lane);
@@ -483,6 +490,12 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   } else {
     __syncthreads();
     device_step_env<B, QSETS, false>(a, *Ks, g, topo_lds, env, lane);
+  }
+  if (PROF && lane == 0) {
+    a.prof_types[((long)env * 64 + 58) * 2] += __builtin_amdgcn_s_memtime() - c_begin;
+    a.prof_types[((long)env * 64 + 58) * 2 + 1] += 1;
+    a.prof_types[((long)env * 64 + 59) * 2] += __builtin_amdgcn_s_memrealtime() - r_begin;
+    a.prof_types[((long)env * 64 + 59) * 2 + 1] += 1;
   }
 }
 
@@ -554,6 +567,7 @@ class SimContext {
       td.pdelay = ptr<const double>(t["pdelay"].cast<uintptr_t>());
       td.plen = ptr<const int16_t>(t["plen"].cast<uintptr_t>());
       td.pnodes = ptr<const int16_t>(t["pnodes"].cast<uintptr_t>());
+      td.pedges = ptr<const int16_t>(t["pedges"].cast<uintptr_t>());
       td.edge_id = ptr<const int16_t>(t["edge_id"].cast<uintptr_t>());
       td.edge_cap = ptr<const double>(t["edge_cap"].cast<uintptr_t>());
       td.ingress = ptr<const int16_t>(t["ingress"].cast<uintptr_t>());

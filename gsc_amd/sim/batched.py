@@ -174,10 +174,16 @@ class BatchedSimulator:
         # topology tables
         topo_dicts = []
         for t in self.topologies:
+            # edge of hop k on the shortest path i -> j (from node k-1 of the path, or i), so the
+            # forwarder reads a hop's node and edge in parallel instead of one after the other
+            pn = np.asarray(t.path_nodes)
+            prev = np.concatenate([np.broadcast_to(np.arange(t.n)[:, None, None], (t.n, t.n, 1)), pn[:, :, :-1]], axis=2)
+            pedges = np.where(pn >= 0, np.asarray(t.edge_id)[prev.clip(0), pn.clip(0)], -1)
             tens = dict(cap=torch.from_numpy(t.node_cap.astype(np.float64)),
                         pdelay=torch.from_numpy(np.ascontiguousarray(t.path_delay.reshape(-1))),
                         plen=torch.from_numpy(t.path_len.reshape(-1).astype(np.int16)),
                         pnodes=torch.from_numpy(t.path_nodes.reshape(-1).astype(np.int16)),
+                        pedges=torch.from_numpy(pedges.reshape(-1).astype(np.int16)),
                         edge_id=torch.from_numpy(t.edge_id.reshape(-1).astype(np.int16)),
                         edge_cap=torch.from_numpy(np.ascontiguousarray(t.edge_cap) if t.num_edges else np.zeros(1)),
                         ingress=torch.from_numpy(t.ingress.astype(np.int16) if len(t.ingress) else np.zeros(1, np.int16)),

@@ -60,14 +60,16 @@ if args.profile:
     names = ["free", "writer", "mmpp", "trace", "arrival", "handle", "decide", "forward", "process", "request",
              "finish", "retlink"]
     phases = {60: "copy-in (state HBM->LDS)", 61: "copy-out (LDS->HBM)", 62: "prologue", 63: "epilogue"}
-    tot = ty[:60, 0].sum()
-    for i in range(60):
+    tot = ty[:58, 0].sum()
+    for i in range(58):
         if ty[i, 1] > 0:
             print(f"  {names[i // 4]:8s} state {i % 4} events/env-step={ty[i, 1] / (args.envs * args.steps):7.1f} "
                   f"cycles/dispatch={ty[i, 0] / ty[i, 1]:7.0f} share={ty[i, 0] / tot:.3f}")
     for i, nm in phases.items():
         if ty[i, 1] > 0:
             print(f"  {nm:26s} cycles/env-step={ty[i, 0] / ty[i, 1]:9.0f}")
+    if ty[59, 0] > 0:  # whole-workgroup shader cycles / 100 MHz wall ticks
+        print(f"  effective engine clock  {ty[58, 0] / ty[59, 0] * 100:.0f} MHz")
     print(f"cycles/event: select={p[0] / p[3]:.0f} dispatch={p[1] / p[3]:.0f} merge={p[2] / p[3]:.0f} "
           f"events/env-step={p[3] / (args.envs * args.steps):.0f}  "
           f"event loop cycles/env-step={(p[0] + p[1] + p[2]) / (args.envs * args.steps):.0f}")
