@@ -83,6 +83,7 @@ struct Header {
   double total_e2e, total_path_delay, total_proc_delay;
   double run_e2e, run_max_e2e, run_total_path_delay, run_avg_path_delay;
   double ewma_flows, episode_return;
+  int32_t proc_head, pad_h;  // proc_free[proc_top - 1] (the next pid to allocate), cached off the LDS stack
 };
 
 // Read-only per-topology tables (device or host memory).
@@ -312,7 +313,11 @@ GSC_HD void timeout(Env& S, int pid, int flow, double delay) {
 GSC_HD int alloc_proc(Env& S, uint8_t type, uint8_t state, int flow, int parent) {
   Header* h = S.h;
   if (h->proc_top <= 0) { h->flags |= FLAG_PROC_OVERFLOW; return -1; }
-  const int pid = GSC_UNI(S.proc_free[--h->proc_top]);
+  // the stack top is cached in the header: no dependent LDS read before the new record is written;
+  // the next top is loaded now and only needed by the next allocation
+  const int pid = GSC_UNI(h->proc_head);
+  --h->proc_top;
+  h->proc_head = h->proc_top > 0 ? (int)S.proc_free[h->proc_top - 1] : -1;
   Proc& p = S.procs[pid];
   p.type = type; p.state = state; p.flow = (int16_t)flow; p.parent = (int16_t)parent;
   p.a = p.b = p.c = p.ret = 0; p.x = p.y = 0.0;
@@ -344,6 +349,7 @@ GSC_HD void proc_return(Env& S, int pid, const Proc& P, int16_t value) {
   }
   S.procs[pid].type = P_FREE;
   S.proc_free[S.h->proc_top++] = (int16_t)pid;
+  S.h->proc_head = pid;
 }
 
 GSC_HD int alloc_flow(Env& S) {
@@ -914,6 +920,7 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
   h->flow_top = S.d.flow_cap;
   for (int i = l0; i < S.d.flow_cap; i += ls) S.flow_free[i] = (int16_t)(S.d.flow_cap - 1 - i);
   h->proc_top = S.d.proc_cap;
+  h->proc_head = S.d.proc_cap > 0 ? 0 : -1;  // == proc_free[proc_cap - 1]
   for (int i = l0; i < S.d.proc_cap; i += ls) { S.proc_free[i] = (int16_t)(S.d.proc_cap - 1 - i); S.procs[i].type = P_FREE; }
   reset_run_metrics(S, K, n, l0, ls);  // ends with lanes_sync
   // reference order: writer, (MMPP), (trace), arrivals; then one env.step()

@@ -333,6 +333,10 @@ class TrainerConfig:
                                             # (metrics/flush/state_dict/load_state_dict/reseed), not around every
                                             # step -- saves two cross-stream event hops per step; the caller must
                                             # not touch trainer tensors between steps without those (or a device sync)
+    act_on_sim_stream: bool = os.environ.get("GSC_ACT_ON_SIM", "1") == "1"  # overlap mode: the actor forward + exploration of step t+1 run on the
+                                            # simulator's stream right behind step t's simulator kernel (after the
+                                            # learner's update t), so the act -> simulate chain has no cross-stream
+                                            # hop; the learner waits for the act (it reads the actor weights)
 
 
 class BatchedTrainer:
@@ -379,7 +383,9 @@ class BatchedTrainer:
         self.topo = self.sim.topo_cur.to(torch.int64).clone()
         self.masks = self.learner.masks
         self._act_bufs = [torch.empty(self.E, sim.action_dim, device=self.device) for _ in range(2)]
-        self._pending = None  # (obs, topo, act, out) of the last step, not yet in replay / metrics
+        self._pending = None  # (obs, topo, act, out, sim event) of the last step, not yet in replay / metrics
+        # recycled events of the act-on-simulator-stream chain (at most a few in flight)
+        self._events = [torch.cuda.Event() for _ in range(6)] if self.device.type == "cuda" else []
         if self.device.type == "cuda":
             self.learner.enable_native_act(self.E)
         # device-side metric accumulators (read back only when logging)
@@ -460,16 +466,24 @@ class BatchedTrainer:
                                      torch.cuda.current_stream(self.device).cuda_stream
                                      if self.device.type == "cuda" else 0)
 
+    def _event(self):
+        return self._events.pop(0) if self._events else torch.cuda.Event()
+
     def _flush_pending(self) -> None:
         if self._pending is not None:
             p, self._pending = self._pending, None
-            self._record(*p)
+            if p[4] is not None:  # simulator outputs produced on the simulator's stream
+                torch.cuda.current_stream(self.device).wait_event(p[4])
+                self._events.append(p[4])
+            self._record(*p[:4])
 
     def _join(self) -> None:
         """Caller's stream waits for the trainer's streams; the next step re-syncs in the other direction."""
         if self.learn_stream is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.learn_stream)
             self._handoff = True
+        if self.sim_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.sim_stream)
 
     def flush(self) -> None:
         """Complete the deferred replay insert / metrics of the last step (before reading them)."""
@@ -496,23 +510,51 @@ class BatchedTrainer:
         else:
             self._step()
 
+    def _act(self, obs, topo, warm: bool, k: int) -> torch.Tensor:
+        with trace_range("act"):
+            mu = self.learner.act(obs, topo)
+        with trace_range("explore"):
+            return explore_postprocess(mu, self.masks, self.sim.n_pad, warm, self.rand_mu, self.rand_sigma,
+                                       seed=self.t.seed * 131 + self.dist.rank, step=self.global_step,
+                                       out=self._act_bufs[k], topo=topo)
+
     def _step(self) -> None:
         warm = self.global_step < self.learning_starts
         k = self.global_step & 1
         obs, topo = self._obs_bufs[self.global_step % 3], self.topo
         obs_next = self._obs_bufs[(self.global_step + 1) % 3]
-        with trace_range("act"):
-            mu = self.learner.act(obs, topo)
-        with trace_range("explore"):
-            act = explore_postprocess(mu, self.masks, self.sim.n_pad, warm, self.rand_mu, self.rand_sigma,
-                                      seed=self.t.seed * 131 + self.dist.rank, step=self.global_step,
-                                      out=self._act_bufs[k], topo=topo)
-        self._schedule_next()
+        episode_end = (self.global_step + 1) % self.sim.episode_steps == 0
         train = self.global_step >= self.learning_starts - 1 and (len(self.replay) > 0 or self._pending is not None)
-        if self.sim_stream is not None and train:
+        overlap = self.sim_stream is not None and train
+        main = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        new_topo = None
+        if overlap and self.t.act_on_sim_stream:
+            # act(t) -> explore(t) -> simulator(t) in order on the simulator's stream, after everything the
+            # learner's stream holds so far (update t-1 wrote the actor weights; replay inserts read the
+            # buffers this step reuses).  The learner's replay insert of step t-1 and update t wait for the
+            # act only (the update rewrites the actor weights), so they run concurrently with simulator(t).
+            self.sim_stream.wait_stream(main)
+            with torch.cuda.stream(self.sim_stream):
+                act = self._act(obs, topo, warm, k)
+                ev_act = self._event()
+                ev_act.record(self.sim_stream)
+                self._schedule_next()
+                out = self.sim.step(act, buffer_set=k, obs_out=obs_next)
+                ev_sim = self._event()
+                ev_sim.record(self.sim_stream)
+                if episode_end:
+                    new_topo = self.sim.topo_next.to(torch.int64).clone()
+            main.wait_event(ev_act)
+            self._events.append(ev_act)
+            self._flush_pending()
+            with trace_range("learn"):
+                self._learn()
+            self._pending = (obs, topo, act, out, ev_sim)
+        elif overlap:
+            act = self._act(obs, topo, warm, k)
+            self._schedule_next()
             # simulator kernel (one wave per env) runs concurrently with the previous step's replay
             # insert and the learner update, which samples transitions up to the previous step
-            main = torch.cuda.current_stream(self.device)
             self.sim_stream.wait_stream(main)
             with torch.cuda.stream(self.sim_stream):
                 out = self.sim.step(act, buffer_set=k, obs_out=obs_next)
@@ -520,8 +562,10 @@ class BatchedTrainer:
             with trace_range("learn"):
                 self._learn()
             main.wait_stream(self.sim_stream)
-            self._pending = (obs, topo, act, out)
+            self._pending = (obs, topo, act, out, None)
         else:
+            act = self._act(obs, topo, warm, k)
+            self._schedule_next()
             self._flush_pending()
             with trace_range("sim"):
                 out = self.sim.step(act, buffer_set=k, obs_out=obs_next)
@@ -529,14 +573,15 @@ class BatchedTrainer:
             if train:
                 with trace_range("learn"):
                     self._learn()
-        episode_end = (self.global_step + 1) % self.sim.episode_steps == 0
         if episode_end:
             self.episode += 1
-            self.topo = self.sim.topo_next.to(torch.int64).clone()
+            self.topo = new_topo if new_topo is not None else self.sim.topo_next.to(torch.int64).clone()
         self.global_step += 1
         # pool overflow (flows / processes / events dropped) fails the run at the latest at the end of
         # the episode it happened in (one flag read per episode), or every check_every steps
         if episode_end or (self.t.check_every and self.global_step % self.t.check_every == 0):
+            if overlap and self.t.act_on_sim_stream:
+                main.wait_stream(self.sim_stream)
             self.sim.check_flags()
 
     def _learn(self) -> None:

@@ -27,6 +27,7 @@ def main():
         xccs = sorted({i[0] for i in ids})
         per = {x: sum(1 for i in ids if i[0] == x) for x in xccs}
         print(f"{label:>28}: {len(ids):3d} distinct CUs  per-XCC {per}", flush=True)
+        return ids
 
     probe(None, "default stream")
     probe(list(range(n)), "all bits")
@@ -37,6 +38,10 @@ def main():
     probe([i for i in range(n) if i % 8 in (0, 1)], "bits i%8 in {0,1}")
     probe(list(range(128)), "bits 0-127")
     probe(list(range(128, 256)), "bits 128-255")
+    # per-bit mapping (mask bit -> xcc, se, sh, cu) for the first 64 bits
+    for i in range(64):
+        ids = probe([i], f"bit {i}")
+        print(f"    bit {i} -> {sorted(ids)}", flush=True)
 
 
 if __name__ == "__main__":
