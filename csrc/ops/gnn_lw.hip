@@ -11,8 +11,8 @@
 // atomics), weight gradients dW = dX^T h and input gradients dX W on the GEMM engine, vector
 // gradients by deterministic two-phase column sums.
 //
-// Lanes: a 32-lane half-wave owns one (graph, node) with lane c = channel (H <= 32); message scores
-// reduce over the half-wave with xor shuffles.  Reference: PyG GATv2Conv as gatv2_dense_reference
+// Lanes: a 32-lane half-wave (H <= 32) or a whole wave (H <= 64) owns one (graph, node) with lane
+// c = channel; message scores reduce over those lanes with xor shuffles.  Reference: PyG GATv2Conv as gatv2_dense_reference
 // (gsc_amd/models/gnn.py) -- reference repo src/rlsp/agents/models.py:10-53.
 #include <pybind11/pybind11.h>
 
@@ -35,9 +35,11 @@ struct LwGraph {
   int B, P, M, H;
 };
 
-__device__ __forceinline__ float lw_sum32(float v) {
+// sum over the NL lanes (32: half-wave, 64: wave) that own one node
+template <int NL>
+__device__ __forceinline__ float lw_sum(float v) {
 #pragma unroll
-  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+  for (int o = NL / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, NL);
   return v;
 }
 
@@ -45,12 +47,13 @@ __device__ __forceinline__ float leaky(float z) { return z > 0.f ? z : kLwSlope 
 
 // ---- forward attention + aggregation ---------------------------------------------------------------
 // h_out[b,i,:] = act( sum_q alpha_q x_l[b,j_q,:] / deg_i + bias ),  alpha_q saved as [B, M]
+template <int NL>
 __global__ __launch_bounds__(256) void lw_attn_fwd_kernel(LwGraph g, const float* __restrict__ xl,
                                                           const float* __restrict__ xr, const float* __restrict__ att,
                                                           const float* __restrict__ bias, int relu,
                                                           float* __restrict__ h_out, float* __restrict__ alpha) {
-  const long node = (long)blockIdx.x * 8 + (threadIdx.x >> 5);  // 8 nodes per block
-  const int c = threadIdx.x & 31;
+  const long node = (long)blockIdx.x * (256 / NL) + (threadIdx.x / NL);  // 256 / NL nodes per block
+  const int c = threadIdx.x & (NL - 1);
   if (node >= (long)g.B * g.P) return;
   const int b = (int)(node / g.P), i = (int)(node - (long)b * g.P);
   const int t = g.topo[b];
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(256) void lw_attn_fwd_kernel(LwGraph g, const float
   // max, softmax denominator, then alpha (saved) and the aggregation
   auto score = [&](int q, float& xlj) {
     xlj = c < H ? xlb[(long)src[q] * H + c] : 0.f;
-    return lw_sum32(ac * leaky(xlj + xri));
+    return lw_sum<NL>(ac * leaky(xlj + xri));
   };
   float mx = -__builtin_inff(), xlj;
   for (int q = q0; q < q1; ++q) {
@@ -93,9 +96,10 @@ __global__ __launch_bounds__(256) void lw_attn_fwd_kernel(LwGraph g, const float
 }
 
 // emb[b,:] = mean over the graph's real nodes of h[b,:,:]
+template <int NL>
 __global__ __launch_bounds__(256) void lw_pool_kernel(LwGraph g, const float* __restrict__ h, float* __restrict__ emb) {
-  const long b = (long)blockIdx.x * 8 + (threadIdx.x >> 5);
-  const int c = threadIdx.x & 31;
+  const long b = (long)blockIdx.x * (256 / NL) + (threadIdx.x / NL);
+  const int c = threadIdx.x & (NL - 1);
   if (b >= g.B || c >= g.H) return;
   const int n = g.nnodes[g.topo[b]];
   const float* hb = h + b * g.P * g.H;
@@ -120,14 +124,15 @@ __global__ __launch_bounds__(256) void lw_pool_bwd_kernel(LwGraph g, const float
 // In:  dh (gradient at this conv's output; overwritten by dY = dh * relu'(h_out)), h_out (null: no
 //      ReLU), x_l, x_r, alpha.  Out: dxr[b,i,:] (gathered), per-message x_l gradients msg[b,q,:]
 //      = alpha_q dY_i / deg_i + dz_q, per-node d att partials datt[b,i,:].
+template <int NL>
 __global__ __launch_bounds__(256) void lw_attn_bwd_kernel(LwGraph g, float* __restrict__ dh,
                                                           const float* __restrict__ h_out, const float* __restrict__ xl,
                                                           const float* __restrict__ xr,
                                                           const float* __restrict__ alpha, const float* __restrict__ att,
                                                           float* __restrict__ dxr, float* __restrict__ msg,
                                                           float* __restrict__ datt) {
-  const long node = (long)blockIdx.x * 8 + (threadIdx.x >> 5);
-  const int c = threadIdx.x & 31;
+  const long node = (long)blockIdx.x * (256 / NL) + (threadIdx.x / NL);
+  const int c = threadIdx.x & (NL - 1);
   if (node >= (long)g.B * g.P) return;
   const int b = (int)(node / g.P), i = (int)(node - (long)b * g.P);
   const int t = g.topo[b];
@@ -156,14 +161,14 @@ __global__ __launch_bounds__(256) void lw_attn_bwd_kernel(LwGraph g, float* __re
   float sad = 0.f;
   for (int q = q0; q < q1; ++q) {
     const int j = src[q];
-    const float da = lw_sum32(ch ? gc * xlb[(long)j * H + c] : 0.f);
+    const float da = lw_sum<NL>(ch ? gc * xlb[(long)j * H + c] : 0.f);
     sad += al[q] * da;
   }
   float dxr_acc = 0.f, datt_acc = 0.f;
   for (int q = q0; q < q1; ++q) {
     const int j = src[q];
     const float xlj = ch ? xlb[(long)j * H + c] : 0.f;
-    const float da = lw_sum32(gc * xlj);
+    const float da = lw_sum<NL>(gc * xlj);
     const float de = al[q] * (da - sad);
     const float z = xlj + xri;
     datt_acc += de * leaky(z);
@@ -178,9 +183,10 @@ __global__ __launch_bounds__(256) void lw_attn_bwd_kernel(LwGraph g, float* __re
 }
 
 // dxl[b,j,:] = sum over messages out of j of msg[b,q,:]   (source-sorted CSR; no atomics)
+template <int NL>
 __global__ __launch_bounds__(256) void lw_src_gather_kernel(LwGraph g, const float* __restrict__ msg, float* __restrict__ dxl) {
-  const long node = (long)blockIdx.x * 8 + (threadIdx.x >> 5);
-  const int c = threadIdx.x & 31;
+  const long node = (long)blockIdx.x * (256 / NL) + (threadIdx.x / NL);
+  const int c = threadIdx.x & (NL - 1);
   if (node >= (long)g.B * g.P || c >= g.H) return;
   const int b = (int)(node / g.P), j = (int)(node - (long)b * g.P);
   const int t = g.topo[b];
@@ -236,16 +242,22 @@ static LwGraph lw_graph(py::dict t, uintptr_t topo, int B, int P, int H) {
   g.B = B;
   g.P = P;
   g.H = H;
-  GSC_CHECK(H <= 32, "layer-wise GATv2: at most 32 channels");
+  GSC_CHECK(H <= 64, "layer-wise GATv2: at most 64 channels");
   return g;
 }
 
-static dim3 node_grid(const LwGraph& g) { return dim3((unsigned)(((long)g.B * g.P + 7) / 8)); }
+// lanes per node: a half-wave for H <= 32 (two nodes per wave), a whole wave up to 64 channels
+static int lanes_per_node(const LwGraph& g) { return g.H <= 32 ? 32 : 64; }
+static dim3 node_grid(const LwGraph& g) {
+  const long per = 256 / lanes_per_node(g);
+  return dim3((unsigned)(((long)g.B * g.P + per - 1) / per));
+}
 
 void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t xl, uintptr_t xr, uintptr_t att,
                  uintptr_t bias, int relu, uintptr_t h_out, uintptr_t alpha, uintptr_t stream) {
   const LwGraph g = lw_graph(tables, topo, B, P, H);
-  hipLaunchKernelGGL(lw_attn_fwd_kernel, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<const float>(xl),
+  auto k = lanes_per_node(g) == 32 ? lw_attn_fwd_kernel<32> : lw_attn_fwd_kernel<64>;
+  hipLaunchKernelGGL(k, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<const float>(xl),
                      ptr<const float>(xr), ptr<const float>(att), ptr<const float>(bias), relu, ptr<float>(h_out),
                      ptr<float>(alpha));
   check_launch();
@@ -253,7 +265,9 @@ void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
 
 void lw_pool(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t h, uintptr_t emb, uintptr_t stream) {
   const LwGraph g = lw_graph(tables, topo, B, P, H);
-  hipLaunchKernelGGL(lw_pool_kernel, dim3((B + 7) / 8), dim3(256), 0, stream_of(stream), g, ptr<const float>(h),
+  const int per = 256 / lanes_per_node(g);
+  auto k = per == 8 ? lw_pool_kernel<32> : lw_pool_kernel<64>;
+  hipLaunchKernelGGL(k, dim3((B + per - 1) / per), dim3(256), 0, stream_of(stream), g, ptr<const float>(h),
                      ptr<float>(emb));
   check_launch();
 }
@@ -270,7 +284,8 @@ void lw_attn_bwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
                  uintptr_t xr, uintptr_t alpha, uintptr_t att, uintptr_t dxr, uintptr_t msg, uintptr_t datt,
                  uintptr_t stream) {
   const LwGraph g = lw_graph(tables, topo, B, P, H);
-  hipLaunchKernelGGL(lw_attn_bwd_kernel, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<float>(dh),
+  auto k = lanes_per_node(g) == 32 ? lw_attn_bwd_kernel<32> : lw_attn_bwd_kernel<64>;
+  hipLaunchKernelGGL(k, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<float>(dh),
                      ptr<const float>(h_out), ptr<const float>(xl), ptr<const float>(xr), ptr<const float>(alpha),
                      ptr<const float>(att), ptr<float>(dxr), ptr<float>(msg), ptr<float>(datt));
   check_launch();
@@ -278,7 +293,8 @@ void lw_attn_bwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
 
 void lw_src_gather(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t msg, uintptr_t dxl, uintptr_t stream) {
   const LwGraph g = lw_graph(tables, topo, B, P, H);
-  hipLaunchKernelGGL(lw_src_gather_kernel, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<const float>(msg),
+  auto k = lanes_per_node(g) == 32 ? lw_src_gather_kernel<32> : lw_src_gather_kernel<64>;
+  hipLaunchKernelGGL(k, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<const float>(msg),
                      ptr<float>(dxl));
   check_launch();
 }

@@ -49,6 +49,7 @@ struct SimArgs {
   int prio;                  // wave priority of the step kernel (s_setprio), see sim_step_kernel
   unsigned long long* prof_types;  // optional [E, 64, 2] dispatch cycles / count per (process type, state)
   int32_t* topo_cur;         // optional [E]: topology each env runs now (updated where an env was reset)
+  int stage_pedges;          // the per-hop edge table is part of the staged topology
 };
 
 GSC_HD void step_epilogue(Env& S, const SimArgs& a, const SimConst& K, int env) {
@@ -138,15 +139,17 @@ __device__ __forceinline__ int argmin_event_wave(const Env& S, int lane) {
 }
 
 // Bytes of LDS used to stage SimConst + the env's topology tables in front of the state blob.
-__host__ __device__ inline long topo_stage_bytes(const Dims& D, int H) {
+// (pedges: the per-hop edge table is staged too; else it is read from L2)
+__host__ __device__ inline long topo_stage_bytes(const Dims& D, int H, bool pedges = true) {
   const long n2 = (long)D.N * D.N;
   return align16(sizeof(TopoDev)) + align16((int)(8 * D.N)) + align16((int)(8 * n2)) + align16((int)(2 * n2)) +
-         2 * align16((int)(2 * n2 * H)) + align16((int)(2 * n2)) + align16((int)(8 * D.E)) + 2 * align16(2 * D.N);
+         (pedges ? 2 : 1) * align16((int)(2 * n2 * H)) + align16((int)(2 * n2)) + align16((int)(8 * D.E)) +
+         2 * align16(2 * D.N);
 }
 __host__ __device__ inline long const_stage_bytes() { return align16(sizeof(SimConst)); }
 
 // Copy one topology's tables into LDS and return a TopoDev whose pointers address the copies.
-__device__ __forceinline__ TopoDev stage_topo(const TopoDev& g, char* dst, int lane) {
+__device__ __forceinline__ TopoDev stage_topo(const TopoDev& g, char* dst, int lane, bool pedges) {
   TopoDev t = g;
   const int n = g.n, n2 = n * n;
   char* p = dst;
@@ -175,7 +178,7 @@ __device__ __forceinline__ TopoDev stage_topo(const TopoDev& g, char* dst, int l
   t.pdelay = (const double*)put(g.pdelay, 8 * n2);
   t.plen = (const int16_t*)put(g.plen, 2 * n2);
   t.pnodes = (const int16_t*)put(g.pnodes, 2 * n2 * g.H);
-  t.pedges = (const int16_t*)put(g.pedges, 2 * n2 * g.H);
+  if (pedges) t.pedges = (const int16_t*)put(g.pedges, 2 * n2 * g.H);
   t.edge_id = (const int16_t*)put(g.edge_id, 2 * n2);
   t.edge_cap = (const double*)put(g.edge_cap, 8 * (g.E > 0 ? g.E : 1));
   t.ingress = (const int16_t*)put(g.ingress, 2 * (g.n_ing > 0 ? g.n_ing : 1));
@@ -304,7 +307,8 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   // (measured: header in LDS instead = 2.83 vs 2.30 ms/step for 256 Abilene envs)
   Header h_reg = *h_mem;
   S.h = &h_reg;
-  const TopoDev T = a.topo_stage ? stage_topo(a.topos[S.h->topo], topo_lds, lane) : a.topos[S.h->topo];
+  const TopoDev T = a.topo_stage ? stage_topo(a.topos[S.h->topo], topo_lds, lane, a.stage_pedges)
+                                 : a.topos[S.h->topo];
   load_action(S, K, T, a.actions + (long)env * a.action_stride, lane, 64);
   __syncthreads();
   // pending events -> sorted register queue; S.events then serves as the handlers' inbox
@@ -591,8 +595,25 @@ class SimContext {
       // Large topologies (N^2 * hops path tables beyond the LDS budget, e.g. 200 nodes): the tables
       // stay in HBM and are served from L2 — only SimConst (+ the state blob, if it fits) is staged.
       if (const_stage_bytes() + topo_stage_ + 1024 > max_lds) topo_stage_ = 0;
+      // the state blob has priority over the topology tables: every event reads and writes it,
+      // while the tables are read-only and stay L2-resident (e.g. 50-node topologies: both do
+      // not fit one workgroup's LDS together)
+      if (topo_stage_ && const_stage_bytes() + topo_stage_ + L_.total > max_lds &&
+          const_stage_bytes() + L_.total <= max_lds)
+        topo_stage_ = 0;
       const long fixed = const_stage_bytes() + topo_stage_;
       use_lds_ = fixed + L_.total <= max_lds;
+      // the per-hop edge table saves one dependent lookup per hop, but not at the price of a
+      // workgroup per CU (50-node topologies with the state blob in HBM: 112 vs 72 KB of tables)
+      if (topo_stage_) {
+        const long state = use_lds_ ? L_.total : 0;
+        const long without = topo_stage_bytes(D_, maxH, false);
+        const long cu_lds = 160 * 1024;
+        if (cu_lds / (const_stage_bytes() + topo_stage_ + state) < cu_lds / (const_stage_bytes() + without + state)) {
+          topo_stage_ = without;
+          stage_pedges_ = 0;
+        }
+      }
       const long need = fixed + (use_lds_ ? L_.total : 0);
       qsets_ = D_.event_cap <= 64 ? 1 : (D_.event_cap <= 128 ? 2 : (D_.event_cap <= 256 ? 4 : 8));
       if (need > 65536) {
@@ -683,6 +704,7 @@ class SimContext {
     a.E = E;
     a.use_lds = use_lds_ ? 1 : 0;
     a.topo_stage = topo_stage_;
+    a.stage_pedges = stage_pedges_;
     return a;
   }
 
@@ -755,6 +777,7 @@ class SimContext {
   int host_threads_;
   bool use_lds_ = false;
   long topo_stage_ = 0;
+  int stage_pedges_ = 1;
   int qsets_ = 8;
   Dims D_{};
   Layout L_{};

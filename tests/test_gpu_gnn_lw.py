@@ -86,3 +86,11 @@ def test_native_update_uses_layerwise_for_200_nodes():
     assert L._native is not None and L._native.layerwise
     assert torch.isfinite(L.actor_flat.flat).all() and not torch.equal(before, L.actor_flat.flat)
     assert all(float(v) == float(v) for v in L.last.values())
+
+
+@pytest.mark.parametrize("hidden", [40, 64])
+def test_layerwise_wide_hidden(hidden):
+    """More than 32 channels: one whole wave per node (lw_*_kernel<64>), Abilene + BtEurope."""
+    gs = GraphSet([load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml")),
+                   load_topology(cfg_path("networks", "bteurope", "bteurope-in4-rand-cap0-2.graphml"))], 24, DEV)
+    _check(gs, 24, 333, hidden=hidden, direct=True)
