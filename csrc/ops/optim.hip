@@ -140,21 +140,26 @@ void polyak(uintptr_t target, uintptr_t p, long n, float tau, uintptr_t stream) 
 
 // flag[0] = any non-finite value in g[0..n); flag[1] += flag[0] (skipped-update counter).
 // One block per 64K elements, atomicOr into the flag; a second tiny launch bumps the counter.
+// flag = [this step flagged, flagged-step count, bad-wave events (monotonic), events seen so far]:
+// waves that see a non-finite gradient bump flag[2]; the single-thread kernel turns "flag[2] moved"
+// into flag[0] -- no per-step memset (a runtime fill node in the captured update) is needed
 __global__ __launch_bounds__(256) void nonfinite_kernel(const float* __restrict__ g, long n, int* flag) {
   int bad = 0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     bad |= !isfinite(g[i]);
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicAdd(flag + 2, 1);
 }
 // flagged steps counter; optionally advances the device Adam step counter unless the step is skipped
 __global__ void nonfinite_count_kernel(int* flag, long long* step) {
-  flag[1] += flag[0] ? 1 : 0;
-  if (step && !flag[0]) *step += 1;
+  const int bad = flag[2] != flag[3];
+  flag[3] = flag[2];
+  flag[0] = bad;
+  flag[1] += bad;
+  if (step && !bad) *step += 1;
 }
 
 void grad_guard(uintptr_t g, long n, uintptr_t flag, uintptr_t stream, uintptr_t step) {
   hipStream_t st = stream_of(stream);
-  GSC_HIP_CHECK(hipMemsetAsync(ptr<int>(flag), 0, sizeof(int), st));
   long grid = (n + 255) / 256;
   if (grid > 1024) grid = 1024;
   hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)(grid > 0 ? grid : 1)), dim3(256), 0, st, ptr<const float>(g), n,

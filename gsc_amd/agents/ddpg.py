@@ -410,10 +410,13 @@ class BatchedTrainer:
                 self.sim_stream = torch.cuda.ExternalStream(nat.create_cu_masked_stream(list(range(k))),
                                                             device=self.device)
                 # The learner stream is restricted to the complement, so no learner wave shares a SIMD
-                # with a simulator wave (the simulator is the critical path and the learner has slack:
-                # 103.6k vs 102.3k env-steps/s unmasked, 256 Abilene envs; when the learner was the longer
-                # chain the unmasked stream won, 57.2k vs 52.4k).  GSC_LEARNER_MASK=0 leaves it unmasked.
-                if os.environ.get("GSC_LEARNER_MASK", "1") == "0":
+                # with a simulator wave -- when the simulator is the critical path (small topologies whose
+                # envs pack three per CU: 103.6k vs 102.3k env-steps/s unmasked, 256 Abilene envs).  When
+                # the learner is the longer chain (large graphs) the whole device serves it (--preset
+                # syn50: 4.10k unmasked vs 3.56k masked).  GSC_LEARNER_MASK=0/1 forces either.
+                mask_env = os.environ.get("GSC_LEARNER_MASK", "auto")
+                small = (160 * 1024) // max(int(sim.ctx.lds_per_env), 1) >= 3
+                if mask_env == "0" or (mask_env == "auto" and not small):
                     self.learn_stream = torch.cuda.Stream(self.device)
                 else:
                     self.learn_stream = torch.cuda.ExternalStream(

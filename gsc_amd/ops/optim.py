@@ -111,9 +111,10 @@ class FusedAdamPolyak:
         # the step counter lives on the device so a captured HIP graph advances it on every replay
         self.step_t = torch.zeros((), dtype=torch.int64, device=flat.flat.device)
         self._host_step = 0
-        # non-finite gradient guard: [flag, skipped-count]; a flagged step leaves params/moments/target
+        # non-finite gradient guard: [flag, skipped-count, bad-wave events, events seen] (no per-step reset);
+        # a flagged step leaves params/moments/target
         # untouched (device-side decision, no host sync, works inside captured HIP graphs)
-        self.guard = torch.zeros(2, dtype=torch.int32, device=flat.flat.device)
+        self.guard = torch.zeros(4, dtype=torch.int32, device=flat.flat.device)
         self.guard_enabled = os.environ.get("GSC_GRAD_GUARD", "1") != "0"
 
     @property
@@ -144,6 +145,7 @@ class FusedAdamPolyak:
             stream = torch.cuda.current_stream(p.device).cuda_stream
             skip = 0
             if self.guard_enabled:
+                assert self.guard.numel() >= 4 and self.guard.dtype == torch.int32
                 # a skipped step does not advance Adam's bias-correction counter (done on the device)
                 nat.grad_guard(g.data_ptr(), self.fp.numel, self.guard.data_ptr(), stream, self.step_t.data_ptr())
                 skip = self.guard.data_ptr()

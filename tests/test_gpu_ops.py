@@ -133,7 +133,7 @@ def test_adam_polyak_matches_reference():
         opt.m, opt.v = m, v
         opt.step_t = torch.full((), step - 1, dtype=torch.int64, device=DEV)  # device step counter
         opt._host_step = step - 1
-        opt.guard, opt.guard_enabled = torch.zeros(2, dtype=torch.int32, device=DEV), True
+        opt.guard, opt.guard_enabled = torch.zeros(4, dtype=torch.int32, device=DEV), True
         opt.step()
         assert opt.step_count == step
     torch.testing.assert_close(p, p2, rtol=1e-6, atol=1e-6)
