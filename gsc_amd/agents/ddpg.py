@@ -430,17 +430,19 @@ class BatchedTrainer:
     @staticmethod
     def auto_sim_cus(sim) -> int:
         """CUs for one round of the simulator's env workgroups, at most 3 envs (waves) per CU so every
-        simulator wave keeps a SIMD to itself and the fourth SIMD takes learner waves, rounded up to
-        whole CU-mask groups of 8 (one CU per XCD) plus one group of slack, capped at half the device.
-        Measured on MI355X, 256 Abilene envs with the MFMA GNN learner (env-steps/s): 64 CUs (4 per
-        CU) 65.3k, 80 CUs 65.5k, 96 CUs 70.5k, 112 CUs 70.1k, 128 CUs 69.7k, 160 CUs 60.5k."""
+        simulator wave keeps a SIMD to itself, rounded up to whole XCDs (MI355X: 8 XCDs x 32 CUs, each
+        with its own L2; contiguous CU-mask bits fill one XCD after the other), capped at half the device.
+        Measured on MI355X, 256 Abilene envs (env-steps/s): 96 CUs (3 whole XCDs) 104.1k; 88 CUs 78.2k
+        and 104 CUs 71.1k (an XCD shared between simulator and learner); 128 CUs 93.0k (the learner
+        becomes the longer chain); 64 CUs 56.6k (4 envs per CU do not fit LDS: two rounds)."""
         nat = sim.native
         n = nat.cu_count()
+        xcd = max(n // 8, 8)
         lds = max(int(sim.ctx.lds_per_env), 1)
         per_cu = max(1, min(3, (160 * 1024) // lds))
         need = -(-sim.E // per_cu)
-        k = 8 * -(-need // 8) + (8 if per_cu > 1 else 0)
-        return int(min(max(k, 8), n // 2))
+        k = xcd * -(-need // xcd)
+        return int(min(max(k, xcd), n // 2))
 
     def _schedule_next(self) -> None:
         """Network scheduler: topology used by the episode that starts after this step."""
