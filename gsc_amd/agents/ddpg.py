@@ -102,6 +102,8 @@ class DDPGLearner:
         """Re-derive the bf16 shadows after parameters were written outside the optimizer."""
         for fp in (self.actor_flat, self.critic_flat, self.target_actor_flat, self.target_critic_flat):
             fp.refresh_shadow()
+        if self._act_native is not None:
+            self._act_native.rowtab_dirty = True
 
     @torch.no_grad()
     def act(self, obs: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:
@@ -224,9 +226,25 @@ class DDPGLearner:
                 self.critic_opt.step(grad_scale=inv_world)
                 nu.stage_actor_grad(b)
 
-            return [s1, lambda: nu.stage_actor_fwd(b), s3, lambda: self.actor_opt.step(grad_scale=inv_world)]
+            def s4():
+                self.actor_opt.step(grad_scale=inv_world)
+                self._after_actor_step()
+
+            return [s1, lambda: nu.stage_actor_fwd(b), s3, s4]
+
+        def s4_autograd():
+            self._stage_actor_opt(inv_world)
+            self._after_actor_step()
+
         return [lambda: self._stage_critic(b), lambda: self._stage_actor_fwd(b),
-                lambda: self._stage_actor_grad(b, inv_world), lambda: self._stage_actor_opt(inv_world)]
+                lambda: self._stage_actor_grad(b, inv_world), s4_autograd]
+
+    def _after_actor_step(self) -> None:
+        # the acting forward's per-topology mask fold follows the new actor weights (see NativeAct)
+        na = self._act_native
+        if na is not None:
+            na.refresh_rowtab()
+            na.rowtab_owned = True
 
     def _metrics_now(self) -> Dict[str, torch.Tensor]:
         if self.native_ok and self._native is not None:
@@ -308,6 +326,8 @@ class DDPGLearner:
         self.critic_opt.load_state_dict({k: (v.to(self.device) if torch.is_tensor(v) else v)
                                          for k, v in sd["critic_opt"].items()})
         self.updates = int(sd.get("updates", 0))
+        if self._act_native is not None:  # weights written outside the optimizer
+            self._act_native.rowtab_dirty = True
 
 
 @dataclass

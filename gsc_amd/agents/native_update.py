@@ -380,6 +380,7 @@ class NativeAct:
         self.out = torch.zeros(E, self.A, device=dev)
         self.topo32 = torch.zeros(E, dtype=torch.int32, device=dev)
         self._topo_ref, self._topo_ver = None, -1
+        self.rowtab_owned, self.rowtab_dirty = False, True
         self.lw = None
         if not gnn_use_fused(L.actor.embedder, L.graphs, self.P, self.Fin):
             from gsc_amd.ops.gnn_lw import LayerwiseGAT
@@ -389,6 +390,17 @@ class NativeAct:
     @staticmethod
     def supported(learner) -> bool:
         return bool(learner.native_ok and len(learner.actor.mlp.layers) >= 2)
+
+    def refresh_rowtab(self) -> None:
+        """mask[t] @ W_m^T of the first layer for every topology (current stream).  The learner calls it
+        right after each actor optimizer step (inside the captured update), so the acting chain -- the
+        simulator's critical path -- does not recompute it every step (``rowtab_owned``); weight writes
+        outside the optimizer (checkpoint load, shadow refresh) mark it dirty."""
+        n, s = self.net, torch.cuda.current_stream(self.L.device).cuda_stream
+        w = n.w16(0)
+        self.nat.rowdot(self.masks.data_ptr(), self.masks.stride(0), self.T, w.data_ptr() + 2 * self.H, w.stride(0),
+                        n.width(0), self.A, self.rowtab.data_ptr(), self.rowtab.stride(0), s)
+        self.rowtab_dirty = False
 
     def __call__(self, obs: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:
         n, s = self.net, torch.cuda.current_stream(self.L.device).cuda_stream
@@ -404,8 +416,8 @@ class NativeAct:
             self.nat.gnn_forward(self.tables, n.emb_ptr(), obs.data_ptr(), self.topo32.data_ptr(), self.emb.data_ptr(),
                                  self.E, self.P, self.Fin, self.H, self.layer_of, s, 0)
         w = n.w16(0)
-        self.nat.rowdot(self.masks.data_ptr(), self.masks.stride(0), self.T, w.data_ptr() + 2 * self.H, w.stride(0),
-                        n.width(0), self.A, self.rowtab.data_ptr(), self.rowtab.stride(0), s)
+        if not self.rowtab_owned or self.rowtab_dirty:
+            self.refresh_rowtab()
         gemm(self.emb, w[:, :self.H], "nt", out16=self.hid[0], bias=n.b32(0), rowtab=self.rowtab, topo=self.topo32,
              relu=True)
         for i in range(1, n.nh):
