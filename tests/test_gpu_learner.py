@@ -133,3 +133,25 @@ def test_native_act_matches_fp32_module(T):
     # masked entries (padding nodes / other topologies' rows) are exactly zero
     m = ref.masks[b.topo]
     assert torch.equal(got * (1 - m), torch.zeros_like(got))
+
+
+def test_native_act_follows_graphed_updates():
+    """The acting forward's folded mask block is refreshed by the (captured) update after each actor
+    step: after several graphed updates the native act still matches the fp32 actor module on the
+    updated weights (the module's parameters alias the learner's flat buffer)."""
+    cfg = _cfg()
+    _, gpu = _learners(cfg, 2)
+    E = 300
+    gpu.enable_native_act(E)
+    obs = _batch(E, 2, "cuda", seed=5)
+    gpu.act(obs.obs.contiguous(), obs.topo)            # first act computes the fold itself
+    b = _batch(1024, 2, "cuda", seed=7)
+    for _ in range(4):                                 # 1 eager warm-up, capture, replays
+        gpu.update_graphed(b, warmup=1)
+    torch.cuda.synchronize()
+    assert gpu._act_native.rowtab_owned
+    got = gpu.act(obs.obs.contiguous(), obs.topo)
+    with torch.no_grad():
+        want = gpu.actor(obs.obs, obs.topo, gpu.graphs, gpu.masks).float()
+    err = ((got - want).norm() / want.norm()).item()
+    assert err < 0.02, err
