@@ -382,7 +382,8 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     }
     it += __builtin_amdgcn_readfirstlane(n_disp) - 1;
     // (measured: inserting a one-event inbox's event from registers instead of re-reading it here
-    // duplicated the insert code and was slower, 97.3k vs 105.2k env-steps/s)
+    // was slower both with a second insert site, 97.3k vs 105.2k env-steps/s, and through the one
+    // insert site, 101.3k vs 104.5k: the event kept live across the chain costs more than the read)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
