@@ -120,8 +120,11 @@ class DDPGLearner:
         if NativeAct.supported(self):
             self._act_native = NativeAct(self, E)
 
-    def _allreduce(self, flat: FlatParams):
-        return allreduce_sum_(flat.grad, async_op=True) if self.dist.enabled else None
+    def _allreduce(self, flat: FlatParams, lo: int = 0, hi: Optional[int] = None):
+        if not self.dist.enabled:
+            return None
+        g = flat.grad if (lo == 0 and hi is None) else flat.grad[lo:hi]
+        return allreduce_sum_(g, async_op=True)
 
     # -- update stages of the autograd path (CPU; GPU reference with GSC_NATIVE_LEARNER=0) -------
     def _target(self, b: Batch) -> torch.Tensor:
@@ -192,26 +195,38 @@ class DDPGLearner:
 
         Data parallel: the critic-gradient all-reduce is issued as soon as the critic gradients exist
         and runs on the communicator's stream while the actor's embedding + hidden layers (which do
-        not read critic weights) run on the compute stream; the critic step waits for it."""
-        s1, s2, s3, s4 = self._stages(b, 1.0 / self.dist.world_size)
-        s1()
-        h_c = self._allreduce(self.critic_flat)
-        s2()
-        if h_c is not None:
-            h_c.wait()
-        s3()
-        h_a = self._allreduce(self.actor_flat)
-        if h_a is not None:
-            h_a.wait()
-        s4()
+        not read critic weights) run on the compute stream; the critic step waits for it.  The actor's
+        MLP gradients are all-reduced while the actor embedder's backward runs; only the embedder's
+        (small) gradient all-reduce is exposed before the actor step."""
+        stages, split = self._stages(b, 1.0 / self.dist.world_size)
+        self._run_stages([lambda f=f: f() for f in stages], split)
         self.updates += 1
         self.last = self._metrics_now()
 
+    def _run_stages(self, run, split: int) -> None:
+        """``run``: five callables (critic grads | actor fwd | critic step + actor MLP grads | actor
+        embedder bwd | actor step) with the gradient all-reduces issued between them."""
+        r1, r2, r3, r3b, r4 = run
+        r1()
+        h_c = self._allreduce(self.critic_flat)
+        r2()
+        if h_c is not None:
+            h_c.wait()
+        r3()
+        h_am = self._allreduce(self.actor_flat, split, None)
+        r3b()
+        h_ag = self._allreduce(self.actor_flat, 0, split) if split > 0 else None
+        for h in (h_am, h_ag):
+            if h is not None:
+                h.wait()
+        r4()
+
     # -- HIP-graph replay ----------------------------------------------------------------------
     def _stages(self, b: Batch, inv_world: float):
-        """The update as four stages: critic gradients | actor forward | critic step + actor
-        gradients | actor step.  The critic all-reduce runs between stages 1 and 3, concurrently
-        with stage 2; the actor all-reduce between stages 3 and 4."""
+        """The update as five stages: critic gradients | actor forward | critic step + actor MLP
+        gradients | actor embedder backward | actor step, and the split index of the actor's flat
+        gradient (embedder first: ``grad[:split]`` is written by stage 4 only).  The critic all-reduce
+        runs concurrently with stage 2, the actor MLP all-reduce with stage 4."""
         if self.native_ok:
             nu = self.native_update(b.obs.shape[0])
 
@@ -230,14 +245,14 @@ class DDPGLearner:
                 self.actor_opt.step(grad_scale=inv_world)
                 self._after_actor_step()
 
-            return [s1, lambda: nu.stage_actor_fwd(b), s3, s4]
+            return [s1, lambda: nu.stage_actor_fwd(b), s3, lambda: nu.stage_actor_gnn_bwd(b), s4], nu.ne
 
         def s4_autograd():
             self._stage_actor_opt(inv_world)
             self._after_actor_step()
 
         return [lambda: self._stage_critic(b), lambda: self._stage_actor_fwd(b),
-                lambda: self._stage_actor_grad(b, inv_world), s4_autograd]
+                lambda: self._stage_actor_grad(b, inv_world), lambda: None, s4_autograd], 0
 
     def _after_actor_step(self) -> None:
         # the acting forward's per-topology mask fold follows the new actor weights (see NativeAct)
@@ -253,9 +268,10 @@ class DDPGLearner:
 
     def update_graphed(self, b: Batch, warmup: int = 2, pre=None, topo_ready: bool = False) -> None:
         """Same update, replayed from captured HIP graphs (``b`` must be the same static buffers on
-        every call).  One process: one graph for the whole update.  Data parallel: four graphs with
+        every call).  One process: one graph for the whole update.  Data parallel: five graphs with
         the gradient all-reduces issued eagerly between them (collectives stay out of capture); the
-        critic all-reduce overlaps the actor-forward graph.  The first ``warmup`` calls run eagerly
+        critic all-reduce overlaps the actor-forward graph, the actor-MLP all-reduce the actor
+        embedder-backward graph.  The first ``warmup`` calls run eagerly
         (they are real updates) on a side stream.  ``pre`` (e.g. the replay sampler filling ``b``)
         runs first and is captured with the update; ``topo_ready``: ``pre`` also fills
         :meth:`topo32_buffer`."""
@@ -276,30 +292,25 @@ class DDPGLearner:
         if len(self._graphs) == 1:
             self._graphs[0].replay()
         else:
-            g1, g2, g3, g4 = self._graphs
-            g1.replay()
-            h = self._allreduce(self.critic_flat)
-            g2.replay()
-            if h is not None:
-                h.wait()
-            g3.replay()
-            h = self._allreduce(self.actor_flat)
-            if h is not None:
-                h.wait()
-            g4.replay()
+            self._run_stages([g.replay if g is not None else (lambda: None) for g in self._graphs], self._split)
         self.updates += 1
         self.last = self._metrics_now()
 
     def _capture(self, b: Batch, inv_world: float, pre=None) -> None:
         # thread-local capture: the RCCL watchdog thread keeps querying its events while we capture
         pool = torch.cuda.graph_pool_handle()
-        stages = self._stages(b, inv_world)
+        stages, self._split = self._stages(b, inv_world)
         if pre is not None:
             s1 = stages[0]
             stages[0] = lambda: (pre(), s1())
         graphs = []
+        # one process: one graph; data parallel: one graph per stage (collectives between them, eager);
+        # a stage that launches nothing (autograd path's embedder stage) gets no graph
         groups = [stages] if self.dist.world_size == 1 else [[f] for f in stages]
-        for grp in groups:
+        for k, grp in enumerate(groups):
+            if self.dist.world_size > 1 and not self.native_ok and k == 3:
+                graphs.append(None)
+                continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
                 for fn in grp:

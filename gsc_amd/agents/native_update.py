@@ -349,7 +349,11 @@ class NativeDDPGUpdate:
             gemm(self.dact, a.w16(last), "nn", out16=dz, gate=hl)
         dh0a = self._hidden_bwd(a, self.hid_a, dz, grads=True)
         self._first_bwd(a, self.emb["a"], dh0a)
-        self._gnn_bwd(a, b.obs, self.demb, self.blob["a"], key="a")
+
+    def stage_actor_gnn_bwd(self, b) -> None:
+        """The actor embedder's backward: writes only the first ``ne`` entries of ``actor_flat.grad``
+        (the MLP part written by :meth:`stage_actor_grad` can be all-reduced meanwhile)."""
+        self._gnn_bwd(self.actor, b.obs, self.demb, self.blob["a"], key="a")
 
     def last_metrics(self) -> dict:
         m = self.metrics

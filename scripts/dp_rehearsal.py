@@ -83,7 +83,7 @@ def main():
             torch.cuda.synchronize()
             grads = [L.critic_flat.grad.clone(), L.actor_flat.grad.clone()]   # all-reduced sums
     torch.cuda.synchronize()
-    res = {"world": W, "backend": info.backend, "graphed": L._graphs is not None and len(L._graphs) == 4,
+    res = {"world": W, "backend": info.backend, "graphed": L._graphs is not None and len(L._graphs) == 5,
            "replicas_bitwise": bitwise_same(flats(L), W)}
     if r == 0:
         ref = DDPGLearner(cfg, 3, 1728, gs, 1, 3, dev, None, seed=3)
