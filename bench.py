@@ -124,12 +124,19 @@ def main():
     diag = os.environ.get("GSC_SIM_PROFILE") == "1" and device.type == "cuda"
     if diag:
         sim.enable_profiling()
+    # GSC_PROF_WINDOW=1: one roctx range around exactly the timed steps, so a
+    # `rocprofv3 --kernel-trace --marker-trace` table can be cut to the timed region (scripts/prof_summary.py)
+    window = os.environ.get("GSC_PROF_WINDOW") == "1" and device.type == "cuda"
     barrier()
     sync()
+    if window:
+        torch.cuda.nvtx.range_push("bench_timed")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         trainer.step()
     sync()
+    if window:
+        torch.cuda.nvtx.range_pop()
     barrier()
     dt = time.perf_counter() - t0
     sim.check_flags()
@@ -178,6 +185,8 @@ def main():
                      f"{', '.join(os.path.basename(n) for n in networks)}, {os.path.basename(service)}), "
                      "random-init weights"),
             "success_ratio": round(m["success_ratio"], 4),
+            **({"diagnostic": "GSC_SIM_PROFILE=1: cycle-counting simulator variant, not a benchmark number"}
+               if diag else {}),
             "config": {
                 "model": pre["model"],
                 "global_batch": trainer.batch_size * info.world_size,

@@ -346,28 +346,44 @@ class SimpleDDPG(RLSPAgent):
     def save_checkpoint(self, path: str) -> None:
         """Rank 0 writes ``path`` (learner + its trainer state).  Data parallel: every other rank writes
         its own simulator states / replay ring / RNG state to ``ckpt.rank_path(path, r)`` -- the shards
-        are rank-seeded and must stay disjoint after a resume."""
+        are rank-seeded and must stay disjoint after a resume.  Every file of one save carries the same
+        stamp (global step, episode, world size), and the ranks meet at a barrier once all are written,
+        so a save interrupted between two ranks' writes is detected on resume."""
         sd = self.state_dict()
         meta = {"experiment_id": self.agent_helper.experiment_id, "time": time.time(), "rank": self.dist.rank,
-                "world_size": self.dist.world_size}
+                "world_size": self.dist.world_size, "stamp": ckpt.save_stamp(sd, self.dist.world_size)}
         if self._per_rank() and self.dist.rank > 0:
             sd["trainer"].pop("learner", None)       # replicas are identical: rank 0's file holds the learner
             ckpt.save_checkpoint(ckpt.rank_path(path, self.dist.rank), sd, meta=meta, rank=0)
         else:
             ckpt.save_checkpoint(path, sd, meta=meta, rank=self.dist.rank)
+        if self._per_rank():
+            from gsc_amd.parallel.dist import barrier
+            barrier()
 
     def load_checkpoint(self, path: str) -> None:
-        sd = ckpt.load_checkpoint(path)["state"]
+        d0 = ckpt.load_checkpoint(path)
+        sd = d0["state"]
         if self._per_rank() and self.dist.rank > 0:
             rp = ckpt.rank_path(path, self.dist.rank)
+            stamp = ckpt.save_stamp(sd, self.dist.world_size)
+            why = "missing"
             if os.path.exists(rp):
-                local = ckpt.load_checkpoint(rp)["state"]
-                local["trainer"]["learner"] = sd["trainer"]["learner"]
-                self.load_state_dict(local)
-                return
-            # no per-rank state (e.g. a checkpoint written by fewer ranks): take rank 0's learner and
-            # re-seed this rank's simulator streams / replay sampler so the shards stay disjoint
-            logger.warning(f"{rp} missing: rank {self.dist.rank} re-seeds its simulator and replay sampler")
+                dr = ckpt.load_checkpoint(rp)
+                got = dr.get("meta", {}).get("stamp")
+                if got == stamp and d0.get("meta", {}).get("stamp") == stamp:
+                    local = dr["state"]
+                    local["trainer"]["learner"] = sd["trainer"]["learner"]
+                    self.load_state_dict(local)
+                    return
+                why = f"from another save (stamp {got} != rank 0's {stamp})"
+            # no matching per-rank state (fewer ranks, or a save interrupted between two ranks' writes):
+            # take rank 0's learner, drop rank 0's replay ring (this rank's shard must not start as a copy
+            # of rank 0's transitions: it refills with a full warm-up) and re-seed this rank's simulator
+            # streams / replay sampler so the shards stay disjoint
+            logger.warning(f"{rp} {why}: rank {self.dist.rank} re-seeds its simulator and replay sampler and "
+                           "refills its replay ring")
+            sd["trainer"].pop("replay", None)
             self.load_state_dict(sd)
             self.trainer.reseed(int(self.agent_helper.seed) * 1000 + self.dist.rank)
             return

@@ -26,7 +26,10 @@ from typing import Optional
 import torch
 
 ACTOR_FORMAT = "gsc_amd.actor/1"
-CHECKPOINT_FORMAT = "gsc_amd.checkpoint/1"
+# /2: MLP matrices of the flat parameter buffers padded to 8 elements, trainer "rng" = the 5-int64
+# device sampler state, per-rank files stamped with the save's (global_step, episode, world_size)
+CHECKPOINT_FORMAT = "gsc_amd.checkpoint/2"
+_OLD_FORMATS = {"gsc_amd.checkpoint/1": "flat parameter layout and sampler state changed in /2"}
 
 
 def atomic_save(obj, path: str) -> None:
@@ -82,9 +85,19 @@ def to_cpu(x):
 
 def load_checkpoint(path: str) -> dict:
     d = torch.load(path, map_location="cpu", weights_only=True)
-    if not isinstance(d, dict) or d.get("format") != CHECKPOINT_FORMAT:
+    fmt = d.get("format") if isinstance(d, dict) else None
+    if fmt in _OLD_FORMATS:
+        raise ValueError(f"{path}: checkpoint format {fmt} is no longer readable ({_OLD_FORMATS[fmt]}); "
+                         f"this build reads {CHECKPOINT_FORMAT}")
+    if fmt != CHECKPOINT_FORMAT:
         raise ValueError(f"{path}: not a {CHECKPOINT_FORMAT} file")
     return d
+
+
+def save_stamp(state: dict, world_size: int) -> dict:
+    """Identity of one data-parallel save: every rank's file of the same save carries the same stamp."""
+    return {"global_step": int(state["global_step"]), "episode": int(state["episode"]),
+            "world_size": int(world_size)}
 
 
 def save_agent_helper(path: str, helper) -> None:

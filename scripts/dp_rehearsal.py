@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Data-parallel rehearsal on ONE GPU: N ranks (gloo collectives, GSC_DIST_BACKEND=gloo) through the
-GPU learner's HIP-graph path (native kernels, 4 captured stages with the critic/actor gradient
+GPU learner's HIP-graph path (native kernels, 5 captured stages with the critic/actor gradient
 all-reduces between them) and through the batched trainer (device simulator + learner).
 
 Run:  GSC_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
@@ -8,8 +8,11 @@ Run:  GSC_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-p
 
 Rank 0 prints one JSON line:
   replicas_bitwise      every rank's four flat parameter buffers are bit-identical (all_gather + torch.equal)
-  grad_vs_single        max relative error of the first update's all-reduced gradients against one
-                        process updating on the concatenated batch (same kernels, fp32 accumulation order)
+  grad_vs_single        max relative error of the all-reduced critic / actor gradients of every update
+                        against one process updating on the concatenated batch (same kernels, fp32
+                        accumulation order); update 0 is the eager warm-up
+  grad_vs_single_graphed  the same over the captured updates only (k >= 1: the five-stage graph path,
+                        actor-MLP all-reduce overlapping the embedder backward)
   param_mismatch_frac   fraction of parameters differing by > 1e-4 from that single process after 3 updates
   trainer_replicas_bitwise  same check after 6 batched-trainer steps (per-rank envs, shared learner)
 """
@@ -74,28 +77,28 @@ def main():
     L = DDPGLearner(cfg, 3, 1728, gs, 1, 3, dev, info, seed=3 if r == 0 else 100 + r)
     assert L.native_ok
     static = Batch(*(torch.empty_like(t[:Bp]) for t in full[0]))
-    grads = None
+    grads = []
     for k, b in enumerate(full):
         for d, s in zip(static, b):
             d.copy_(s[r * Bp:(r + 1) * Bp])
         L.update_graphed(static, warmup=1)
-        if k == 0:
-            torch.cuda.synchronize()
-            grads = [L.critic_flat.grad.clone(), L.actor_flat.grad.clone()]   # all-reduced sums
+        torch.cuda.synchronize()
+        grads.append([L.critic_flat.grad.clone(), L.actor_flat.grad.clone()])   # all-reduced sums
     torch.cuda.synchronize()
     res = {"world": W, "backend": info.backend, "graphed": L._graphs is not None and len(L._graphs) == 5,
            "replicas_bitwise": bitwise_same(flats(L), W)}
     if r == 0:
         ref = DDPGLearner(cfg, 3, 1728, gs, 1, 3, dev, None, seed=3)
         # single process: the same updates on the concatenated batches (world_size 1 inside the learner)
+        per_k = []
         for k, b in enumerate(full):
             ref.update(b)
-            if k == 0:
-                torch.cuda.synchronize()
-                # DP buffers hold the sum of per-rank means = W x the single-process mean gradient
-                errs = [((g / W - rg).norm() / rg.norm()).item()
-                        for g, rg in zip(grads, [ref.critic_flat.grad, ref.actor_flat.grad])]
-                res["grad_vs_single"] = max(errs)
+            torch.cuda.synchronize()
+            # DP buffers hold the sum of per-rank means = W x the single-process mean gradient
+            per_k.append(max(((g / W - rg).norm() / rg.norm()).item()
+                             for g, rg in zip(grads[k], [ref.critic_flat.grad, ref.actor_flat.grad])))
+        res["grad_vs_single"] = max(per_k)
+        res["grad_vs_single_graphed"] = max(per_k[1:])
         torch.cuda.synchronize()
         d = torch.cat([(a - b).abs().view(-1) for a, b in zip(flats(L), flats(ref))])
         res["param_mismatch_frac"] = float((d > 1e-4).float().mean())

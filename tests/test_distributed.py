@@ -126,7 +126,7 @@ def test_dp_batched_trainer_replicas_identical():
     assert float(r[0]["succ"]) == float(r[1]["succ"]) > 0
 
 
-def _resume_worker(rank, port, out_dir):
+def _resume_worker(rank, port, out_dir, stale=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -155,6 +155,22 @@ def _resume_worker(rank, port, out_dir):
     path = os.path.join(out_dir, "ck.pt")
     a.save_checkpoint(path)
     torch.distributed.barrier()
+    if stale:
+        # a save interrupted between the ranks' writes: rank 1's file is from the previous save
+        import shutil
+        if rank == 1:
+            shutil.copy(os.path.join(out_dir, "ck.rank1.pt"), os.path.join(out_dir, "old.pt"))
+        a.train(1)
+        a.save_checkpoint(path)
+        if rank == 1:
+            shutil.copy(os.path.join(out_dir, "old.pt"), os.path.join(out_dir, "ck.rank1.pt"))
+        torch.distributed.barrier()
+        b = make()
+        b.load_checkpoint(path)
+        torch.save({"replay_len": len(b.trainer.replay), "step": b.global_step,
+                    "learning_starts": b.trainer.learning_starts}, os.path.join(out_dir, f"res{rank}.pt"))
+        shutdown()
+        return
     a.train(1)
     b = make()
     b.load_checkpoint(path)
@@ -181,3 +197,23 @@ def test_dp_resume_keeps_rank_local_state():
     assert not torch.equal(r[0]["b_states"], r[1]["b_states"])
     assert not torch.equal(r[0]["b_rng"], r[1]["b_rng"])
     assert torch.equal(r[0]["b_actor"], r[1]["b_actor"])
+
+
+def test_dp_resume_rejects_stale_rank_file():
+    """A rank file from another save (stamp mismatch) is not merged with rank 0's learner: that rank
+    re-seeds and refills its replay ring from empty (no copy of rank 0's transitions)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_resume_worker, args=(_free_port(), d, True), nprocs=WORLD, join=True, start_method="spawn")
+        r = [torch.load(os.path.join(d, f"res{i}.pt"), weights_only=True) for i in range(WORLD)]
+    assert r[0]["step"] == r[1]["step"]
+    assert r[0]["replay_len"] > 0
+    assert r[1]["replay_len"] == 0
+    assert r[1]["learning_starts"] > r[1]["step"]
+
+
+def test_checkpoint_format_1_rejected(tmp_path):
+    from gsc_amd.utils import checkpoint as ck
+    p = str(tmp_path / "old.pt")
+    torch.save({"format": "gsc_amd.checkpoint/1", "meta": {}, "state": {}}, p)
+    with pytest.raises(ValueError, match="no longer readable"):
+        ck.load_checkpoint(p)

@@ -33,6 +33,6 @@ def test_two_ranks_one_gpu_graphed_dp():
     print(res)
     assert res["world"] == 2 and res["backend"] == "gloo" and res["graphed"]
     assert res["replicas_bitwise"] and res["trainer_replicas_bitwise"]
-    assert res["grad_vs_single"] < 1e-3, res
+    assert res["grad_vs_single"] < 1e-3 and res["grad_vs_single_graphed"] < 1e-3, res
     assert res["param_mismatch_frac"] < 1e-3, res
     assert res["trainer_graphed"] and res["trainer_updates"] >= 4 and res["envs_differ"]
