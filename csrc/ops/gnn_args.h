@@ -1,5 +1,4 @@
-// Shared argument block and per-wave topology helpers of the fused GATv2 kernels
-// (channel-lane gnn_cl.hip, MFMA gnn_mf.hip; dispatched from gnn.hip).
+// Shared argument block of the fused MFMA GATv2 kernels (gnn_mf.hip, gnn_mt.hip; dispatched from gnn.hip).
 #pragma once
 #include "../common.h"
 
@@ -8,7 +7,7 @@ namespace gsc {
 constexpr int kClMaxLayers = 16;
 constexpr float kClSlope = 0.2f;
 
-// Optional per-phase cycle counters of the backward (s_memtime; gnn_cl_set_profile).
+// Optional per-phase cycle counters (s_memtime); compiled out unless enabled at the call site.
 struct ClClock {
   unsigned long long last, acc[12];
   bool on;
@@ -46,7 +45,7 @@ struct ClArgs {
   int B, P, Fin, H, L, M, NM, n_params, n_blocks, waves;
   int layer_of[kClMaxLayers];
   unsigned long long* prof;  // 12 phase counters or null
-  const void* s_dst;         // MFMA backward: bf16 [T, 32, MP] one-hot target / source of each message
+  const void* s_dst;         // MFMA backward: bf16 [T, 32 * tiles, MP] one-hot target / source of each message
   const void* s_src;
   int MP;                    // messages padded to a multiple of 16
   void* blob;                // MFMA path: per-graph forward state saved for the backward (or null)
@@ -62,43 +61,4 @@ __host__ __device__ __forceinline__ int cl_block_size(int Fi, int H) { return 2 
 __host__ __device__ __forceinline__ int cl_block_offset(int b, int Fin, int H) {
   return b == 0 ? 0 : cl_block_size(Fin, H) + (b - 1) * cl_block_size(H, H);
 }
-struct ClTopo {
-  int *isrc, *idst, *iptr, *oq, *odst, *optr;
-  float* deg;
-  int n, m, t;
-};
-
-__host__ __device__ __forceinline__ int cl_topo_ints(const ClArgs& a) { return ((4 * a.M + 2 * (a.P + 1) + a.P) + 3) & ~3; }
-
-__device__ __forceinline__ void cl_bind_topo(ClTopo& T, int* base, const ClArgs& a) {
-  T.isrc = base;
-  T.idst = T.isrc + a.M;
-  T.oq = T.idst + a.M;
-  T.odst = T.oq + a.M;
-  T.iptr = T.odst + a.M;
-  T.optr = T.iptr + a.P + 1;
-  T.deg = reinterpret_cast<float*>(T.optr + a.P + 1);
-  T.t = -1;
-}
-
-__device__ __forceinline__ void cl_load_topo(ClTopo& T, const ClArgs& a, int t, int lane) {
-  T.n = a.nnodes[t];
-  T.m = a.nmsgs[t];
-  if (T.t == t) return;
-  T.t = t;
-  const long mo = (long)t * a.M, po = (long)t * (a.P + 1);
-  for (int i = lane; i < a.M; i += 64) {
-    T.isrc[i] = a.in_src[mo + i];
-    T.idst[i] = a.in_dst[mo + i];
-    T.oq[i] = a.out_q[mo + i];
-    T.odst[i] = a.out_dst[mo + i];
-  }
-  for (int i = lane; i <= a.P; i += 64) {
-    T.iptr[i] = a.in_ptr[po + i];
-    T.optr[i] = a.out_ptr[po + i];
-  }
-  for (int i = lane; i < a.P; i += 64) T.deg[i] = a.deg[(long)t * a.P + i];
-  cl_wave_sync();
-}
-
 }  // namespace gsc

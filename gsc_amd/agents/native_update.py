@@ -139,19 +139,16 @@ class NativeDDPGUpdate:
         self.Fin = Fin
         ne = sum(p.numel() for p in L.actor.embedder.flat_parameters())
         self.ne = ne
-        # large graphs (beyond LDS, e.g. 200 nodes, or >= GSC_GNN_LW_MIN_NODES): layer-wise GNN kernels, one
+        # shapes beyond the fused MFMA kernels (e.g. 200-node graphs): layer-wise GNN kernels, one
         # workspace per saved forward ("a", "c") plus one for forwards without a backward
         self.layerwise = not gnn_use_fused(L.actor.embedder, L.graphs, self.P, Fin)
         if self.layerwise:
             from gsc_amd.ops.gnn_lw import LayerwiseGAT
             self.lwo = {k: LayerwiseGAT(self.tables, B, self.P, Fin, H, self.layer_of, dev) for k in ("a", "c", "-")}
             self.blob = {"a": None, "c": None}
-        elif os.environ.get("GSC_GNN_SAVE", "1") == "0":
-            # GSC_GNN_SAVE=0: the backward recomputes the forward in LDS.  Default: the forward saves its
-            # per-layer images for the backward (measured on MI355X, 256 Abilene envs, after the backward
-            # stopped spilling: 101.9k vs 101.2k env-steps/s; recompute had won before, 88.2k vs 86.7k)
-            self.blob = {"a": None, "c": None}
         else:
+            # the grad-requiring forwards save their per-layer images for the backward (measured on
+            # MI355X, 256 Abilene envs: 101.9k vs 101.2k env-steps/s against recomputing them in LDS)
             sb = nat.gnn_saved_bytes(self.tables, self.P, Fin, H, self.layer_of)
             self.blob = {k: torch.empty(B * sb, device=dev, dtype=torch.uint8) for k in ("a", "c")}
         self.gnn_rows = 1024

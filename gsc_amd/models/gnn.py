@@ -124,7 +124,7 @@ class GNNEmbedder(nn.Module):
             from gsc_amd.ops.gnn import gnn_embed, gnn_embed_layerwise, gnn_use_fused
             if gnn_use_fused(self, graphs, x.shape[1], x.shape[2]):
                 return gnn_embed(self, x, topo, graphs)
-            # large graphs (beyond LDS, or >= GSC_GNN_LW_MIN_NODES nodes): layer-wise native kernels
+            # shapes beyond the fused MFMA kernels (e.g. 200-node graphs): layer-wise native kernels
             return gnn_embed_layerwise(self, x, topo, graphs)
         return self.forward_reference(x, topo, graphs)
 

@@ -70,7 +70,7 @@ class GraphSet:
                 lst[i, :len(order)] = order
                 cnt = np.bincount(key, minlength=self.n_pad)
                 ptr[i, 1:] = np.cumsum(cnt)
-        # CSR-ordered message arrays (channel-lane kernels): messages sorted by target node keep
+        # CSR-ordered message arrays (fused + layer-wise kernels): messages sorted by target node keep
         # their source/target directly, and the source-sorted view stores positions in that order.
         in_src = np.zeros((T, self.M), np.int32)
         in_dst = np.zeros((T, self.M), np.int32)
@@ -93,13 +93,15 @@ class GraphSet:
         self.out_ptr = torch.from_numpy(out_ptr).to(dev)
         self.out_msg = torch.from_numpy(out_msg).to(dev)
         self.n_nodes_i32 = self.n_nodes.to(torch.int32)
-        # one-hot message matrices of the MFMA backward (csrc/ops/gnn_mf.hip), bf16 [T, 32, MP]:
-        # s_dst[t, i, q] = 1 if message q (target-sorted order) ends at node i, s_src likewise for
-        # its source; dX_r = s_dst G and dX_l = s_src G are then matrix-core products
+        # one-hot message matrices of the MFMA backward (csrc/ops/gnn_mf.hip, gnn_mt.hip), bf16
+        # [T, 32 * tiles, MP] (one 32-node tile up to 32 nodes, two up to 64): s_dst[t, i, q] = 1 if
+        # message q (target-sorted order) ends at node i, s_src likewise for its source; dX_r = s_dst G
+        # and dX_l = s_src G are then matrix-core products
         self.mf_mp = ((self.M + 15) // 16) * 16
-        s_dst = np.zeros((T, 32, self.mf_mp), np.float32)
-        s_src = np.zeros((T, 32, self.mf_mp), np.float32)
-        if self.max_nodes <= 32:
+        rows = 32 * max(1, -(-self.max_nodes // 32)) if self.max_nodes <= 64 else 32
+        s_dst = np.zeros((T, rows, self.mf_mp), np.float32)
+        s_src = np.zeros((T, rows, self.mf_mp), np.float32)
+        if self.max_nodes <= 64:
             for i, (s, _) in enumerate(msgs):
                 q = np.arange(len(s))
                 s_dst[i, in_dst[i, :len(s)], q] = 1.0

@@ -1,9 +1,9 @@
-"""Autograd wrappers around the native GATv2 embedder kernels: the fused per-graph kernels
-(``csrc/ops/gnn.hip`` / ``gnn_mf.hip``) and, for graphs whose working set exceeds LDS, the
+"""Autograd wrappers around the native GATv2 embedder kernels: the fused per-graph MFMA kernels
+(``csrc/ops/gnn_mf.hip`` for <= 32 nodes, ``gnn_mt.hip`` for 33..64 nodes, dispatched by ``gnn.hip``)
+and, for every other shape (200-node topologies, wider embedders, other layer counts), the
 layer-wise kernels (``gsc_amd/ops/gnn_lw.py``)."""
 from __future__ import annotations
 
-import os
 from typing import List
 
 import torch
@@ -49,8 +49,6 @@ def _flat(params: List[torch.Tensor]) -> torch.Tensor:
 
 
 _PARTIALS = {}
-# GSC_GNN_SAVE=0: the backward recomputes the forward instead of loading its saved state
-_NO_SAVE = os.environ.get("GSC_GNN_SAVE", "1") == "0"
 
 
 class _GnnEmbed(torch.autograd.Function):
@@ -65,7 +63,7 @@ class _GnnEmbed(torch.autograd.Function):
         emb = torch.empty(B, H, device=x.device, dtype=torch.float32)
         # grad-requiring forward: save the per-layer state for the backward (MFMA path) instead of
         # having it recompute the forward
-        nbytes = 0 if _NO_SAVE else nat.gnn_saved_bytes(_tables(graphs), P, Fin, H, layer_of) if grad_mode and any(ctx.needs_input_grad[4:]) \
+        nbytes = nat.gnn_saved_bytes(_tables(graphs), P, Fin, H, layer_of) if grad_mode and any(ctx.needs_input_grad[4:]) \
             else 0
         blob = torch.empty(B * nbytes if B > 0 else 0, device=x.device, dtype=torch.uint8)
         if B > 0:
@@ -103,24 +101,21 @@ class _GnnEmbed(torch.autograd.Function):
         return (None, None, None, None, *out)
 
 
-# graphs with at least this many nodes take the layer-wise kernels even when the fused per-graph
-# kernels would fit (GSC_GNN_LW_MIN_NODES; syn50 measured equal: 3981 vs 3977 env-steps/s, so off by default)
-_LW_MIN_NODES = int(os.environ.get("GSC_GNN_LW_MIN_NODES", "100000"))
-
-
 def gnn_fits(embedder, graphs, P: int, Fin: int) -> bool:
-    """Fused kernels handle these graph sizes (per-graph working set fits one CU's LDS)."""
+    """The fused MFMA kernels cover this shape (<= 64 nodes, H <= 32, F_in <= 16, encoder + one
+    shared process block, unique messages; per-graph working set within one CU's LDS)."""
     key = ("_gnn_fits", embedder.hidden_dim, tuple(_layer_of(embedder)), P, Fin)
     cache = graphs.__dict__.setdefault("_fits_cache", {})
     if key not in cache:
         cache[key] = bool(load_native().gnn_fused_fits(int(graphs.M), int(graphs.max_nodes), int(P), int(Fin),
-                                                       int(embedder.hidden_dim), _layer_of(embedder)))
+                                                       int(embedder.hidden_dim), _layer_of(embedder),
+                                                       bool(graphs.unique_messages)))
     return cache[key]
 
 
 def gnn_use_fused(embedder, graphs, P: int, Fin: int) -> bool:
-    """Fused per-graph kernels (small graphs) or the layer-wise kernels (large graphs)."""
-    return gnn_fits(embedder, graphs, P, Fin) and int(graphs.max_nodes) < _LW_MIN_NODES
+    """Fused per-graph MFMA kernels, or the layer-wise kernels for every shape they do not cover."""
+    return gnn_fits(embedder, graphs, P, Fin)
 
 
 def gnn_embed(embedder, x: torch.Tensor, topo: torch.Tensor, graphs) -> torch.Tensor:

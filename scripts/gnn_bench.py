@@ -1,10 +1,11 @@
 #!/usr/bin/env python
-"""Micro-benchmark of the fused GATv2 embedder kernels (sample-agent shapes).
+"""Micro-benchmark of the native GATv2 embedder kernels (sample-agent shapes, default routing:
+MFMA one-tile <= 32 nodes, two-tile 33..64 nodes, layer-wise beyond).
 
-    python scripts/gnn_bench.py [--batch 25600] [--path 0|1|3] [--profile]
+    python scripts/gnn_bench.py [--batch 25600] [--network <graphml>] [--n-pad 24]
 
-Times forward and forward+backward per call (HIP events); ``--profile`` prints the generic
-backward's per-phase cycle counters (s_memtime, summed over waves, per graph).
+Times the inference forward, the grad-requiring forward (saves the per-layer state) and
+forward+backward per call (HIP events).
 """
 import argparse
 import os
@@ -13,18 +14,11 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PHASES = ["topo", "fwd-recompute", "bias", "d-alpha", "softmax-bwd", "d-att", "dxl/dxr", "dW", "d-bl/br|dh(cl)",
-          "dh|relu-mask(cl)", "-", "-"]
-MF_PHASES = ["topo+x", "fwd-recompute", "x_l/x_r", "bias+p+ssum", "scatter dX", "dX images", "dW mfma", "dh mfma",
-             "-", "-", "-", "-"]
-
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=25600)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--path", type=int, default=None, help="bits: 1 cl fwd, 2 cl bwd, 4 node-lane fwd (0 = generic)")
-    ap.add_argument("--profile", action="store_true")
     ap.add_argument("--hidden", type=int, default=22)
     ap.add_argument("--network", default="configs/networks/abilene/abilene-in4-rand-cap1-2.graphml")
     ap.add_argument("--n-pad", type=int, default=24)
@@ -32,10 +26,7 @@ def main():
     import torch
     from gsc_amd.coordsim.reader import load_topology
     from gsc_amd.models import GNNEmbedder, GraphSet
-    from gsc_amd.native import load
-    nat = load()
-    if a.path is not None:
-        nat.gnn_set_path(a.path)
+    from gsc_amd.ops.gnn import gnn_use_fused
     dev = "cuda"
     gs = GraphSet([load_topology(os.path.join(ROOT, a.network))], a.n_pad, dev)
     emb = GNNEmbedder(3, a.hidden, 2, "mean", 2).to(dev)
@@ -46,17 +37,21 @@ def main():
     params = list(emb.parameters())
 
     def fwd():
+        with torch.no_grad():
+            return emb(x, topo, gs, use_native=True)
+
+    def fwd_save():
         return emb(x, topo, gs, use_native=True)
 
     def fwdbwd():
         out = emb(x, topo, gs, use_native=True)
         return torch.autograd.grad((out * w).sum(), params)
 
-    for f in (fwd, fwdbwd):
+    for f in (fwd, fwd_save, fwdbwd):
         f()
     torch.cuda.synchronize()
     res = {}
-    for name, f in (("fwd", fwd), ("fwd+bwd", fwdbwd)):
+    for name, f in (("fwd", fwd), ("fwd_save", fwd_save), ("fwd+bwd", fwdbwd)):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(a.iters):
@@ -64,21 +59,10 @@ def main():
         e.record()
         torch.cuda.synchronize()
         res[name] = s.elapsed_time(e) / a.iters * 1e3
-    print(f"path={nat.gnn_get_path()} B={B} fwd {res['fwd']:.1f} us  fwd+bwd {res['fwd+bwd']:.1f} us  "
-          f"bwd~{res['fwd+bwd'] - res['fwd']:.1f} us")
-    if a.profile:
-        prof = torch.zeros(12, dtype=torch.int64, device=dev)
-        nat.gnn_set_profile(prof.data_ptr())
-        fwdbwd()
-        torch.cuda.synchronize()
-        nat.gnn_set_profile(0)
-        p = prof.cpu().tolist()
-        tot = sum(p)
-        print("backward phase cycles per graph (s_memtime ticks, summed over waves; cl: bias+d-alpha in 'd-alpha'):")
-        names = MF_PHASES if nat.gnn_get_path() & 32 else PHASES
-        for k, v in enumerate(p):
-            if v:
-                print(f"  {names[k]:>14}: {v / B:10.1f}  ({100 * v / tot:5.1f} %)")
+    kind = "fused-mfma" if gnn_use_fused(emb, gs, a.n_pad, 3) else "layer-wise"
+    print(f"{os.path.basename(a.network)} nodes={gs.max_nodes} n_pad={a.n_pad} {kind} B={B}: "
+          f"fwd {res['fwd']:.1f} us  fwd(save) {res['fwd_save']:.1f} us  fwd+bwd {res['fwd+bwd']:.1f} us  "
+          f"bwd~{res['fwd+bwd'] - res['fwd_save']:.1f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -21,64 +21,57 @@ def _graphs(dev):
     return GraphSet(topos, 24, dev)
 
 
-@pytest.mark.parametrize("path", [0, 1, 3, 7], ids=["generic", "cl-fwd", "cl-fwd-bwd", "nl-fwd"])
-@pytest.mark.parametrize("layers,iters,hidden", [(2, 2, 22), (1, 1, 22), (3, 1, 22), (2, 2, 32), (2, 2, 40)])
-def test_gnn_fused_matches_reference(layers, iters, hidden, path):
-    """Channel-lane kernels (H <= 32, <= 2 parameter blocks) and the generic fused kernels, selected
-    via gnn_set_path; unsupported shapes fall back to the generic kernels."""
-    from gsc_amd.native import load
-    nat = load()
-    old = nat.gnn_get_path()
-    nat.gnn_set_path(path)
-    try:
-        _check_gnn(layers, iters, hidden)
-    finally:
-        nat.gnn_set_path(old)
+def _mid_graphs(dev, P=64):
+    """33..64-node topologies (two 32-node MFMA tiles: gnn_mt.hip) next to an 11-node one."""
+    topos = [load_topology(cfg_path("networks", "synthetic", "syn50-in8-cap1-3.graphml")),
+             load_topology(cfg_path("networks", "tinet", "tinet-in4-rand-cap0-2.graphml")),
+             load_topology(cfg_path("networks", "chinanet", "chinanet-in4-rand-cap0-2.graphml")),
+             load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml"))]
+    return GraphSet(topos, P, dev)
 
 
-@pytest.mark.parametrize("path", [0, 1, 3, 7], ids=["generic", "cl-fwd", "cl-fwd-bwd", "nl-fwd"])
-def test_gnn_fused_50_nodes(path):
-    """50-node synthetic topology (n_pad 50, 250 messages) next to Abilene."""
-    from gsc_amd.native import load
-    nat = load()
-    old = nat.gnn_get_path()
-    nat.gnn_set_path(path)
-    try:
-        gs = GraphSet([load_topology(cfg_path("networks", "synthetic", "syn50-in8-cap1-3.graphml")),
-                       load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml"))], 50, DEV)
-        _check_gnn(2, 2, 22, gs, 50)
-    finally:
-        nat.gnn_set_path(old)
-
-
-MF_PATH = 16 | 32  # MFMA forward + backward only (unsupported shapes fall back to the generic kernels)
-
-
-@pytest.mark.parametrize("layers,iters,hidden", [(2, 2, 22), (2, 2, 16), (2, 2, 32), (2, 3, 22), (1, 1, 22),
-                                                 (3, 1, 22), (2, 2, 40)])
-def test_gnn_mfma_matches_reference(layers, iters, hidden):
-    """MFMA kernels (bf16 operands, fp32 accumulation) vs the fp32 PyTorch reference: Abilene (11
-    nodes, one 16-node tile), triangle and BtEurope (24 nodes, two tiles) in one batch."""
-    from gsc_amd.native import load
-    nat = load()
-    old = nat.gnn_get_path()
-    nat.gnn_set_path(MF_PATH)
-    try:
-        _check_gnn(layers, iters, hidden, bf16=True)
-    finally:
-        nat.gnn_set_path(old)
-
-
-def test_gnn_mfma_is_default_and_deterministic():
-    """The default path is the MFMA one for GSC shapes, and its gradients are bitwise reproducible."""
-    from gsc_amd.native import load
-    nat = load()
-    assert nat.gnn_get_path() & MF_PATH == MF_PATH
-    torch.manual_seed(3)
+@pytest.mark.parametrize("layers,iters,hidden,fused", [(2, 2, 22, True), (2, 2, 16, True), (2, 2, 32, True),
+                                                       (2, 3, 22, True), (1, 1, 22, False), (3, 1, 22, False),
+                                                       (2, 2, 40, False)])
+def test_gnn_native_matches_reference(layers, iters, hidden, fused):
+    """Native embedder vs the fp32 PyTorch reference on Abilene (11 nodes), triangle and BtEurope (24
+    nodes) in one batch.  GSC shapes (encoder + one shared process block, H <= 32) run the MFMA
+    kernels of gnn_mf.hip; the others run the layer-wise kernels (gnn_lw.py).  bf16 operands."""
+    from gsc_amd.ops.gnn import gnn_use_fused
     gs = _graphs(DEV)
+    assert gnn_use_fused(GNNEmbedder(3, hidden, layers, "mean", iters), gs, 24, 3) == fused
+    _check_gnn(layers, iters, hidden, gs, bf16=True)
+
+
+@pytest.mark.parametrize("hidden", [22, 32, 16])
+def test_gnn_mfma_two_tiles_matches_reference(hidden):
+    """33..64-node graphs on the two-tile MFMA kernels (gnn_mt.hip): 50-node synthetic, TiNet (53),
+    ChinaNet (42) and Abilene (11, second tile empty) in one batch, forward + backward vs fp32."""
+    from gsc_amd.native import load
+    from gsc_amd.ops.gnn import _tables, gnn_use_fused
+    gs = _mid_graphs(DEV)
+    emb = GNNEmbedder(3, hidden, 2, "mean", 2)
+    assert gnn_use_fused(emb, gs, 64, 3)
+    assert load().gnn_saved_bytes(_tables(gs), 64, 3, hidden, [0, 1, 1]) > 0
+    _check_gnn(2, 2, hidden, gs, 64, bf16=True)
+
+
+def test_gnn_50_nodes_padded_50():
+    """BASELINE config-4 shape: n_pad = 50 (the agent's max_nodes), 50-node topology + Abilene."""
+    gs = GraphSet([load_topology(cfg_path("networks", "synthetic", "syn50-in8-cap1-3.graphml")),
+                   load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml"))], 50, DEV)
+    _check_gnn(2, 2, 22, gs, 50, bf16=True)
+
+
+@pytest.mark.parametrize("mid", [False, True], ids=["one-tile", "two-tile"])
+def test_gnn_mfma_deterministic(mid):
+    """MFMA gradients are bitwise reproducible (per-workgroup partial rows, fixed-order sums)."""
+    torch.manual_seed(3)
+    gs = _mid_graphs(DEV) if mid else _graphs(DEV)
+    P = 64 if mid else 24
     emb = GNNEmbedder(3, 22, 2, "mean", 2).to(DEV)
     topo = torch.randint(0, gs.num_topologies, (4096,), device=DEV)
-    x = torch.rand(4096, 24, 3, device=DEV) * gs.node_mask[topo].unsqueeze(-1)
+    x = torch.rand(4096, P, 3, device=DEV) * gs.node_mask[topo].unsqueeze(-1)
     runs = []
     for _ in range(2):
         out = emb(x, topo, gs, use_native=True)
