@@ -136,10 +136,14 @@ struct Dims {
   int N, S, C, E, flow_cap, proc_cap, event_cap;
 };
 
+// The blob is [hot | cold]: everything the event handlers touch per event first, then the two
+// [N, C, S, N] tables a WRR decision reads one row of (the schedule and the per-run flow counters).
+// Topologies whose whole blob exceeds LDS (50 / 200 nodes: the tables alone are 270 KB / 4.3 MB)
+// stage only the hot prefix [0, hot) in LDS and keep the cold tables in HBM (served from L2).
 struct Layout {
   int hdr, node_cap, node_rem, inter_arr, max_usage, run_drop_node, mmpp_state, sf_load, sf_start, proc_traffic,
-      requested, drop_locs, sched, wrr, link_rem, link_passed, flows, procs, events, flow_free, proc_free,
-      sf_present, placement, total;
+      requested, drop_locs, link_rem, link_passed, flows, procs, events, flow_free, proc_free, sf_present,
+      placement, hot, sched, wrr, total;
 };
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
@@ -160,8 +164,6 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   GSC_TAKE(proc_traffic, 8 * d.N * d.S);
   GSC_TAKE(requested, 8 * d.N * d.C * d.S);
   GSC_TAKE(drop_locs, 4 * d.N * (d.S + 1));
-  GSC_TAKE(sched, 8 * d.N * d.C * d.S * d.N);
-  GSC_TAKE(wrr, 4 * d.N * d.C * d.S * d.N);
   GSC_TAKE(link_rem, 8 * d.E);
   GSC_TAKE(link_passed, 8 * d.E);
   GSC_TAKE(flows, sizeof(Flow) * d.flow_cap);
@@ -171,12 +173,16 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   GSC_TAKE(proc_free, 2 * d.proc_cap);
   GSC_TAKE(sf_present, d.N * d.S);
   GSC_TAKE(placement, d.N * d.S);
+  L.hot = o;
+  GSC_TAKE(sched, 8 * d.N * d.C * d.S * d.N);
+  GSC_TAKE(wrr, 4 * d.N * d.C * d.S * d.N);
 #undef GSC_TAKE
   L.total = o;
   return L;
 }
 
-// Typed view of one env's state blob.
+// Typed view of one env's state blob (the hot prefix at `base`, the cold tables at `cold`: the same
+// blob unless the hot prefix was staged into LDS on its own).
 struct Env {
   Header* h;
   double *node_cap, *node_rem, *inter_arr, *max_usage, *sf_load, *sf_start, *proc_traffic, *requested, *sched,
@@ -189,7 +195,8 @@ struct Env {
   uint8_t *sf_present, *placement;
   Dims d;
 
-  GSC_HD Env(char* base, const Layout& L, const Dims& dims) : d(dims) {
+  GSC_HD Env(char* base, const Layout& L, const Dims& dims, char* cold = nullptr) : d(dims) {
+    char* const cb = cold ? cold : base;
     h = (Header*)(base + L.hdr);
     node_cap = (double*)(base + L.node_cap);
     node_rem = (double*)(base + L.node_rem);
@@ -202,8 +209,8 @@ struct Env {
     proc_traffic = (double*)(base + L.proc_traffic);
     requested = (double*)(base + L.requested);
     drop_locs = (int32_t*)(base + L.drop_locs);
-    sched = (double*)(base + L.sched);
-    wrr = (int32_t*)(base + L.wrr);
+    sched = (double*)(cb + L.sched);
+    wrr = (int32_t*)(cb + L.wrr);
     link_rem = (double*)(base + L.link_rem);
     link_passed = (double*)(base + L.link_passed);
     flows = (Flow*)(base + L.flows);

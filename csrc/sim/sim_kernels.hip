@@ -28,6 +28,7 @@ constexpr long kMaxEventsPerStep = 4000000;  // runaway guard (no GPU hang on a 
 struct SimArgs {
   char* states;
   long state_bytes;
+  long lds_state_bytes;      // bytes of the blob staged in LDS (mode 1: all, mode 2: the hot prefix)
   Layout L;
   Dims D;
   SimConst K;
@@ -297,11 +298,11 @@ struct BucketLayout {
 
 template <class B, int QS, bool PROF>
 __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst& K, char* base, char* topo_lds,
-                                                int env, int lane) {
+                                                int env, int lane, char* cold = nullptr) {
   const unsigned long long t_entry = PROF ? __builtin_amdgcn_s_memtime() : 0;
   Env S = [&] {
-    if constexpr (std::is_same<B, DynLayout>::value) return Env(base, a.L, a.D);
-    else return Env(base, BucketLayout<B>::L, BucketLayout<B>::D);
+    if constexpr (std::is_same<B, DynLayout>::value) return Env(base, a.L, a.D, cold);
+    else return Env(base, BucketLayout<B>::L, BucketLayout<B>::D, cold);
   }();
   // Keep the env header in registers for the whole window (written back once at the end).
   Header* const h_mem = S.h;
@@ -456,7 +457,9 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   }
 }
 
-template <int QSETS, bool LDS_STATE, bool PROF = false, class B = DynLayout>
+// LDS_STATE: 0 = the state blob stays in HBM, 1 = the whole blob is staged in LDS, 2 = only its hot
+// prefix is (the [N, C, S, N] schedule / WRR tables stay in HBM: 50- and 200-node topologies).
+template <int QSETS, int LDS_STATE, bool PROF = false, class B = DynLayout>
 __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int env = blockIdx.x;
@@ -468,10 +471,10 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
   else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
   constexpr bool STATIC = !std::is_same<B, DynLayout>::value;
-  // LDS: [state blob (LDS mode)][SimConst][topology tables] -- the blob at offset 0, so with a
-  // compile-time layout every state address is a constant
-  long sbytes = a.state_bytes;
-  if constexpr (STATIC) sbytes = BucketLayout<B>::L.total;
+  // LDS: [state blob or its hot prefix (LDS modes)][SimConst][topology tables] -- the blob at offset
+  // 0, so with a compile-time layout every state address is a constant
+  long sbytes = a.lds_state_bytes;
+  if constexpr (STATIC) sbytes = LDS_STATE == 2 ? BucketLayout<B>::L.hot : BucketLayout<B>::L.total;
   const long sb = LDS_STATE ? align16((int)sbytes) : 0;
   SimConst* Ks = reinterpret_cast<SimConst*>(smem + sb);
   if (lane == 0) *Ks = a.K;
@@ -481,12 +484,12 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   // 58 / 59) -> the effective engine clock while the simulator runs (e.g. beside the learner)
   const unsigned long long c_begin = PROF ? __builtin_amdgcn_s_memtime() : 0;
   const unsigned long long r_begin = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
-  if constexpr (LDS_STATE) {
+  if constexpr (LDS_STATE != 0) {
     const unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0;
     copy16(smem, g, sbytes, lane);
     __syncthreads();
     const unsigned long long t1 = PROF ? __builtin_amdgcn_s_memtime() : 0;
-    device_step_env<B, QSETS, PROF>(a, *Ks, smem, topo_lds, env, lane);
+    device_step_env<B, QSETS, PROF>(a, *Ks, smem, topo_lds, env, lane, LDS_STATE == 2 ? g : nullptr);
     const unsigned long long t2 = PROF ? __builtin_amdgcn_s_memtime() : 0;
     copy16(g, smem, sbytes, lane);
     if (PROF && lane == 0) {  // state blob HBM -> LDS / LDS -> HBM
@@ -595,20 +598,22 @@ class SimContext {
       for (auto& t : topos_) maxH = t.H > maxH ? t.H : maxH;
       topo_stage_ = topo_stage_bytes(D_, maxH);
       // Large topologies (N^2 * hops path tables beyond the LDS budget, e.g. 200 nodes): the tables
-      // stay in HBM and are served from L2 — only SimConst (+ the state blob, if it fits) is staged.
+      // stay in HBM and are served from L2 — only SimConst (+ the state, if it fits) is staged.
       if (const_stage_bytes() + topo_stage_ + 1024 > max_lds) topo_stage_ = 0;
-      // the state blob has priority over the topology tables: every event reads and writes it,
-      // while the tables are read-only and stay L2-resident (e.g. 50-node topologies: both do
-      // not fit one workgroup's LDS together)
-      if (topo_stage_ && const_stage_bytes() + topo_stage_ + L_.total > max_lds &&
-          const_stage_bytes() + L_.total <= max_lds)
-        topo_stage_ = 0;
+      // state in LDS: the whole blob, else its hot prefix (the schedule / WRR tables stay in HBM)
+      const long total = L_.total, hot = L_.hot;
+      auto fits = [&](long state) { return const_stage_bytes() + topo_stage_ + state <= max_lds; };
+      auto fits_alone = [&](long state) { return const_stage_bytes() + state <= max_lds; };
+      // the state has priority over the topology tables: every event reads and writes it, while the
+      // tables are read-only and stay L2-resident (e.g. 50-node topologies: both do not fit one
+      // workgroup's LDS together)
+      if (topo_stage_ && !fits(total) && (fits_alone(total) || (!fits(hot) && fits_alone(hot)))) topo_stage_ = 0;
+      lds_mode_ = fits(total) ? 1 : (fits(hot) ? 2 : 0);
+      const long state = lds_mode_ == 1 ? total : (lds_mode_ == 2 ? hot : 0);
       const long fixed = const_stage_bytes() + topo_stage_;
-      use_lds_ = fixed + L_.total <= max_lds;
       // the per-hop edge table saves one dependent lookup per hop, but not at the price of a
       // workgroup per CU (50-node topologies with the state blob in HBM: 112 vs 72 KB of tables)
       if (topo_stage_) {
-        const long state = use_lds_ ? L_.total : 0;
         const long without = topo_stage_bytes(D_, maxH, false);
         const long cu_lds = 160 * 1024;
         if (cu_lds / (const_stage_bytes() + topo_stage_ + state) < cu_lds / (const_stage_bytes() + without + state)) {
@@ -616,16 +621,20 @@ class SimContext {
           stage_pedges_ = 0;
         }
       }
-      const long need = fixed + (use_lds_ ? L_.total : 0);
+      const long need = fixed + state;
       qsets_ = D_.event_cap <= 64 ? 1 : (D_.event_cap <= 128 ? 2 : (D_.event_cap <= 256 ? 4 : 8));
       if (need > 65536) {
         const void* fns[] = {
-            (const void*)sim_step_kernel<1, true>, (const void*)sim_step_kernel<2, true>,
-            (const void*)sim_step_kernel<4, true>, (const void*)sim_step_kernel<8, true>,
-            (const void*)sim_step_kernel<1, false>, (const void*)sim_step_kernel<2, false>,
-            (const void*)sim_step_kernel<4, false>, (const void*)sim_step_kernel<8, false>,
-            (const void*)sim_step_kernel<1, true, true>, (const void*)sim_step_kernel<2, true, true>,
-            (const void*)sim_step_kernel<4, true, true>, (const void*)sim_step_kernel<8, true, true>};
+            (const void*)sim_step_kernel<1, 1>, (const void*)sim_step_kernel<2, 1>,
+            (const void*)sim_step_kernel<4, 1>, (const void*)sim_step_kernel<8, 1>,
+            (const void*)sim_step_kernel<1, 2>, (const void*)sim_step_kernel<2, 2>,
+            (const void*)sim_step_kernel<4, 2>, (const void*)sim_step_kernel<8, 2>,
+            (const void*)sim_step_kernel<1, 0>, (const void*)sim_step_kernel<2, 0>,
+            (const void*)sim_step_kernel<4, 0>, (const void*)sim_step_kernel<8, 0>,
+            (const void*)sim_step_kernel<1, 1, true>, (const void*)sim_step_kernel<2, 1, true>,
+            (const void*)sim_step_kernel<4, 1, true>, (const void*)sim_step_kernel<8, 1, true>,
+            (const void*)sim_step_kernel<1, 2, true>, (const void*)sim_step_kernel<2, 2, true>,
+            (const void*)sim_step_kernel<4, 2, true>, (const void*)sim_step_kernel<8, 2, true>};
         for (auto f : fns) GSC_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
       }
     }
@@ -635,9 +644,13 @@ class SimContext {
   }
 
   long state_bytes() const { return L_.total; }
-  bool use_lds() const { return use_lds_; }
-  // LDS bytes one env's workgroup needs on the device (SimConst + topology tables + state blob)
-  long lds_per_env() const { return const_stage_bytes() + topo_stage_ + (use_lds_ ? L_.total : 0); }
+  long hot_bytes() const { return L_.hot; }
+  bool use_lds() const { return lds_mode_ != 0; }
+  // 0: state in HBM, 1: whole state blob in LDS, 2: its hot prefix in LDS (schedule / WRR tables in HBM)
+  int lds_mode() const { return lds_mode_; }
+  long lds_state() const { return lds_mode_ == 1 ? L_.total : (lds_mode_ == 2 ? L_.hot : 0); }
+  // LDS bytes one env's workgroup needs on the device (SimConst + topology tables + staged state)
+  long lds_per_env() const { return const_stage_bytes() + topo_stage_ + lds_state(); }
 
   void reset(uintptr_t states, uintptr_t topo_init, uintptr_t seeds, uintptr_t obs, int E, uintptr_t stream) {
     SimArgs a = args(states, topo_init, seeds, 0, 0, obs, 0, 0, 0, 0, 0, E);
@@ -663,12 +676,14 @@ class SimContext {
     static const int prio = getenv("GSC_SIM_PRIO") ? atoi(getenv("GSC_SIM_PRIO")) : 3;
     a.prio = prio;
     if (device_) {
-      const size_t lds = const_stage_bytes() + topo_stage_ + (use_lds_ ? (size_t)L_.total : 0);
+      const size_t lds = (size_t)lds_per_env();
       const hipStream_t st = stream_of(stream);
-#define GSC_LAUNCH_SIM(QS)                                                                             \
-  if (use_lds_ && a.prof) hipLaunchKernelGGL((sim_step_kernel<QS, true, true>), dim3(E), dim3(64), lds, st, a); \
-  else if (use_lds_) hipLaunchKernelGGL((sim_step_kernel<QS, true>), dim3(E), dim3(64), lds, st, a);          \
-  else hipLaunchKernelGGL((sim_step_kernel<QS, false>), dim3(E), dim3(64), lds, st, a);
+#define GSC_LAUNCH_SIM(QS)                                                                                     \
+  if (lds_mode_ == 1 && a.prof) hipLaunchKernelGGL((sim_step_kernel<QS, 1, true>), dim3(E), dim3(64), lds, st, a); \
+  else if (lds_mode_ == 1) hipLaunchKernelGGL((sim_step_kernel<QS, 1>), dim3(E), dim3(64), lds, st, a);           \
+  else if (lds_mode_ == 2 && a.prof) hipLaunchKernelGGL((sim_step_kernel<QS, 2, true>), dim3(E), dim3(64), lds, st, a); \
+  else if (lds_mode_ == 2) hipLaunchKernelGGL((sim_step_kernel<QS, 2>), dim3(E), dim3(64), lds, st, a);           \
+  else hipLaunchKernelGGL((sim_step_kernel<QS, 0>), dim3(E), dim3(64), lds, st, a);
       switch (qsets_) {
         case 1: GSC_LAUNCH_SIM(1) break;
         case 2: GSC_LAUNCH_SIM(2) break;
@@ -689,6 +704,7 @@ class SimContext {
     SimArgs a{};
     a.states = ptr<char>(states);
     a.state_bytes = L_.total;
+    a.lds_state_bytes = lds_state();
     a.L = L_;
     a.D = D_;
     a.K = K_;
@@ -704,7 +720,7 @@ class SimContext {
     a.stats = ptr<float>(stats);
     a.ep_return = ptr<float>(ep_return);
     a.E = E;
-    a.use_lds = use_lds_ ? 1 : 0;
+    a.use_lds = lds_mode_;
     a.topo_stage = topo_stage_;
     a.stage_pedges = stage_pedges_;
     return a;
@@ -777,7 +793,7 @@ class SimContext {
 
   bool device_;
   int host_threads_;
-  bool use_lds_ = false;
+  int lds_mode_ = 0;
   long topo_stage_ = 0;
   int stage_pedges_ = 1;
   int qsets_ = 8;
@@ -795,6 +811,8 @@ void register_sim(py::module_& m) {
       .def_property_readonly("state_bytes", &SimContext::state_bytes)
       .def_property_readonly("use_lds", &SimContext::use_lds)
       .def_property_readonly("lds_per_env", &SimContext::lds_per_env)
+      .def_property_readonly("lds_mode", &SimContext::lds_mode)
+      .def_property_readonly("hot_bytes", &SimContext::hot_bytes)
       .def("reset", &SimContext::reset)
       .def("step", &SimContext::step, py::arg("states"), py::arg("topo_next"), py::arg("seeds"), py::arg("actions"),
            py::arg("action_stride"), py::arg("obs"), py::arg("next_obs"), py::arg("reward"), py::arg("done"),

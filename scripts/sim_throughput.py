@@ -23,15 +23,21 @@ ap.add_argument("--net", default="configs/networks/abilene/abilene-in4-rand-cap1
 ap.add_argument("--profile", action="store_true")
 ap.add_argument("--simcfg", default="configs/config/simulator/sample_config.yaml")
 ap.add_argument("--cus", type=int, default=0, help="run on a stream CU-masked to this many CUs (0: all)")
+ap.add_argument("--preset", default=None, help="bench.py preset (network / service / simulator / agent config)")
 args = ap.parse_args()
-cfg = yaml.safe_load(open("configs/config/agent/sample_agent.yaml"))
-sim = load_batched_from_paths([args.net], "configs/service_functions/abc.yaml", args.simcfg, cfg, args.envs,
-                              device=args.device)
-n = sim.topologies[0].n
+if args.preset:
+    from bench import PRESETS
+    pre = PRESETS[args.preset]
+    nets, svc, args.simcfg, agent = pre["network"], pre["service"], pre["sim_config"], pre["agent_config"]
+else:
+    nets, svc, agent = [args.net], "configs/service_functions/abc.yaml", "configs/config/agent/sample_agent.yaml"
+cfg = yaml.safe_load(open(agent))
+sim = load_batched_from_paths(nets, svc, args.simcfg, cfg, args.envs, device=args.device)
+n, P = sim.topologies[0].n, sim.n_pad
 rng = np.random.default_rng(0)
-a = np.zeros((24, 1, 3, 24))
-a[:n, :, :, :n] = rng.random((n, 1, 3, n))
-a = threshold_normalize(a.reshape(-1), 24, 0.1, 2).astype(np.float32)
+a = np.zeros((P, sim.C, sim.F, P))
+a[:n, :, :, :n] = rng.random((n, sim.C, sim.F, n))
+a = threshold_normalize(a.reshape(-1), P, 0.1, 2).astype(np.float32)
 A = torch.from_numpy(np.tile(a, (args.envs, 1))).to(args.device)
 if args.cus:
     stream = torch.cuda.ExternalStream(sim.native.create_cu_masked_stream(list(range(args.cus))))
@@ -51,7 +57,8 @@ if args.device == "cuda":
     torch.cuda.synchronize()
 dt = time.perf_counter() - t
 sim.check_flags()
-print(f"cus={args.cus or 'all'} envs={args.envs} steps={args.steps} state_bytes={sim.state_bytes} lds={sim.ctx.use_lds} "
+print(f"cus={args.cus or 'all'} envs={args.envs} steps={args.steps} state_bytes={sim.state_bytes} "
+      f"lds_mode={sim.ctx.lds_mode} lds_per_env={sim.ctx.lds_per_env} "
       f"env_steps_per_s={args.envs * args.steps / dt:.1f} ms_per_step={dt / args.steps * 1e3:.3f}")
 if args.profile:
     pr = sim.prof.double().cpu()
