@@ -36,6 +36,14 @@ namespace gsc {
 
 constexpr int kMtTS = 40;  // bf16 row stride of the per-tile [k][32 nodes] images (80 B rows)
 
+// Workgroup barrier ordering LDS only: the saved-state stores to HBM stay in flight across it (a
+// plain __syncthreads() waits for every outstanding global store of the wave first)
+__device__ __forceinline__ void mt_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 struct MtLayout {
   int NT, NV, NVS, MS;           // tiles, node rows (32 NT), bf16 stride of [.][node] images, G^T stride
   int hTrows0, hTrows;           // rows of the per-tile [k][node] images: encoder input (Fin -> 4), hidden
@@ -145,7 +153,7 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
       for (int i = lane; i < n0 + n1; i += 64)
         reinterpret_cast<uint4*>(dst)[i] = i < n0 ? s0[i] : s1[i - n0];
     }
-    __syncthreads();  // topology visible to every wave
+    mt_barrier();  // topology visible to every wave
     int cur = 0;
     float pl = 0.f;
     for (int l = 0; l < a.L; ++l) {
@@ -162,7 +170,7 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
         mx[32 * w + v] = kMfKeyNegInf;
         sm[32 * w + v] = 0.f;
       }
-      __syncthreads();  // B1: x_l rows and X_l^T of every tile
+      mt_barrier();  // B1: x_l rows and X_l^T of every tile
       // scores / softmax over the messages into the own tile (wave-local atomics)
       asm volatile("" ::: "memory");
       for (int q = T.q0 + lane; q < T.q1; q += 64) {
@@ -239,13 +247,13 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
         }
         cur ^= 1;
       }
-      __syncthreads();  // B2: every wave is done with this layer's x_l / X_l^T
+      mt_barrier();  // B2: every wave is done with this layer's x_l / X_l^T
     }
     {
       const int lane = mf_lane(), c = lane & 31, hh = lane >> 5;
       pl += __shfl_xor(pl, 32);
       if (hh == 0) pool[32 * w + c] = pl;
-      __syncthreads();
+      mt_barrier();
       if (w == 0 && hh == 0 && c < a.H) {
         float s = 0.f;
         for (int t2 = 0; t2 < m.NT; ++t2) s += pool[32 * t2 + c];
@@ -316,7 +324,7 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
   const int NVS = m.NVS, MS = m.MS;
   for (int g = blockIdx.x; g < a.B; g += gridDim.x) {
     // the partner may still read dy^T / E^T / the topology of the previous graph's first conv
-    __syncthreads();
+    mt_barrier();
     int lane = mf_lane();
     mt_load_topo(T, a, a.topo[g], w);
     const int n = T.n, nl = n - 32 * w;
@@ -373,7 +381,7 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
         mf_store_rows<HPF>(xb, nl, xr + 32 * w * mf_xs(HPF), lane);
       }
       for (int v = lane; v < 32; v += 64) ssum[32 * w + v] = 0.f;
-      __syncthreads();  // B1: x_l rows, dy^T of every tile; E^T rows cleared
+      mt_barrier();  // B1: x_l rows, dy^T of every tile; E^T rows cleared
       // p_q = alpha_q (dy[i] . x_l[j]) / deg_i ; ssum_i = sum_{q -> i} p_q ; E^T[j][i] = alpha_q / deg_i
       asm volatile("" ::: "memory");
       for (int q = T.q0 + lane; q < T.q1; q += 64) {
@@ -398,7 +406,7 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
       //   d att_c += de_q lrelu(z) ;  G[q][c] = de_q att_c lrelu'(z)   (stored as G^T[c][q], bf16)
       if (l == 0) mt_att_bwd<HPF>(T, da, al, ssum, xl, xr, vec, U, MS, lane, gattE);
       else mt_att_bwd<HPF>(T, da, al, ssum, xl, xr, vec, U, MS, lane, gattP);
-      __syncthreads();  // B2: E^T and G^T of every tile
+      mt_barrier();  // B2: E^T and G^T of every tile
       const int nn = nl - 4 * hh;
       if (l == 0) GE.bias += mf_colsum(dyt, nn);
       else GP.bias += mf_colsum(dyt, nn);
