@@ -43,11 +43,18 @@ PRESETS = {
                   sim_config="configs/config/simulator/rand-arrival12_trace_syn50.yaml",
                   agent_config="configs/config/agent/agent_syn50.yaml", envs=256, batch=None, period=0,
                   model="GSC GATv2-DDPG, 50-node synthetic topology, 3 SFCs, trace traffic (A = 22,500)"),
+    # BASELINE config 5 ("scheduler-driven network changes during training"): the network scheduler
+    # switches every env to the next topology at every episode end (period 1) and episodes are 20 steps,
+    # so any timed window of more than 20 steps contains a switch (counted in the JSON line).  Learner
+    # batch 16 per env-step: the [B, A] actor output / action gradient at A = 360,000 (three
+    # topologies: not re-associated) bounds it (2.9 GB per bf16 buffer at B = 4,096)
     "syn200": dict(network=[f"configs/networks/synthetic/syn200-in16-cap1-3-s{i}.graphml" for i in range(3)],
                    service="configs/service_functions/abc-3sfc.yaml",
                    sim_config="configs/config/simulator/sample_config.yaml",
-                   agent_config="configs/config/agent/agent_syn200.yaml", envs=64, batch=1024, period=2,
-                   model="GSC GATv2-DDPG, 200-node synthetic topologies switched every 2 episodes, 3 SFCs (A = 360,000)"),
+                   agent_config="configs/config/agent/agent_syn200.yaml", envs=128, batch=2048, period=1,
+                   episode_steps=20,
+                   model="GSC GATv2-DDPG, 200-node synthetic topologies switched every episode (20 steps), 3 SFCs "
+                         "(A = 360,000)"),
 }
 
 
@@ -103,6 +110,8 @@ def main():
         device = torch.device("cpu")
     os.chdir(ROOT)
     cfg = yaml.safe_load(open(agent_config))
+    if pre.get("episode_steps"):
+        cfg["episode_steps"] = int(pre["episode_steps"])
     sim = load_batched_from_paths(networks, service, sim_config, cfg, args.envs, device=device,
                                   seed=args.seed * 1000 + info.rank)
     tcfg = TrainerConfig(num_envs=args.envs, batch_size=args.batch_size, updates_per_step=args.updates_per_step,
@@ -165,6 +174,16 @@ def main():
     dt = float(dt_t.item())
     total_envs = args.envs * info.world_size
     value = total_envs * args.steps / dt
+    # topology switches of the network scheduler inside the timed window (episode ends at steps
+    # k * episode_steps - 1; the episode that starts after one uses schedule[(episode // period) % T])
+    ep_steps, T = sim.episode_steps, len(networks)
+    period = pre["period"]
+    switches = 0
+    if period and T > 1:
+        topo_of = lambda ep: (ep // period) % T
+        for ep in range(args.warmup // ep_steps + 1, (args.warmup + args.steps) // ep_steps + 1):
+            if ep * ep_steps < args.warmup + args.steps and topo_of(ep) != topo_of(ep - 1):
+                switches += 1
     if info.is_main:
         rec = {
             "metric": "env-steps/sec (whole node) + flow success ratio, Abilene SFC" if args.preset == "abilene"
@@ -198,6 +217,9 @@ def main():
                 "updates_per_step": args.updates_per_step,
                 "sim_learner_overlap": not args.no_overlap,
                 "sim_cus": getattr(trainer, "sim_cus", 0),
+                "episode_steps": ep_steps,
+                "scheduler_period": period,
+                "topology_switches_timed": switches,
                 "topology": ",".join(os.path.basename(n) for n in networks),
                 "device": torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu",
             },

@@ -17,9 +17,10 @@ constexpr int kMaxS = 8;      // distinct SFs
 constexpr int kMaxTTL = 8;
 constexpr int kNumStats = 16;
 
+// (return_link_resources is no process here: a per-link release ledger, see ledger_push)
 enum ProcType : uint8_t {
   P_FREE = 0, P_WRITER, P_MMPP, P_TRACE, P_ARRIVAL, P_HANDLE, P_DECIDE, P_FORWARD, P_PROCESS, P_REQUEST,
-  P_FINISH, P_RETLINK
+  P_FINISH
 };
 // per-type resume states
 enum : uint8_t {
@@ -32,12 +33,13 @@ enum : uint8_t {
   F_INIT = 0, F_AFTER_HOP,
   PR_INIT = 0, PR_AFTER_REQ, PR_AFTER_WAIT,
   RQ_INIT = 0, RQ_AFTER,
-  FI_INIT = 0, FI_AFTER,
-  RL_INIT = 0, RL_AFTER
+  FI_INIT = 0, FI_AFTER
 };
 enum DropReason { R_TTL = 0, R_DECISION = 1, R_LINK = 2, R_NODE = 3 };
 enum Objective { OBJ_PRIO_FLOW = 0, OBJ_SOFT_DEADLINE = 1, OBJ_SOFT_DEADLINE_EXP = 2, OBJ_WEIGHTED = 3 };
-enum Flags { FLAG_FLOW_OVERFLOW = 1, FLAG_PROC_OVERFLOW = 2, FLAG_EVENT_OVERFLOW = 4, FLAG_BAD_STATE = 8 };
+enum Flags {
+  FLAG_FLOW_OVERFLOW = 1, FLAG_PROC_OVERFLOW = 2, FLAG_EVENT_OVERFLOW = 4, FLAG_BAD_STATE = 8, FLAG_REL_OVERFLOW = 16
+};
 constexpr int16_t kStopProc = -2;
 
 struct alignas(16) Event {  // 16 B
@@ -58,6 +60,13 @@ struct alignas(16) Proc {  // 32 B
   uint8_t type, state;
   int16_t flow, parent, a, b, c, ret, pad;
   double x, y;
+};
+
+// A pending link-capacity return: return_link_resources' timeout, keyed like the SimPy event it replaces.
+struct alignas(8) Release {  // 24 B
+  double t, dr;
+  uint32_t key;
+  int32_t edge;
 };
 
 struct alignas(16) Flow {  // 64 B: four 16-byte LDS accesses per copy
@@ -83,7 +92,9 @@ struct Header {
   double total_e2e, total_path_delay, total_proc_delay;
   double run_e2e, run_max_e2e, run_total_path_delay, run_avg_path_delay;
   double ewma_flows, episode_return;
-  int32_t proc_head, pad_h;  // proc_free[proc_top - 1] (the next pid to allocate), cached off the LDS stack
+  int32_t proc_head;         // proc_free[proc_top - 1] (the next pid to allocate), cached off the LDS stack
+  uint32_t cur_key;          // key of the event being dispatched (orders the release ledger against it)
+  int32_t n_rel, max_rel;    // pending link releases, high-water mark
 };
 
 // Read-only per-topology tables (device or host memory).
@@ -133,7 +144,7 @@ struct SimConst {
 };
 
 struct Dims {
-  int N, S, C, E, flow_cap, proc_cap, event_cap;
+  int N, S, C, E, flow_cap, proc_cap, event_cap, rel_cap;
 };
 
 // The blob is [hot | cold]: everything the event handlers touch per event first, then the two
@@ -142,8 +153,8 @@ struct Dims {
 // stage only the hot prefix [0, hot) in LDS and keep the cold tables in HBM (served from L2).
 struct Layout {
   int hdr, node_cap, node_rem, inter_arr, max_usage, run_drop_node, mmpp_state, sf_load, sf_start, proc_traffic,
-      requested, drop_locs, link_rem, link_passed, flows, procs, events, flow_free, proc_free, sf_present,
-      placement, hot, sched, wrr, total;
+      requested, drop_locs, link_rem, link_passed, link_next, rel, flows, procs, events, flow_free, proc_free,
+      sf_present, placement, hot, sched, wrr, total;
 };
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
@@ -166,6 +177,8 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   GSC_TAKE(drop_locs, 4 * d.N * (d.S + 1));
   GSC_TAKE(link_rem, 8 * d.E);
   GSC_TAKE(link_passed, 8 * d.E);
+  GSC_TAKE(link_next, 8 * d.E);
+  GSC_TAKE(rel, sizeof(Release) * d.rel_cap);
   GSC_TAKE(flows, sizeof(Flow) * d.flow_cap);
   GSC_TAKE(procs, sizeof(Proc) * d.proc_cap);
   GSC_TAKE(events, sizeof(Event) * d.event_cap);
@@ -186,8 +199,9 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
 struct Env {
   Header* h;
   double *node_cap, *node_rem, *inter_arr, *max_usage, *sf_load, *sf_start, *proc_traffic, *requested, *sched,
-      *link_rem, *link_passed;
+      *link_rem, *link_passed, *link_next;
   int32_t *run_drop_node, *mmpp_state, *drop_locs, *wrr;
+  Release* rel;
   Flow* flows;
   Proc* procs;
   Event* events;
@@ -213,6 +227,8 @@ struct Env {
     wrr = (int32_t*)(cb + L.wrr);
     link_rem = (double*)(base + L.link_rem);
     link_passed = (double*)(base + L.link_passed);
+    link_next = (double*)(base + L.link_next);
+    rel = (Release*)(base + L.rel);
     flows = (Flow*)(base + L.flows);
     procs = (Proc*)(base + L.procs);
     events = (Event*)(base + L.events);
@@ -368,6 +384,91 @@ GSC_HD int alloc_flow(Env& S) {
   return fid;
 }
 GSC_HD void free_flow(Env& S, int fid) { S.flow_free[S.h->flow_top++] = (int16_t)fid; }
+
+// ------------------------------------------------------------------------------------------------
+// Link-capacity returns as a per-link ledger (DefaultFlowForwarder.return_link_resources,
+// default_forwarder.py:112-125: after each hop a process waits flow.duration, then adds flow.dr back
+// to the link).  The forwarder's hop step spawns that process and yields; the next event is always
+// its URGENT initialise event (no other URGENT event can be pending at the time of a NORMAL hop
+// timeout), whose only action is the duration timeout.  So the return takes effect exactly at
+// (now + duration, NORMAL, the event id drawn right after the forwarder's own event), and its
+// completion event has no waiter.  The ledger records that key instead of the three SimPy events;
+// a capacity check of link e at event (t, key) first applies e's entries with a smaller key, in key
+// order.  Event ids of the replaced events are not drawn: every remaining event and ledger key keeps
+// its relative order, so the outcome is bit-identical (tests/test_batched_sim_diff.py) with about a
+// quarter fewer dispatched events per step.
+// ------------------------------------------------------------------------------------------------
+GSC_HD bool key_less(double ta, uint32_t ka, double tb, uint32_t kb) { return ta < tb || (ta == tb && ka < kb); }
+
+GSC_HD void ledger_push(Env& S, double t, int e, double dr) {
+  Header* h = S.h;
+  const uint32_t key = (1u << 31) | (h->eid & 0x7fffffffu);
+  h->eid++;
+  if (h->n_rel >= S.d.rel_cap) { h->flags |= FLAG_REL_OVERFLOW; return; }
+  Release r;
+  r.t = t;
+  r.dr = dr;
+  r.key = key;
+  r.edge = e;
+  S.rel[h->n_rel++] = r;
+  if (h->n_rel > h->max_rel) h->max_rel = h->n_rel;
+  if (t < S.link_next[e]) S.link_next[e] = t;
+}
+
+// Apply link e's returns that precede the current event, in key order, then refresh link_next[e].
+GSC_HD_CALL void ledger_apply(Env& S, int e) {
+  const double now = S.h->now;
+  if (GSC_UNI(now < S.link_next[e])) return;  // nothing due (the common case: one LDS read)
+  const uint32_t ck = S.h->cur_key;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int lane = wave_lane();
+  for (;;) {
+    const int nr = GSC_UNI(S.h->n_rel);
+    double bt = 1.0 / 0.0;
+    uint32_t bk = 0xffffffffu;
+    int bi = -1;
+    for (int i = lane; i < nr; i += 64) {
+      const Release r = S.rel[i];
+      if (r.edge == e && key_less(r.t, r.key, now, ck) && key_less(r.t, r.key, bt, bk)) { bt = r.t; bk = r.key; bi = i; }
+    }
+    const double tmin = -wave_max_f64(-bt);
+    const uint32_t kmin = dpp_red_u32(bt == tmin ? bk : 0xffffffffu, 0xffffffffu,
+                                      [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+    if (kmin == 0xffffffffu) break;
+    const unsigned long long who = __ballot(bi >= 0 && bt == tmin && bk == kmin);
+    const int idx = __builtin_amdgcn_readlane(bi, (int)__ffsll((long long)who) - 1);
+    S.link_rem[e] += S.rel[idx].dr;
+    const int last = nr - 1;
+    if (idx != last) S.rel[idx] = S.rel[last];
+    S.h->n_rel = last;
+    __builtin_amdgcn_wave_barrier();
+  }
+  double nx = 1.0 / 0.0;
+  for (int i = lane; i < S.h->n_rel; i += 64) {
+    const Release r = S.rel[i];
+    if (r.edge == e && r.t < nx) nx = r.t;
+  }
+  S.link_next[e] = -wave_max_f64(-nx);
+#else
+  for (;;) {
+    int bi = -1;
+    for (int i = 0; i < S.h->n_rel; ++i) {
+      const Release& r = S.rel[i];
+      if (r.edge == e && key_less(r.t, r.key, now, ck) &&
+          (bi < 0 || key_less(r.t, r.key, S.rel[bi].t, S.rel[bi].key)))
+        bi = i;
+    }
+    if (bi < 0) break;
+    S.link_rem[e] += S.rel[bi].dr;
+    const int last = --S.h->n_rel;
+    if (bi != last) S.rel[bi] = S.rel[last];
+  }
+  double nx = 1.0 / 0.0;
+  for (int i = 0; i < S.h->n_rel; ++i)
+    if (S.rel[i].edge == e && S.rel[i].t < nx) nx = S.rel[i].t;
+  S.link_next[e] = nx;
+#endif
+}
 
 // ------------------------------------------------------------------------------------------------
 // Metrics hooks (reference coordsim/metrics/metrics.py)
@@ -547,13 +648,14 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
   proc_return(S, pid, P, (int16_t)best);
 }
 
-// DefaultFlowForwarder.forward_flow (default_forwarder.py:21-90) + return_link_resources.
+// DefaultFlowForwarder.forward_flow (default_forwarder.py:21-90); return_link_resources -> ledger_push.
 GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P0, const Flow& f0) {
   Proc P = P0;
   const int fid = GSC_UNI(P.flow);
   Flow f = f0;
   const int n = GSC_UNI(T.n);
   const int nxt = GSC_UNI(P.b);
+  int rel_e = -1;  // link of the hop just taken: its capacity return is recorded after this step's event
   if (GSC_UNI(P.state) == F_INIT) {
     const int cur = GSC_UNI(f.node);
     const double pd = (cur != nxt) ? T.pdelay[cur * n + nxt] : 0.0;
@@ -568,9 +670,7 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
     // the hop just taken and its edge were kept in the record (ret / pad: a forwarder has no
     // children) when it was scheduled: no dependent path-table / edge-table lookups here
     const int hop = GSC_UNI(P.ret);
-    const int e = GSC_UNI(P.pad);
-    const int c = spawn(S, P_RETLINK, RL_INIT, -1, -1);
-    if (c >= 0) { S.procs[c].a = (int16_t)e; S.procs[c].x = f.dr; S.procs[c].y = f.duration; }
+    rel_e = GSC_UNI(P.pad);
     f.node = (int16_t)hop;
     P.c = (int16_t)(pc + 1);
     if (GSC_UNI(pc + 1 >= T.plen[pa * n + nxt])) {
@@ -582,6 +682,7 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
       fm.e2e = f.e2e;
       fm.ttl = f.ttl;
       proc_return(S, pid, P, 1);
+      ledger_push(S, S.h->now + f.duration, rel_e, f.dr);
       return;
     }
   }
@@ -592,11 +693,13 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
   const int e = GSC_UNI(T.pedges[pidx]);  // == edge_id[cur * n + hop]
   Flow& fm = S.flows[fid];
   fm.node = f.node;
+  ledger_apply(S, e);
   const double lrem = S.link_rem[e];
   if (GSC_UNI(lrem - f.dr >= 0)) {
     S.link_rem[e] = lrem - f.dr;
   } else {
     proc_return(S, pid, P, 0);
+    if (rel_e >= 0) ledger_push(S, S.h->now + f.duration, rel_e, f.dr);
     return;
   }
   S.link_passed[e] += f.dr;
@@ -607,17 +710,8 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
   P.pad = (int16_t)e;
   S.procs[pid] = P;
   timeout(S, pid, P.flow, hd);
+  if (rel_e >= 0) ledger_push(S, S.h->now + f.duration, rel_e, f.dr);
   (void)K;
-}
-
-GSC_HD_CALL void run_retlink(Env& S, int pid, const Proc& P) {
-  if (GSC_UNI(P.state) == RL_INIT) {
-    S.procs[pid].state = RL_AFTER;
-    timeout(S, pid, -1, P.y);
-    return;
-  }
-  S.link_rem[GSC_UNI(P.a)] += P.x;
-  proc_return(S, pid, P, 0);
 }
 
 // DefaultFlowProcessor.process_flow (default_processor.py:14-50) + get_processing_delay.
@@ -871,7 +965,6 @@ GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid, int f
     case P_PROCESS: run_process(S, K, T, pid, P, f); break;
     case P_REQUEST: run_request(S, K, pid, P, f); break;
     case P_FINISH: run_finish(S, K, pid, P, f); break;
-    case P_RETLINK: run_retlink(S, pid, P); break;
     case P_ARRIVAL: run_arrival(S, K, T, pid, P); break;
     case P_WRITER: run_writer(S, K, T, pid, P); break;
     case P_MMPP: run_mmpp(S, K, T, pid); break;
@@ -923,7 +1016,11 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
   for (int i = l0; i < N * Sd; i += ls) { S.sf_present[i] = 0; S.placement[i] = 0; S.sf_load[i] = 0; S.sf_start[i] = 0; }
   for (int i = l0; i < N * (Sd + 1); i += ls) S.drop_locs[i] = 0;
   for (int i = l0; i < N * C * Sd * N; i += ls) S.sched[i] = 0.0;
-  for (int e = l0; e < S.d.E; e += ls) { S.link_rem[e] = e < T.E ? T.edge_cap[e] : 0.0; S.link_passed[e] = 0.0; }
+  for (int e = l0; e < S.d.E; e += ls) {
+    S.link_rem[e] = e < T.E ? T.edge_cap[e] : 0.0;
+    S.link_passed[e] = 0.0;
+    S.link_next[e] = 1.0 / 0.0;
+  }
   h->flow_top = S.d.flow_cap;
   for (int i = l0; i < S.d.flow_cap; i += ls) S.flow_free[i] = (int16_t)(S.d.flow_cap - 1 - i);
   h->proc_top = S.d.proc_cap;
@@ -1052,6 +1149,7 @@ GSC_HD void run_until_stop_serial(Env& S, const SimConst& K, const TopoDev& T) {
     const Event ev = S.events[idx];
     remove_event(S, idx);
     S.h->now = ev.t;
+    S.h->cur_key = ev.key;
     if (ev.proc == kStopProc) return;
     dispatch(S, K, T, ev.proc, ev.flow);
   }

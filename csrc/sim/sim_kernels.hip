@@ -250,9 +250,10 @@ __device__ __forceinline__ bool rq_insert(RegQueue<QS>& q, double t, uint32_t ke
 }
 
 template <int QS>
-__device__ __forceinline__ void rq_pop(RegQueue<QS>& q, double& t, int& proc) {
+__device__ __forceinline__ void rq_pop(RegQueue<QS>& q, double& t, int& proc, uint32_t& key) {
   t = pack_t((uint32_t)__builtin_amdgcn_readfirstlane((int)q.tlo[0]), (uint32_t)__builtin_amdgcn_readfirstlane((int)q.thi[0]));
   proc = __builtin_amdgcn_readfirstlane(q.proc[0]);
+  key = (uint32_t)__builtin_amdgcn_readfirstlane((int)q.key[0]);
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     if (s * 64 >= q.n) break;  // remaining sets are empty
@@ -333,7 +334,8 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     }
     double et;
     int ep;
-    rq_pop(q, et, ep);
+    uint32_t ek;
+    rq_pop(q, et, ep, ek);
     const unsigned long long t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (target_proc(ep) == kStopProc) {
       S.h->now = et;
@@ -347,6 +349,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     int n_disp = 0;
     {
       double t = et;
+      uint32_t k = ek;
       int p = target_proc(ep), pf = target_flow(ep);
       // queue head = entry 0 of set 0, held by lane 0
       const double head_t = pack_t((uint32_t)__builtin_amdgcn_readfirstlane((int)q.tlo[0]),
@@ -354,6 +357,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
       const uint32_t head_k = (uint32_t)__builtin_amdgcn_readfirstlane((int)q.key[0]);
       for (;;) {
         S.h->now = t;
+        S.h->cur_key = k;
         const unsigned long long td = prof ? __builtin_amdgcn_s_memtime() : 0;
         const int ptype = prof ? S.procs[p].type * 4 + (S.procs[p].state < 3 ? S.procs[p].state : 3) : 0;
         dispatch(S, K, T, p, pf);
@@ -377,6 +381,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
         if (!(m.t < head_t || (m.t == head_t && m.key < head_k))) break;
         remove_event(S, bi);
         t = m.t;
+        k = m.key;
         p = m.proc;
         pf = m.flow;
       }
@@ -561,6 +566,7 @@ class SimContext {
     D_.flow_cap = dims["flow_cap"].cast<int>();
     D_.proc_cap = dims["proc_cap"].cast<int>();
     D_.event_cap = dims["event_cap"].cast<int>();
+    D_.rel_cap = dims.contains("rel_cap") ? dims["rel_cap"].cast<int>() : D_.flow_cap;
     GSC_CHECK(D_.N <= 256, "at most 256 nodes per topology");
     GSC_CHECK(D_.flow_cap < 32768 && D_.proc_cap < 32768, "pool capacities must be < 32768");
     L_ = make_layout(D_);

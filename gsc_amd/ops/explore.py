@@ -5,9 +5,10 @@ Per env: ``a = unscale(scale(mu(s)) + N(rand_mu, rand_sigma))`` clipped to ``[0,
 twice: zero weights below the threshold and renormalise (all-zero -> uniform ``round(1/P, 10)``,
 residual of the rounded sum added to the first element that can absorb it).
 
-``explore_postprocess`` dispatches to the fused HIP kernel for CUDA tensors (one thread per
-slice, fp64 arithmetic like the reference's Python floats) and to the vectorised PyTorch
-reference below otherwise.
+``explore_postprocess`` dispatches to the fused HIP kernels for CUDA tensors (lane-parallel per
+slice: 32 lanes up to n_pad 32, a wave with up to 4 weights per lane up to n_pad 256; fp64
+arithmetic like the reference's Python floats) and to the vectorised PyTorch reference below
+otherwise.
 """
 from __future__ import annotations
 

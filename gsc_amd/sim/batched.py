@@ -131,7 +131,10 @@ def _default_caps(topos: Sequence[Topology], cfg: dict) -> dict:
     flows = int(min(4096, max(64, 2 * max_ing * per_node)))
     # the pending-event queue lives in VGPRs on the device (64 per set); observed peaks on the reference
     # configs are 30-60 events, so 128 leaves 2x headroom (overflow is flagged, never silent)
-    return dict(flow_cap=flows, proc_cap=min(32000, 3 * flows + 32), event_cap=128 if max_ing <= 8 else 256)
+    # link-capacity returns are a ledger, not processes (csrc/sim/sim_core.h ledger_push): pending returns
+    # are bounded like the flows holding links (overflow is flagged, never silent)
+    return dict(flow_cap=flows, proc_cap=min(32000, 2 * flows + 32), event_cap=128 if max_ing <= 8 else 256,
+                rel_cap=flows)
 
 
 class BatchedSimulator:
@@ -267,8 +270,8 @@ class BatchedSimulator:
     def check_flags(self) -> int:
         flags = int(max(t[4][:, 12].max() for t in self._out_sets).item())
         if flags:
-            raise RuntimeError(f"batched simulator overflow/bad state flags={flags} (caps {self.dims}); "
-                               "increase flow/proc/event capacities")
+            raise RuntimeError(f"batched simulator overflow/bad state flags={flags} (caps {self.dims}; bits: 1 flows, "
+                               "2 processes, 4 events, 8 bad state, 16 link releases); increase the capacities")
         return flags
 
     def action_mask(self, topo_index: int = 0) -> torch.Tensor:

@@ -133,12 +133,15 @@ def test_adam_polyak_matches_reference():
     torch.testing.assert_close(tgt, t2, rtol=1e-6, atol=1e-6)
 
 
-def test_explore_postprocess_device():
+@pytest.mark.parametrize("P,n", [(24, 11), (50, 50), (64, 37), (200, 200), (200, 131)])
+def test_explore_postprocess_device(P, n):
+    """Lane-parallel kernels: two slices per wave (n_pad <= 32), one slice per wave with 1-4 weights per
+    lane (n_pad <= 256, the 50- and 200-node configs)."""
     torch.manual_seed(2)
-    E, P = 64, 24
+    E = 64 if P <= 64 else 8
     A = P * 3 * P
     mask = torch.zeros(E, P, 3, P, device=DEV)
-    mask[:, :11, :, :11] = 1
+    mask[:, :n, :, :n] = 1
     mask = mask.view(E, A)
     mu = torch.rand(E, A, device=DEV) * mask
     for warm in (True, False):
