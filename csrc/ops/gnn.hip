@@ -126,6 +126,27 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
   else gnn_mt_forward(&c, stream, num_cus());
 }
 
+// Two parameter sets on the same graphs (target actor + target critic embedders of next_obs).  One-tile
+// graphs: one launch of 8-wave workgroups holding both weight sets (headline: 108.0k vs 107.2k
+// env-steps/s with two launches).  Two-tile graphs: two launches -- the second weight set's LDS costs
+// the multi-tile kernel a resident workgroup per CU (syn50: 10.1k fused vs 10.6k env-steps/s).
+void gnn_forward2(py::dict tables, uintptr_t params, uintptr_t params2, uintptr_t x, uintptr_t topo, uintptr_t emb,
+                  uintptr_t emb2, int B, int P, int Fin, int H, std::vector<int> layer_of, uintptr_t stream) {
+  GnnPath path;
+  ClArgs c = make_args(tables, params, x, topo, B, P, Fin, H, layer_of, &path);
+  c.emb = ptr<float>(emb);
+  if (path == kPathMf) {
+    c.params2 = ptr<const float>(params2);
+    c.emb2 = ptr<float>(emb2);
+    gnn_mf_forward(&c, stream, num_cus());
+    return;
+  }
+  gnn_mt_forward(&c, stream, num_cus());
+  c.params = ptr<const float>(params2);
+  c.emb = ptr<float>(emb2);
+  gnn_mt_forward(&c, stream, num_cus());
+}
+
 void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo, uintptr_t demb, uintptr_t partials,
                   int max_rows, uintptr_t grad_out, int B, int P, int Fin, int H, std::vector<int> layer_of,
                   uintptr_t stream, uintptr_t blob) {
@@ -161,6 +182,9 @@ void register_gnn(py::module_& m) {
   m.def("gnn_forward", &gnn_forward, py::arg("tables"), py::arg("params"), py::arg("x"), py::arg("topo"), py::arg("emb"),
         py::arg("B"), py::arg("P"), py::arg("Fin"), py::arg("H"), py::arg("layer_of"), py::arg("stream"),
         py::arg("blob") = 0);
+  m.def("gnn_forward2", &gnn_forward2, py::arg("tables"), py::arg("params"), py::arg("params2"), py::arg("x"),
+        py::arg("topo"), py::arg("emb"), py::arg("emb2"), py::arg("B"), py::arg("P"), py::arg("Fin"), py::arg("H"),
+        py::arg("layer_of"), py::arg("stream"));
   m.def("gnn_backward", &gnn_backward, py::arg("tables"), py::arg("params"), py::arg("x"), py::arg("topo"),
         py::arg("demb"), py::arg("partials"), py::arg("max_rows"), py::arg("grad_out"), py::arg("B"), py::arg("P"),
         py::arg("Fin"), py::arg("H"), py::arg("layer_of"), py::arg("stream"), py::arg("blob") = 0);

@@ -49,6 +49,8 @@ struct ClArgs {
   const void* s_src;
   int MP;                    // messages padded to a multiple of 16
   void* blob;                // MFMA path: per-graph forward state saved for the backward (or null)
+  const float* params2;      // forward only: a second parameter set on the same graphs (or null) ...
+  float* emb2;               // ... and its embeddings [B, H] (target actor + target critic in one launch)
 };
 
 __device__ __forceinline__ void cl_wave_sync() {

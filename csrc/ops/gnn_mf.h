@@ -52,9 +52,9 @@ struct MfW {
   bf16x8 l[2], r[2];
 };
 
-__device__ __forceinline__ void mf_load_w(MfW& w, const ClArgs& a, int b, bool trans, int lane) {
+__device__ __forceinline__ void mf_load_w(MfW& w, const ClArgs& a, const float* params, int b, bool trans, int lane) {
   const int Fi = b == 0 ? a.Fin : a.H;
-  const float* src = a.params + cl_block_offset(b, a.Fin, a.H);
+  const float* src = params + cl_block_offset(b, a.Fin, a.H);
   const float* Wl = src;
   const float* Wr = src + a.H * Fi + a.H;
   const int r = lane & 31, hh = lane >> 5;
@@ -65,11 +65,12 @@ __device__ __forceinline__ void mf_load_w(MfW& w, const ClArgs& a, int b, bool t
   }
 }
 
-__device__ __forceinline__ void mf_stage_vec(const ClArgs& a, float* V) {
+__device__ __forceinline__ void mf_stage_vec(const ClArgs& a, float* V, const float* params = nullptr) {
+  if (!params) params = a.params;
   for (int i = threadIdx.x; i < a.n_blocks * kMfVec; i += blockDim.x) {
     const int b = i / kMfVec, j = i - b * kMfVec, which = j >> 5, c = j & 31;
     const int Fi = b == 0 ? a.Fin : a.H;
-    const float* src = a.params + cl_block_offset(b, a.Fin, a.H);
+    const float* src = params + cl_block_offset(b, a.Fin, a.H);
     const int off = which == 0 ? a.H * Fi : (which == 1 ? 2 * a.H * Fi + a.H : 2 * a.H * Fi + a.H * which);
     V[i] = c < a.H ? src[off + c] : 0.f;
   }
@@ -78,11 +79,12 @@ __device__ __forceinline__ void mf_stage_vec(const ClArgs& a, float* V) {
 // Weight fragments staged once per workgroup, lane-linear (conflict-free ds_read_b128): set 0 =
 // encoder, 1 = process block, 2 = process block transposed (backward's dh).  Read back per layer
 // (mf_frags) instead of living in VGPRs for the whole kernel.
-__device__ __forceinline__ void mf_stage_frags(const ClArgs& a, bf16x8* img, int nsets) {
+__device__ __forceinline__ void mf_stage_frags(const ClArgs& a, bf16x8* img, int nsets, const float* params = nullptr) {
+  if (!params) params = a.params;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
   for (int f = wave; f < nsets; f += waves) {
     MfW w;
-    mf_load_w(w, a, f == 0 ? 0 : 1, f == 2, lane);
+    mf_load_w(w, a, params, f == 0 ? 0 : 1, f == 2, lane);
     img[(f * 4 + 0) * 64 + lane] = w.l[0];
     img[(f * 4 + 1) * 64 + lane] = w.l[1];
     img[(f * 4 + 2) * 64 + lane] = w.r[0];

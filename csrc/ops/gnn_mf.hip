@@ -209,15 +209,25 @@ __device__ __forceinline__ void mf_load_x(const ClArgs& a, int g, int n, __bf16*
   cl_wave_sync();
 }
 
-template <int HPF, bool K2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gnn_mf_fwd_kernel(ClArgs a, MfLayout m) {
+// NSETS = 2: a second parameter set (a.params2 -> a.emb2) on the same graphs in the same launch (the
+// target actor's and the target critic's embedders of next_obs): one topology / input load per graph.
+// (NSETS = 2 runs 8-wave workgroups: the second set's weights cost 9 KB of LDS per workgroup, which
+// 4-wave workgroups would pay with a quarter fewer resident waves)
+template <int HPF, bool K2, int NSETS>
+__global__ __launch_bounds__(NSETS == 2 ? 512 : 256) __attribute__((amdgpu_waves_per_eu(4))) void gnn_mf_fwd_kernel(
+    ClArgs a, MfLayout m) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  mf_stage_vec(a, lds);
-  const bf16x8* frags = reinterpret_cast<const bf16x8*>(lds + mf_vec_floats(a.n_blocks));
-  mf_stage_frags(a, reinterpret_cast<bf16x8*>(lds + mf_vec_floats(a.n_blocks)), 2);
+  // per parameter set: [bl br att bias per block][fragment sets: encoder, process]
+  const int set_floats = mf_vec_floats(a.n_blocks) + 2 * kMfFragSet;
+#pragma unroll
+  for (int ws = 0; ws < NSETS; ++ws) {
+    const float* P = ws == 0 ? a.params : a.params2;
+    mf_stage_vec(a, lds + ws * set_floats, P);
+    mf_stage_frags(a, reinterpret_cast<bf16x8*>(lds + ws * set_floats + mf_vec_floats(a.n_blocks)), 2, P);
+  }
   __syncthreads();
-  char* const W0 = reinterpret_cast<char*>(lds + mf_vec_floats(a.n_blocks) + 2 * kMfFragSet);
+  char* const W0 = reinterpret_cast<char*>(lds + NSETS * set_floats);
   int woff = wave * m.per_wave;
   MfTopo T;
   mf_bind_topo(T, W0 + woff + m.topo, a);
@@ -238,30 +248,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     T.deg = reinterpret_cast<float*>(T.idst + a.M);
     mf_load_topo(T, a, a.topo[g], lane);
     const int n = T.n;
-    mf_load_x<false>(a, g, n, hA, nullptr, E, m.NV, m.NVS, lane);
-    __bf16* hin = hA;
-    __bf16* hout = hB;
-    float pool = 0.f;
-    for (int l = 0; l < a.L; ++l) {
-      const float* vec = lds + (l == 0 ? 0 : kMfVec);
-      if (l + 1 < a.L) {
-        if (l == 0)
-          mf_layer<HPF, false, 0, false>(mf_frags(frags, 0, lane), vec, T, hin, xl, xr, al, mx, sm, E, hout, nullptr,
-                                         m.NV, m.NVS, a.H, lane);
-        else
-          mf_layer<HPF, K2, 0, false>(mf_frags(frags, 1, lane), vec, T, hin, xl, xr, al, mx, sm, E, hout, nullptr,
-                                      m.NV, m.NVS, a.H, lane);
-        __bf16* t = hin;
-        hin = hout;
-        hout = t;
-      } else {
-        pool = mf_layer<HPF, K2, 1, false>(mf_frags(frags, 1, lane), vec, T, hin, xl, xr, al, mx, sm, E, nullptr,
-                                           nullptr, m.NV, m.NVS, a.H, lane);
+    for (int ws = 0; ws < NSETS; ++ws) {
+      const float* S0 = lds + ws * set_floats;
+      const bf16x8* frags = reinterpret_cast<const bf16x8*>(S0 + mf_vec_floats(a.n_blocks));
+      // the input image (and the cleared aggregation matrix) for this parameter set
+      mf_load_x<false>(a, g, n, hA, nullptr, E, m.NV, m.NVS, lane);
+      __bf16* hin = hA;
+      __bf16* hout = hB;
+      float pool = 0.f;
+      for (int l = 0; l < a.L; ++l) {
+        const float* vec = S0 + (l == 0 ? 0 : kMfVec);
+        if (l + 1 < a.L) {
+          if (l == 0)
+            mf_layer<HPF, false, 0, false>(mf_frags(frags, 0, lane), vec, T, hin, xl, xr, al, mx, sm, E, hout, nullptr,
+                                           m.NV, m.NVS, a.H, lane);
+          else
+            mf_layer<HPF, K2, 0, false>(mf_frags(frags, 1, lane), vec, T, hin, xl, xr, al, mx, sm, E, hout, nullptr,
+                                        m.NV, m.NVS, a.H, lane);
+          __bf16* t = hin;
+          hin = hout;
+          hout = t;
+        } else {
+          pool = mf_layer<HPF, K2, 1, false>(mf_frags(frags, 1, lane), vec, T, hin, xl, xr, al, mx, sm, E, nullptr,
+                                             nullptr, m.NV, m.NVS, a.H, lane);
+        }
       }
+      pool += __shfl_xor(pool, 32);
+      float* emb = ws == 0 ? a.emb : a.emb2;
+      if (half == 0 && c < a.H) emb[(long)g * a.H + c] = pool / (float)n;
+      cl_wave_sync();
     }
-    pool += __shfl_xor(pool, 32);
-    if (half == 0 && c < a.H) a.emb[(long)g * a.H + c] = pool / (float)n;
-    cl_wave_sync();
   }
 }
 
@@ -724,22 +740,27 @@ bool gnn_mf_supported(int Fin, int H, int NM, int L, int n_blocks, const int* la
 
 template <int HPF, bool K2>
 static void mf_launch_fwd(ClArgs a, hipStream_t st, int cus) {
-  const bool save = a.blob != nullptr;
+  const bool save = a.blob != nullptr, two = a.params2 != nullptr;
+  GSC_CHECK(!(save && two), "the saving forward takes one parameter set");
   const MfLayout m = mf_layout(a, save ? kMfLaySave : kMfLayFwd, HPF);
-  a.waves = 4;
-  const size_t lds = sizeof(float) * (mf_vec_floats(a.n_blocks) + 2 * kMfFragSet) + (size_t)a.waves * m.per_wave;
+  a.waves = two ? 8 : 4;
+  const size_t lds = sizeof(float) * (two ? 2 : 1) * (mf_vec_floats(a.n_blocks) + 2 * kMfFragSet) +
+                     (size_t)a.waves * m.per_wave;
   GSC_CHECK(lds <= 160 * 1024, "GNN (MFMA) forward working set exceeds LDS");
-  const void* fn = save ? (const void*)gnn_mf_fwd_save_kernel<HPF, K2> : (const void*)gnn_mf_fwd_kernel<HPF, K2>;
+  const void* fn = save ? (const void*)gnn_mf_fwd_save_kernel<HPF, K2>
+                        : (two ? (const void*)gnn_mf_fwd_kernel<HPF, K2, 2> : (const void*)gnn_mf_fwd_kernel<HPF, K2, 1>);
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = (int)((160 * 1024) / lds);
-  if (per_cu > 4) per_cu = 4;  // 4 waves/SIMD (VGPR budget)
+  if (per_cu * a.waves > 16) per_cu = 16 / a.waves;  // 4 waves/SIMD (VGPR budget)
   const int need = (a.B + a.waves - 1) / a.waves;
   const int cap = cus * (per_cu > 0 ? per_cu : 1);
   const int grid = need < cap ? need : cap;
   if (save)
     hipLaunchKernelGGL((gnn_mf_fwd_save_kernel<HPF, K2>), dim3(grid > 0 ? grid : 1), dim3(64 * a.waves), lds, st, a, m);
+  else if (two)
+    hipLaunchKernelGGL((gnn_mf_fwd_kernel<HPF, K2, 2>), dim3(grid > 0 ? grid : 1), dim3(64 * a.waves), lds, st, a, m);
   else
-    hipLaunchKernelGGL((gnn_mf_fwd_kernel<HPF, K2>), dim3(grid > 0 ? grid : 1), dim3(64 * a.waves), lds, st, a, m);
+    hipLaunchKernelGGL((gnn_mf_fwd_kernel<HPF, K2, 1>), dim3(grid > 0 ? grid : 1), dim3(64 * a.waves), lds, st, a, m);
   check_launch();
 }
 

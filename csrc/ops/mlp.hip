@@ -568,23 +568,29 @@ struct Cfg {
   int RM, RN, WM, WN;
 };
 
-template <int RM, int RN, int WM, int WN, bool A_COL, bool B_KN>
+template <int RM, int RN, int WM, int WN, int BK, bool A_COL, bool B_KN>
 static void launch_cfg(const GemmArgs& g, int splits, hipStream_t s) {
-  constexpr int BK = 32;
   constexpr int BM = 32 * RM * WM, BN = 32 * RN * WN;
   dim3 grid((g.M + BM - 1) / BM, (g.N + BN - 1) / BN, splits);
   hipLaunchKernelGGL((gemm_kernel<RM, RN, WM, WN, BK, A_COL, B_KN>), grid, dim3(256), 0, s, g);
   check_launch();
 }
 
-// tile shapes: 0 = 128x128 (2x2 waves of 64x64), 1 = 128x64 (4x1 waves of 32x64), 2 = 64x64 (2x2 of 32x32)
-template <bool A_COL, bool B_KN>
-static void launch_layout(const GemmArgs& g, int tile, int splits, hipStream_t s) {
+// tile shapes: 0 = 128x128 (2x2 waves of 64x64), 1 = 128x64 (4x1 waves of 32x64), 2 = 64x64 (2x2 of 32x32),
+// 3 = 64x128 (2x2 waves of 32x64); K staged BK = 32 or 64 deep per barrier
+template <bool A_COL, bool B_KN, int BK>
+static void launch_layout_bk(const GemmArgs& g, int tile, int splits, hipStream_t s) {
   switch (tile) {
-    case 0: launch_cfg<2, 2, 2, 2, A_COL, B_KN>(g, splits, s); break;
-    case 1: launch_cfg<1, 2, 4, 1, A_COL, B_KN>(g, splits, s); break;
-    default: launch_cfg<1, 1, 2, 2, A_COL, B_KN>(g, splits, s); break;
+    case 0: launch_cfg<2, 2, 2, 2, BK, A_COL, B_KN>(g, splits, s); break;
+    case 1: launch_cfg<1, 2, 4, 1, BK, A_COL, B_KN>(g, splits, s); break;
+    case 3: launch_cfg<1, 2, 2, 2, BK, A_COL, B_KN>(g, splits, s); break;
+    default: launch_cfg<1, 1, 2, 2, BK, A_COL, B_KN>(g, splits, s); break;
   }
+}
+template <bool A_COL, bool B_KN>
+static void launch_layout(const GemmArgs& g, int tile, int bk, int splits, hipStream_t s) {
+  if (bk == 64) launch_layout_bk<A_COL, B_KN, 64>(g, tile, splits, s);
+  else launch_layout_bk<A_COL, B_KN, 32>(g, tile, splits, s);
 }
 
 static Operand operand(uintptr_t p, long ld, int dtype) {
@@ -638,7 +644,7 @@ void gemm(int layout, int M, int N, int K, uintptr_t a, long lda, int adt, uintp
   e.vec16 = e.c16 && (gp("c16") % 16 == 0) && (e.ldc16 % 8 == 0);
   const int tile = ep.contains("tile") ? ep["tile"].cast<int>() : 0;
   int splits = ep.contains("splits") ? ep["splits"].cast<int>() : 1;
-  constexpr int BK = 32;
+  const int BK = ep.contains("bk") && ep["bk"].cast<int>() == 64 ? 64 : 32;
   g.kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
   if (g.kchunk < BK) g.kchunk = BK;
   splits = (K + g.kchunk - 1) / g.kchunk;
@@ -650,15 +656,15 @@ void gemm(int layout, int M, int N, int K, uintptr_t a, long lda, int adt, uintp
   GSC_CHECK(!(e.accumulate && splits > 1), "accumulate with split-K: accumulate in splitk_reduce");
   const hipStream_t s = stream_of(stream);
   switch (layout) {
-    case 0: launch_layout<false, false>(g, tile, splits, s); break;  // A_ROW, B_NK
-    case 1: launch_layout<true, true>(g, tile, splits, s); break;    // A_COL, B_KN (weight gradient)
-    case 2: launch_layout<false, true>(g, tile, splits, s); break;   // A_ROW, B_KN (input gradient)
+    case 0: launch_layout<false, false>(g, tile, BK, splits, s); break;  // A_ROW, B_NK
+    case 1: launch_layout<true, true>(g, tile, BK, splits, s); break;    // A_COL, B_KN (weight gradient)
+    case 2: launch_layout<false, true>(g, tile, BK, splits, s); break;   // A_ROW, B_KN (input gradient)
     default: GSC_CHECK(false, "unknown gemm layout");
   }
 }
 
-int gemm_splits(int K, int splits) {
-  constexpr int BK = 32;
+int gemm_splits(int K, int splits, int bk) {
+  const int BK = bk == 64 ? 64 : 32;
   int kchunk = ((K + splits - 1) / splits + BK - 1) / BK * BK;
   if (kchunk < BK) kchunk = BK;
   return (K + kchunk - 1) / kchunk;
@@ -695,7 +701,8 @@ void rowdot(uintptr_t x, long ldx, int T, uintptr_t W, long ldw, int N, int A, u
 void register_mlp(py::module_& m) {
   m.def("gemm", &mlp::gemm, "bf16 MFMA GEMM with fused epilogue (layout 0: A[M,K] B[N,K]; 1: A[K,M] B[K,N]; "
                             "2: A[M,K] B[K,N])");
-  m.def("gemm_splits", &mlp::gemm_splits, "effective split-K count for K and a requested split count");
+  m.def("gemm_splits", &mlp::gemm_splits, py::arg("K"), py::arg("splits"), py::arg("bk") = 32,
+        "effective split-K count for K and a requested split count");
   m.def("splitk_reduce", &mlp::splitk_reduce, "deterministic sum of split-K fp32 slabs into a strided output");
   m.def("cast2d", &mlp::cast2d, "fp32 -> bf16 strided 2-D copy");
   m.def("rowdot", &mlp::rowdot, "out[t][n] = sum_a x[t][a] W[n][a] (mask fold of a first layer, small GEMVs)");

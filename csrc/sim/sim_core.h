@@ -422,7 +422,33 @@ GSC_HD_CALL void ledger_apply(Env& S, int e) {
   const uint32_t ck = S.h->cur_key;
 #if defined(__HIP_DEVICE_COMPILE__)
   const int lane = wave_lane();
-  for (;;) {
+  {
+    // fast path (at most 64 pending returns, exactly one of them due): one entry per lane, the due
+    // one found by a ballot, link_next from the same pass
+    const int nr = GSC_UNI(S.h->n_rel);
+    if (nr <= 64) {
+      Release r;
+      r.t = 1.0 / 0.0;
+      r.dr = 0.0;
+      r.edge = -1;
+      r.key = 0xffffffffu;
+      if (lane < nr) r = S.rel[lane];
+      const bool mine = r.edge == e;
+      const unsigned long long due = __ballot(mine && key_less(r.t, r.key, now, ck));
+      if (due == 0) return;  // returns of link e at this time with a later key: nothing to apply
+      if (__popcll(due) == 1) {
+        const int idx = (int)__ffsll((long long)due) - 1;
+        S.link_rem[e] += readlane_f64(r.dr, idx);
+        S.link_next[e] = -wave_max_f64(-(mine && lane != idx ? r.t : 1.0 / 0.0));
+        const int last = nr - 1;
+        if (idx != last) S.rel[idx] = S.rel[last];
+        S.h->n_rel = last;
+        __builtin_amdgcn_wave_barrier();
+        return;
+      }
+    }
+  }
+  for (;;) {  // general case: repeatedly the smallest due entry (wave min over (t, key))
     const int nr = GSC_UNI(S.h->n_rel);
     double bt = 1.0 / 0.0;
     uint32_t bk = 0xffffffffu;

@@ -169,6 +169,17 @@ class NativeDDPGUpdate:
                              self.P, self.Fin, self.H, self.layer_of, self._stream(),
                              save.data_ptr() if save is not None else 0)
 
+    def _gnn_fwd2(self, na: _Net, nb: _Net, x: torch.Tensor, out_a: torch.Tensor, out_b: torch.Tensor) -> None:
+        """Two embedders on the same graphs (target actor + target critic on next_obs): one launch of the
+        fused MFMA kernels (one topology / input load per graph); two layer-wise passes otherwise."""
+        if self.layerwise:
+            self._gnn_fwd(na, x, out_a, None)
+            self._gnn_fwd(nb, x, out_b, None)
+            return
+        self.nat.gnn_forward2(self.tables, na.emb_ptr(), nb.emb_ptr(), x.data_ptr(), self.topo32.data_ptr(),
+                              out_a.data_ptr(), out_b.data_ptr(), self.B, self.P, self.Fin, self.H, self.layer_of,
+                              self._stream())
+
     def _gnn_bwd(self, net: _Net, x: torch.Tensor, demb: torch.Tensor, blob: torch.Tensor, key: str = "-") -> None:
         # the embedder gradient is the first run of the network's flat gradient buffer
         if self.layerwise:
@@ -270,15 +281,15 @@ class NativeDDPGUpdate:
         """TD target (target nets) + critic loss + all critic gradients into ``critic_flat.grad``."""
         H, A = self.H, self.A
         ta, tc, c = self.tactor, self.tcritic, self.critic
+        # target actor and target critic embedders on s' (one launch)
+        self._gnn_fwd2(ta, tc, b.next_obs, self.emb["ta"], self.emb["tc"])
         # target actor on s'
-        self._gnn_fwd(ta, b.next_obs, self.emb["ta"], None)
         self._first(ta, self.emb["ta"], self._rowtab(ta, "ta"), self.hid_ta[0])
         self._hidden_fwd(ta, self.hid_ta)
         last = ta.nh
         gemm(self.hid_ta[last - 1], ta.w16(last), "nt", out16=self.act_buf, bias=ta.b32(last), colmask=self.masks,
              topo=self.topo32, clamp=(-1.0, 1.0))
         # target critic on (s', a')
-        self._gnn_fwd(tc, b.next_obs, self.emb["tc"], None)
         self._first(tc, self.emb["tc"], self._rowtab(tc, "tc"), self.hid_c[0], extra=self.act_buf,
                     wa=self._wa(tc, "tc"))
         self._hidden_fwd(tc, self.hid_c)

@@ -27,7 +27,7 @@ def _ld(t: torch.Tensor) -> int:
     return t.stride(0)
 
 
-_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64)}
+_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 64), 3: (64, 128)}
 
 
 _TILE_POLICY = os.environ.get("GSC_GEMM_TILE", "small")
@@ -66,7 +66,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str = "nt", *, out16: Optiona
          rowscale: Optional[torch.Tensor] = None, relu: bool = False,
          clamp=None, accumulate: bool = False, splits: Optional[int] = 1, slabs: Optional[torch.Tensor] = None,
          aug_t: int = -1, aug_topo: Optional[torch.Tensor] = None, tile: Optional[int] = None,
-         stream: Optional[int] = None) -> None:
+         bk: Optional[int] = None, stream: Optional[int] = None) -> None:
     """See module docstring.  ``splits=None`` picks a split-K count (needs ``slabs``).  ``aug_t >= 0`` appends ``1 + aug_t`` virtual columns to ``b`` (layouts
     tn/nn): a ones column and the one-hot of ``aug_topo`` (the row topology of ``b``)."""
     nat = load_native()
@@ -112,9 +112,14 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str = "nt", *, out16: Optiona
     if clamp is not None:
         ep["clamp"] = (float(clamp[0]), float(clamp[1]))
     tile = pick_tile(M, N) if tile is None else int(tile)
+    if bk is None:
+        # K staged 32 deep per barrier.  BK = 64 is faster for two products in isolation (scripts/gemm_tune.py,
+        # B = 25,600: [B,256]x[1728,256]^T 88.4 vs 93.0 us, [B,64]^T[B,1728] 40.0 vs 41.0 us) but lost in the
+        # training step beside the concurrent kernels (bench.py 106.3k vs 106.9k env-steps/s)
+        bk = 32
     if splits is None:
         splits = auto_splits(M, N, K, tile, slabs.numel()) if slabs is not None else 1
-    eff = nat.gemm_splits(K, splits) if splits > 1 else 1
+    eff = nat.gemm_splits(K, splits, bk) if splits > 1 else 1
     if accumulate and eff == 1:
         ep["accumulate"] = 1
     if eff > 1:
@@ -130,6 +135,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str = "nt", *, out16: Optiona
             assert out16.dtype == torch.bfloat16
             ep.update(c16=out16.data_ptr(), ldc16=_ld(out16))
     ep["tile"] = tile
+    ep["bk"] = int(bk)
     s = torch.cuda.current_stream(a.device).cuda_stream if stream is None else stream
     nat.gemm(lay, M, N, K, a.data_ptr(), _ld(a), _DT[a.dtype], b.data_ptr(), _ld(b), _DT[b.dtype], ep, s)
     if eff > 1:

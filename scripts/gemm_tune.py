@@ -1,0 +1,59 @@
+#!/usr/bin/env python
+"""Time the MFMA GEMM engine (csrc/ops/mlp.hip) at the DDPG learner's shapes (B = 25,600, Abilene /
+sample agent) for every output tile x K-stage depth, next to hipBLASLt (torch.mm) as a yardstick."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch
+
+from gsc_amd.ops.mlp import gemm
+
+
+def t(fn, n=20):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e3
+
+
+B = 25600
+dev = "cuda"
+bf = torch.bfloat16
+cases = [  # (name, layout, a, b, kwargs)
+    ("actor out  [B,256]x[1728,256]^T -> bf16", "nt", (B, 256), (1728, 256), {}),
+    ("critic act [B,1728]x[64,1728]^T -> f32", "nt", (B, 1728), (64, 1728), {"o32": True}),
+    ("critic dW  [B,64]^T x [B,1728]", "tn", (B, 64), (B, 1728), {"o32": True, "split": True}),
+    ("actor hid  [B,22]x[256,22]^T -> bf16", "nt", (B, 22), (256, 22), {}),
+    ("dX  [B,64]x[64,256] -> bf16", "nn", (B, 64), (64, 256), {}),
+]
+slabs = torch.empty(16 << 20, device=dev)
+for name, lay, sa, sb, kw in cases:
+    a = torch.randn(*sa, device=dev, dtype=bf)
+    b = torch.randn(*sb, device=dev, dtype=bf)
+    if lay == "nt":
+        M, N = sa[0], sb[0]
+    elif lay == "tn":
+        M, N = sa[1], sb[1]
+    else:
+        M, N = sa[0], sb[1]
+    o16 = torch.empty(M, N, device=dev, dtype=bf)
+    o32 = torch.empty(M, N, device=dev)
+    res = {}
+    for tile in (0, 1, 2, 3):
+        for bk in (32, 64):
+            f = lambda: gemm(a, b, lay, out16=None if kw.get("o32") else o16, out32=o32 if kw.get("o32") else None,
+                             tile=tile, bk=bk, splits=None if kw.get("split") else 1, slabs=slabs)
+            res[f"t{tile}/bk{bk}"] = t(f)
+    ref = {"nt": lambda: torch.mm(a, b.t()), "tn": lambda: torch.mm(a.t(), b), "nn": lambda: torch.mm(a, b)}[lay]
+    res["hipblaslt"] = t(ref)
+    best = min((v, k) for k, v in res.items() if k != "hipblaslt")
+    print(f"{name}: " + "  ".join(f"{k} {v:.1f}" for k, v in res.items()) + f"  | best {best[1]} {best[0]:.1f} us",
+          flush=True)

@@ -64,6 +64,33 @@ def test_gnn_50_nodes_padded_50():
 
 
 @pytest.mark.parametrize("mid", [False, True], ids=["one-tile", "two-tile"])
+def test_gnn_forward_two_parameter_sets(mid):
+    """gnn_forward2 (target actor + target critic embedders in one launch) == two gnn_forward launches."""
+    from gsc_amd.native import load
+    from gsc_amd.ops.gnn import _flat, _layer_of, _tables
+    nat = load()
+    torch.manual_seed(4)
+    gs = _mid_graphs(DEV) if mid else _graphs(DEV)
+    P = 64 if mid else 24
+    e1, e2 = GNNEmbedder(3, 22, 2, "mean", 2).to(DEV), GNNEmbedder(3, 22, 2, "mean", 2).to(DEV)
+    p1, p2 = _flat(e1.flat_parameters()).contiguous(), _flat(e2.flat_parameters()).contiguous()
+    B = 1000
+    topo = torch.randint(0, gs.num_topologies, (B,), device=DEV, dtype=torch.int32)
+    x = torch.rand(B, P, 3, device=DEV) * gs.node_mask[topo.long()].unsqueeze(-1)
+    s = torch.cuda.current_stream().cuda_stream
+    ref = [torch.empty(B, 22, device=DEV) for _ in range(2)]
+    for p, o in zip((p1, p2), ref):
+        nat.gnn_forward(_tables(gs), p.data_ptr(), x.data_ptr(), topo.data_ptr(), o.data_ptr(), B, P, 3, 22,
+                        _layer_of(e1), s, 0)
+    got = [torch.empty(B, 22, device=DEV) for _ in range(2)]
+    nat.gnn_forward2(_tables(gs), p1.data_ptr(), p2.data_ptr(), x.data_ptr(), topo.data_ptr(), got[0].data_ptr(),
+                     got[1].data_ptr(), B, P, 3, 22, _layer_of(e1), s)
+    torch.cuda.synchronize()
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("mid", [False, True], ids=["one-tile", "two-tile"])
 def test_gnn_mfma_deterministic(mid):
     """MFMA gradients are bitwise reproducible (per-workgroup partial rows, fixed-order sums)."""
     torch.manual_seed(3)
