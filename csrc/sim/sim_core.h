@@ -439,7 +439,12 @@ GSC_HD_CALL void ledger_apply(Env& S, int e) {
       if (__popcll(due) == 1) {
         const int idx = (int)__ffsll((long long)due) - 1;
         S.link_rem[e] += readlane_f64(r.dr, idx);
-        S.link_next[e] = -wave_max_f64(-(mine && lane != idx ? r.t : 1.0 / 0.0));
+        // link_next = the earliest remaining return of link e: usually none or one (no wave reduction)
+        const unsigned long long rest = __ballot(mine && lane != idx);
+        const int nrest = __popcll(rest);
+        S.link_next[e] = nrest == 0 ? 1.0 / 0.0
+                         : nrest == 1 ? readlane_f64(r.t, (int)__ffsll((long long)rest) - 1)
+                                      : -wave_max_f64(-(mine && lane != idx ? r.t : 1.0 / 0.0));
         const int last = nr - 1;
         if (idx != last) S.rel[idx] = S.rel[last];
         S.h->n_rel = last;
