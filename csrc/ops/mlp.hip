@@ -28,6 +28,7 @@
 // Reference shapes: src/rlsp/agents/models.py:80-92 (critic MLP), 115-122 + 146-154 (actor MLP);
 // the update math of simple_ddpg.py:204-234 is composed from these kernels in gsc_amd/ops/mlp.py.
 #include <hip/hip_bf16.h>
+#include <algorithm>
 #include <pybind11/pybind11.h>
 
 #include "../common.h"
@@ -375,24 +376,72 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* slabs, 
   }
 }
 
-// out[t][n] = sum_a x[t][a] W[n][a]: the per-topology fold of a 0/1 mask block of a first-layer weight
-// (x = masks, W = the mask columns) and small GEMVs (x = a bias vector).  One workgroup per (t, n):
-// 256 lanes over a, fixed-order tree reduction (deterministic).
+// out[t][n] (row stride ldo) = sum_a x[t][a] W[n][a]: the per-topology fold of a 0/1 mask block of a
+// first-layer weight (x = masks [T][A], W = the mask columns) and small GEMVs (x = a bias vector).
+// Grid (N, S): workgroup (n, z) reads row n of W once over its A-chunk for TT topologies at a time (W is
+// the HBM stream; the x rows stay in L2), bf16 pairs when the row is 4-byte aligned.  S > 1 writes
+// partials [S][T][N] for splitk_reduce (fixed order: deterministic).
+template <int TT>
 __global__ __launch_bounds__(256) void rowdot_kernel(const float* x, long ldx, int T, const __hip_bfloat16* W,
-                                                     long ldw, int N, int A, float* out, long ldo) {
-  __shared__ float red[4];
+                                                     long ldw, int N, int A, int achunk, int pair, float* out,
+                                                     long ldo) {
+  __shared__ float red[4][TT];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const long gw = blockIdx.x;
-  const int t = (int)(gw / N), n = (int)(gw - (long)t * N);
-  const float* xr = x + (long)t * ldx;
+  const int n = blockIdx.x, z = blockIdx.y;
+  const int a0 = z * achunk, a1 = min(A, a0 + achunk);
   const __hip_bfloat16* wr = W + (long)n * ldw;
-  float s = 0.f;
-  for (int a = threadIdx.x; a < A; a += 256) s += xr[a] * __bfloat162float(wr[a]);
+  for (int t0 = 0; t0 < T; t0 += TT) {
+    float s[TT];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-  if (lane == 0) red[wv] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) out[(long)t * ldo + n] = (red[0] + red[1]) + (red[2] + red[3]);
+    for (int t = 0; t < TT; ++t) s[t] = 0.f;
+    if (pair) {
+      for (int a = a0 + 2 * (int)threadIdx.x; a < a1; a += 512) {
+        const __hip_bfloat162 w2 = *reinterpret_cast<const __hip_bfloat162*>(wr + a);
+        const float w0 = __low2float(w2), w1 = a + 1 < a1 ? __high2float(w2) : 0.f;
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+          if (t0 + t < T) {
+            const float2 xv = *reinterpret_cast<const float2*>(x + (long)(t0 + t) * ldx + a);
+            s[t] += xv.x * w0 + xv.y * w1;
+          }
+        }
+      }
+    } else {
+      for (int a = a0 + (int)threadIdx.x; a < a1; a += 256) {
+        const float w0 = __bfloat162float(wr[a]);
+#pragma unroll
+        for (int t = 0; t < TT; ++t)
+          if (t0 + t < T) s[t] += x[(long)(t0 + t) * ldx + a] * w0;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s[t] += __shfl_xor(s[t], off);
+      if (lane == 0) red[wv][t] = s[t];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < TT && t0 + (int)threadIdx.x < T) {
+      const int t = threadIdx.x;
+      const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+      if (gridDim.y == 1) out[(long)(t0 + t) * ldo + n] = v;
+      else out[((long)z * T + t0 + t) * N + n] = v;  // partial slab z
+    }
+    __syncthreads();
+  }
+}
+
+// dst[r][t C + c] = (topo[r] == t) ? src[r][c] : 0  (bf16): the per-topology block expansion of an
+// activation / gradient, so a product with per-topology matrices becomes one GEMM over K = T C.
+__global__ __launch_bounds__(256) void topo_expand_kernel(const __hip_bfloat16* src, long lds_, __hip_bfloat16* dst,
+                                                          long ldd, int R, int C, int T, const int* topo) {
+  const long total = (long)R * T * C;
+  const int TC = T * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / TC), j = (int)(i - (long)r * TC);
+    const int t = j / C, c = j - t * C;
+    dst[(long)r * ldd + j] = topo[r] == t ? src[(long)r * lds_ + c] : __float2bfloat16(0.f);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -687,12 +736,39 @@ void cast2d(uintptr_t src, long lds_, uintptr_t dst, long ldd, int R, int C, uin
   check_launch();
 }
 
+// ws (optional, >= S T N floats): A split over S workgroups per row when N alone gives a small grid.
 void rowdot(uintptr_t x, long ldx, int T, uintptr_t W, long ldw, int N, int A, uintptr_t out, long ldo,
-            uintptr_t stream) {
-  const long blocks = (long)T * N;
-  if (blocks <= 0) return;
-  hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)blocks), dim3(256), 0, stream_of(stream),
-                     ptr<const float>(x), ldx, T, ptr<const __hip_bfloat16>(W), ldw, N, A, ptr<float>(out), ldo);
+            uintptr_t stream, uintptr_t ws, long ws_floats) {
+  if ((long)T * N <= 0) return;
+  int S = 1;
+  if (ws) {
+    S = (2048 + N - 1) / N;
+    S = std::min(S, std::max(1, A / 2048));
+    S = std::min(S, 64);
+    while (S > 1 && (long)S * T * N > ws_floats) --S;
+  }
+  int achunk = (A + S - 1) / S;
+  achunk = (achunk + 1) & ~1;
+  S = (A + achunk - 1) / achunk;
+  const int pair = (W % 4 == 0) && (ldw % 2 == 0) && (x % 8 == 0) && (ldx % 2 == 0) && (A % 2 == 0);
+  const hipStream_t s = stream_of(stream);
+  float* dst = S > 1 ? ptr<float>(ws) : ptr<float>(out);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)N, (unsigned)S), dim3(256), 0, s, ptr<const float>(x), ldx, T,
+                       ptr<const __hip_bfloat16>(W), ldw, N, A, achunk, pair, dst, ldo);
+  };
+  if (T <= 1) go(rowdot_kernel<1>);
+  else if (T <= 2) go(rowdot_kernel<2>);
+  else if (T <= 4) go(rowdot_kernel<4>);
+  else go(rowdot_kernel<8>);
+  check_launch();
+  if (S > 1) splitk_reduce(ws, (long)T * N, S, T, N, N, out, ldo, 1.f, 0, stream);
+}
+
+void topo_expand(uintptr_t src, long lds_, uintptr_t dst, long ldd, int R, int C, int T, uintptr_t topo,
+                 uintptr_t stream) {
+  hipLaunchKernelGGL(topo_expand_kernel, dim3(grid_for((long)R * T * C)), dim3(256), 0, stream_of(stream),
+                     ptr<const __hip_bfloat16>(src), lds_, ptr<__hip_bfloat16>(dst), ldd, R, C, T, ptr<const int>(topo));
   check_launch();
 }
 
@@ -705,7 +781,10 @@ void register_mlp(py::module_& m) {
         "effective split-K count for K and a requested split count");
   m.def("splitk_reduce", &mlp::splitk_reduce, "deterministic sum of split-K fp32 slabs into a strided output");
   m.def("cast2d", &mlp::cast2d, "fp32 -> bf16 strided 2-D copy");
-  m.def("rowdot", &mlp::rowdot, "out[t][n] = sum_a x[t][a] W[n][a] (mask fold of a first layer, small GEMVs)");
+  m.def("rowdot", &mlp::rowdot, "out[t][n] = sum_a x[t][a] W[n][a] (mask fold of a first layer, small GEMVs)",
+        py::arg("x"), py::arg("ldx"), py::arg("T"), py::arg("W"), py::arg("ldw"), py::arg("N"), py::arg("A"),
+        py::arg("out"), py::arg("ldo"), py::arg("stream"), py::arg("ws") = 0, py::arg("ws_floats") = 0);
+  m.def("topo_expand", &mlp::topo_expand, "dst[r][t C + c] = (topo[r] == t) src[r][c] (bf16 per-topology blocks)");
   m.def("mlp_head", &mlp::head, "critic output layer + TD target / critic loss / actor loss (fused)");
   m.def("first_layer_grad", &mlp::first_layer_grad, "first-layer weight/bias/mask-block gradient from the aug GEMM");
   m.def("copy2d", &mlp::copy2d, "bf16 strided 2-D copy with optional column mask");

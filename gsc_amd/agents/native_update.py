@@ -19,10 +19,13 @@ preallocated, so the whole update is captured into HIP graphs.  Manual backward 
     hidden        h = relu(x W^T + b):  dW = dh^T x,  db = dh^T 1,  dx = (dh W) * (x > 0)
     actor output  a = (h W^T + b) * mask[topo]           (target: clamped to [-1, 1])
 
-The actor loss goes through the critic's action projection.  With one topology and at least one actor
-hidden layer the projection re-associates (``a W_a^T = h (W_a diag(m) W)^T + W_a (b * m)``), so no
-``[B, A]`` actor output is materialised; otherwise (several topologies, or ``GSC_COMPOSE=0``) the
-``[B, A]`` output and its gradient are materialised -- both paths are the same function.
+The actor loss goes through the critic's action projection.  With at least one actor hidden layer the
+projection re-associates per topology t (``a W_a^T = h (W_a diag(m_t) W)^T + W_a (b * m_t)``), so no
+``[B, A]`` actor output is materialised: with T topologies the rows are expanded into T blocks
+(``hx[r] = onehot(topo[r]) (x) h[r]``) and the T products ``Mc_t = W_a diag(m_t) W`` run as one GEMM
+over ``K = A`` -- T (critic width) x (actor width) x A MACs instead of B x A x (actor width) per
+product.  With ``T * critic width > min(B, 1024)`` (or ``GSC_COMPOSE=0``) the ``[B, A]`` output and
+its gradient are materialised -- both paths are the same function.
 """
 from __future__ import annotations
 
@@ -33,7 +36,7 @@ import torch
 
 from gsc_amd.native import load as load_native
 from gsc_amd.ops.gnn import _layer_of, _tables, gnn_use_fused
-from gsc_amd.ops.mlp import gemm
+from gsc_amd.ops.mlp import auto_splits, gemm
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -98,7 +101,9 @@ class NativeDDPGUpdate:
         self.tcritic = _Net(L.target_critic, L.target_critic_flat, False, H, A, True)
         if L.actor.squash:
             raise NotImplementedError("native update: sigmoid-squashed actor output")
-        self.compose = (os.environ.get("GSC_COMPOSE", "1") != "0" and T == 1 and self.actor.nh >= 1)
+        c1 = self.critic.width(0)
+        self.compose = (os.environ.get("GSC_COMPOSE", "1") != "0" and self.actor.nh >= 1
+                        and T * c1 <= min(B, 1024))
         self.graphs = L.graphs
         self.tables = _tables(L.graphs)
         self.layer_of = _layer_of(L.actor.embedder)
@@ -118,15 +123,19 @@ class NativeDDPGUpdate:
         self.dh = [mk(B, wmax, dt=BF16), mk(B, wmax, dt=BF16)]
         self.dact = mk(B, A, dt=BF16) if not self.compose else None
         self.demb = mk(B, H)
-        c1 = self.critic.width(0)
-        self.wa = {k: mk(c1, A, dt=BF16) for k in ("c", "tc", "cm")}   # aligned critic action blocks
+        self.wa = {k: mk(c1, A, dt=BF16) for k in ("c", "tc")}   # aligned critic action blocks
+        # per-topology masked blocks W_a diag(m_t), stacked [T * c1, A] (composed actor loss)
+        self.wam = mk(T * c1, A, dt=BF16) if self.compose else None
         self.rowtab = {k: mk(T, wmax) for k in ("a", "ta", "c", "tc")}
         self.aug = mk(wmax, max(H + 1 + T, 1))
         hl = self.actor.width(self.actor.nh - 1) if self.actor.nh else 1
-        self.mc32 = mk(c1, hl)
-        self.mc16 = mk(c1, hl, dt=BF16)
-        self.cb = mk(c1, 1)
-        self.dmc = mk(c1, hl + 1)
+        self.mc32 = mk(T * c1, hl)                           # Mc_t = W_a diag(m_t) W, stacked over t
+        self.mc16 = mk(T * c1, hl, dt=BF16)                  # same, bf16 (d hx = dh0x Mc)
+        self.mccat = mk(c1, T * hl, dt=BF16)                 # [Mc_0 | .. | Mc_T-1] (forward, K = T hl)
+        self.cb = mk(T, c1)                                  # W_a (b * m_t) per topology (row table)
+        self.dmc = mk(T * c1, hl + 1)
+        self.hx = mk(B, T * hl, dt=BF16) if T > 1 else None  # topology-expanded actor hidden / critic grads
+        self.dh0x = mk(B, T * c1, dt=BF16) if T > 1 else None
         self.splits = None                                   # auto split-K for the batch reductions
         self.slabs = mk(16 << 20)                            # split-K slabs (64 MB; bounds the split count)
         self.head_blocks = max(64, min(256, -(-B // 64)))    # one block per CU (>= 16 rows per wave)
@@ -195,7 +204,8 @@ class NativeDDPGUpdate:
         out = self.rowtab[key][:, :h0]
         w = net.w16(0)
         self.nat.rowdot(self.masks.data_ptr(), self.masks.stride(0), self.T, w.data_ptr() + 2 * self.H, w.stride(0),
-                        h0, self.A, out.data_ptr(), out.stride(0), self._stream())
+                        h0, self.A, out.data_ptr(), out.stride(0), self._stream(), self.slabs.data_ptr(),
+                        self.slabs.numel())
         return out
 
     def _wa(self, net: _Net, key: str, colmask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -207,12 +217,15 @@ class NativeDDPGUpdate:
                         colmask.data_ptr() if colmask is not None else 0, self._stream())
         return dst
 
-    def _first(self, net: _Net, emb, rowtab, out16, extra=None, wa=None, extra_bias=None):
-        """h0 = relu(emb W_d^T + b + rowtab[topo] (+ extra wa^T + extra_bias)) -> out16."""
+    def _first(self, net: _Net, emb, rowtab, out16, extra=None, wa=None, extra_rowtab=None):
+        """h0 = relu(emb W_d^T + b + rowtab[topo] (+ extra wa^T + extra_rowtab[topo])) -> out16."""
         h0 = net.width(0)
         acc = False
         if extra is not None:
-            gemm(extra, wa, "nt", out32=self.hacc[:, :h0], bias=extra_bias)
+            if extra_rowtab is not None:
+                gemm(extra, wa, "nt", out32=self.hacc[:, :h0], rowtab=extra_rowtab, topo=self.topo32)
+            else:   # K = A: split-K when the [B, h0] output alone gives few workgroups (large A)
+                gemm(extra, wa, "nt", out32=self.hacc[:, :h0], splits=None, slabs=self.slabs)
             acc = True
         gemm(emb, net.w16(0)[:, :self.H], "nt", out16=out16, bias=net.b32(0), rowtab=rowtab, topo=self.topo32,
              relu=True, accumulate=acc, out32=self.hacc[:, :h0] if acc else None)
@@ -321,18 +334,31 @@ class NativeDDPGUpdate:
         hl = self.hid_a[a.nh - 1]
         last = a.nh
         rt_c = self._rowtab(c, "c")
-        wa = self._wa(c, "c")
+        T, c1, hw = self.T, c.width(0), hl.shape[1]
+        st = self._stream()
         if self.compose:
-            m = self.masks[0]
-            wam = self._wa(c, "cm", colmask=m)                       # W_a diag(m)
-            gemm(wam, a.w16(last), "nn", out32=self.mc32, slabs=self.slabs, splits=16)   # Mc = W_a diag(m) W
-            self.nat.cast2d(self.mc32.data_ptr(), self.mc32.stride(0), self.mc16.data_ptr(),
-                                     self.mc16.stride(0), self.mc32.shape[0], self.mc32.shape[1], self._stream())
-            bl = a.b32(last)                                                     # cb = W_a (b * m)
-            self.nat.rowdot(bl.data_ptr(), bl.numel(), 1, wam.data_ptr(), wam.stride(0), wam.shape[0], A,
-                            self.cb.data_ptr(), 1, self._stream())
-            self._first(c, self.emb["c2"], rt_c, self.hid_c[0], extra=hl, wa=self.mc16, extra_bias=self.cb.view(-1))
+            wam = self.wam                                            # W_a diag(m_t), t = 0 .. T-1
+            w = c.w16(0)
+            for t in range(T):
+                self.nat.copy2d(w.data_ptr() + 2 * (H + A), w.stride(0), wam[t * c1].data_ptr(), wam.stride(0), c1, A,
+                                self.masks[t].data_ptr(), st)
+            ks = max(16, auto_splits(T * c1, hw, A, 2, self.slabs.numel()))
+            gemm(wam, a.w16(last), "nn", out32=self.mc32, slabs=self.slabs, splits=ks)   # Mc_t = W_a diag(m_t) W
+            self.nat.cast2d(self.mc32.data_ptr(), hw, self.mc16.data_ptr(), hw, T * c1, hw, st)
+            for t in range(T):                                        # [Mc_0 | .. ]: row j holds Mc_t[j] at t*hw
+                self.nat.cast2d(self.mc32[t * c1].data_ptr(), hw, self.mccat.data_ptr() + 2 * t * hw,
+                                self.mccat.stride(0), c1, hw, st)
+            bl = a.b32(last)                                          # cb_t = W_a (b * m_t)
+            self.nat.rowdot(bl.data_ptr(), bl.numel(), 1, wam.data_ptr(), wam.stride(0), T * c1, A,
+                            self.cb.data_ptr(), T * c1, st, self.slabs.data_ptr(), self.slabs.numel())
+            hx = hl
+            if T > 1:
+                hx = self.hx
+                self.nat.topo_expand(hl.data_ptr(), hl.stride(0), hx.data_ptr(), hx.stride(0), self.B, hw, T,
+                                     self.topo32.data_ptr(), st)
+            self._first(c, self.emb["c2"], rt_c, self.hid_c[0], extra=hx, wa=self.mccat, extra_rowtab=self.cb)
         else:
+            wa = self._wa(c, "c")
             gemm(hl, a.w16(last), "nt", out16=self.act_buf, bias=a.b32(last), colmask=self.masks, topo=self.topo32)
             self._first(c, self.emb["c2"], rt_c, self.hid_c[0], extra=self.act_buf, wa=wa)
         self._hidden_fwd(c, self.hid_c)
@@ -341,15 +367,19 @@ class NativeDDPGUpdate:
         self._critic_tail(c, self.hid_c, 2, dh, b)
         self._head_reduce(c, C, 2)
         dh0 = self._hidden_bwd(c, self.hid_c, dh, grads=False)      # gated grad at the critic's layer-0 pre-act
-        c1 = c.width(0)
-        hw = hl.shape[1]
         dz = self.dh[1][:, :hw] if dh0.data_ptr() != self.dh[1].data_ptr() else self.dh[0][:, :hw]
         if self.compose:
-            # dMc | dcb = dh0^T [h | 1];  dW = diag(m) W_a^T dMc;  db = diag(m) W_a^T dcb;  dh = (dh0 Mc) * (h > 0)
-            gemm(dh0, hl, "tn", out32=self.dmc, aug_t=0, aug_topo=self.topo32, splits=self.splits, slabs=self.slabs)
-            gemm(wa, self.dmc[:, :hw], "tn", out32=a.gw(last), rowscale=m)
-            gemm(wa, self.dmc[:, hw:hw + 1], "tn", out32=a.gb(last).view(-1, 1), rowscale=m)
-            gemm(dh0, self.mc16, "nn", out16=dz, gate=hl)
+            # per topology t (rows of dh0x hold dh0 in block topo[r]):  dMc_t | dcb_t = dh0x_t^T [h | 1];
+            # dW = sum_t diag(m_t) W_a^T dMc_t;  db = sum_t diag(m_t) W_a^T dcb_t;  dh = (dh0x Mc) * (h > 0)
+            dh0x = dh0
+            if T > 1:
+                dh0x = self.dh0x
+                self.nat.topo_expand(dh0.data_ptr(), dh0.stride(0), dh0x.data_ptr(), dh0x.stride(0), self.B, c1, T,
+                                     self.topo32.data_ptr(), st)
+            gemm(dh0x, hl, "tn", out32=self.dmc, aug_t=0, aug_topo=self.topo32, splits=self.splits, slabs=self.slabs)
+            gemm(self.wam, self.dmc[:, :hw], "tn", out32=a.gw(last))
+            gemm(self.wam, self.dmc[:, hw:hw + 1], "tn", out32=a.gb(last).view(-1, 1))
+            gemm(dh0x, self.mc16, "nn", out16=dz, gate=hl)
         else:
             gemm(dh0, wa, "nn", out16=self.dact, colmask=self.masks, topo=self.topo32)   # dL/da (masked)
             gemm(self.dact, hl, "tn", out32=a.gw(last), splits=self.splits, slabs=self.slabs)
@@ -389,6 +419,7 @@ class NativeAct:
         self.emb = torch.zeros(E, self.H, device=dev)
         self.hid = [torch.zeros(E, n.width(i), device=dev, dtype=BF16) for i in range(n.nh)]
         self.rowtab = torch.zeros(self.T, n.width(0), device=dev)
+        self.rowdot_ws = torch.zeros(64 * self.T * n.width(0), device=dev)   # split-A partials of the fold
         self.out = torch.zeros(E, self.A, device=dev)
         self.topo32 = torch.zeros(E, dtype=torch.int32, device=dev)
         self._topo_ref, self._topo_ver = None, -1
@@ -411,7 +442,8 @@ class NativeAct:
         n, s = self.net, torch.cuda.current_stream(self.L.device).cuda_stream
         w = n.w16(0)
         self.nat.rowdot(self.masks.data_ptr(), self.masks.stride(0), self.T, w.data_ptr() + 2 * self.H, w.stride(0),
-                        n.width(0), self.A, self.rowtab.data_ptr(), self.rowtab.stride(0), s)
+                        n.width(0), self.A, self.rowtab.data_ptr(), self.rowtab.stride(0), s, self.rowdot_ws.data_ptr(),
+                        self.rowdot_ws.numel())
         self.rowtab_dirty = False
 
     def __call__(self, obs: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:

@@ -1,12 +1,13 @@
 """Layer-wise GATv2 embedder on native kernels, for graphs too large for the fused per-graph
 kernels (``gnn_fits`` false: e.g. the 200-node synthetic topologies of BASELINE config 5).
 
-Per conv (``csrc/ops/gnn_lw.hip``): node linears ``x_l = h W_l^T + b_l``, ``x_r = h W_r^T + b_r`` on
-the MFMA GEMM engine over all ``B x P`` node rows; attention + segment softmax + mean aggregation
-(+ bias, ReLU) per target node; mean pool per graph.  Backward: attention backward per target node
-(``d x_r`` gathered per target, ``d x_l`` per source through the source-sorted CSR), weight
-gradients ``dW = dX^T h`` (split-K GEMM, deterministic reduction), input gradients ``dX W`` (GEMM),
-vector gradients by deterministic column sums.  Same semantics as ``gatv2_dense_reference``
+Per conv (``csrc/ops/gnn_lw.hip``): node linears ``x_l = h W_l^T + b_l``, ``x_r = h W_r^T + b_r``
+(first conv: the MFMA GEMM engine over all ``B x P`` node rows; later convs: in the previous
+attention kernel's epilogue); attention + online segment softmax + mean aggregation (+ bias, ReLU) per
+target node; mean pool per graph.  Backward: attention backward per target node (``d x_r`` gathered
+per target, ``d x_l`` per source through the source-sorted CSR, with the input gradient
+``dX W`` in the same gather), weight gradients ``dW = dX^T h`` (split-K GEMM, deterministic
+reduction), vector gradients by deterministic column sums.  Same semantics as ``gatv2_dense_reference``
 (reference ``src/rlsp/agents/models.py:10-53``).
 
 A :class:`LayerwiseGAT` owns the workspaces of one batch size; ``forward`` keeps every conv's
@@ -90,11 +91,17 @@ class LayerwiseGAT:
         h = x.view(B * P, self.Fin)
         for l, blk in enumerate(self.layer_of):
             Fi, Wl, bl, Wr, br, att, bias = self._params(flat, blk)
-            gemm(h, Wl, "nt", out32=self.xl[l], bias=bl)
-            gemm(h, Wr, "nt", out32=self.xr[l], bias=br)
+            if l == 0:   # later convs' node linears come from the previous attention kernel
+                gemm(h, Wl, "nt", out32=self.xl[l], bias=bl)
+                gemm(h, Wr, "nt", out32=self.xr[l], bias=br)
+            nxt = ()
+            if l + 1 < self.L:
+                _, Wl2, bl2, Wr2, br2, _, _ = self._params(flat, self.layer_of[l + 1])
+                nxt = (Wl2.data_ptr(), bl2.data_ptr(), Wr2.data_ptr(), br2.data_ptr(), self.xl[l + 1].data_ptr(),
+                       self.xr[l + 1].data_ptr())
             nat.lw_attn_fwd(t, topo32.data_ptr(), B, P, H, self.xl[l].data_ptr(), self.xr[l].data_ptr(),
                             att.data_ptr(), bias.data_ptr(), int(self._relu(l)), self.hout[l].data_ptr(),
-                            self.alpha[l].data_ptr(), s)
+                            self.alpha[l].data_ptr(), s, nxt)
             h = self.hout[l]
         nat.lw_pool(t, topo32.data_ptr(), B, P, H, self.hout[self.L - 1].data_ptr(), emb.data_ptr(), s)
 
@@ -116,12 +123,13 @@ class LayerwiseGAT:
             nat.lw_attn_bwd(t, tp, B, P, H, cur.data_ptr(), self.hout[l].data_ptr() if self._relu(l) else 0,
                             self.xl[l].data_ptr(), self.xr[l].data_ptr(), self.alpha[l].data_ptr(), att.data_ptr(),
                             self.dxr.data_ptr(), self.msg.data_ptr(), self.datt.data_ptr(), s)
-            nat.lw_src_gather(t, tp, B, P, H, self.msg.data_ptr(), self.dxl.data_ptr(), s)
+            # l > 0: the gather also writes the input gradient dxl W_l + dxr W_r into nxt
+            nat.lw_src_gather(t, tp, B, P, H, self.msg.data_ptr(), self.dxl.data_ptr(), s, self.dxr.data_ptr(),
+                              Wl.data_ptr() if l > 0 else 0, Wr.data_ptr() if l > 0 else 0,
+                              nxt.data_ptr() if l > 0 else 0)
             gemm(self.dxl, hin, "tn", out32=gWl, splits=None, slabs=self.slabs, accumulate=acc)
             gemm(self.dxr, hin, "tn", out32=gWr, splits=None, slabs=self.slabs, accumulate=acc)
             for src, dst in ((self.dxl, gbl), (self.dxr, gbr), (self.datt, gatt), (cur, gbias)):
                 nat.lw_colsum(src.data_ptr(), R, H, H, self.part.data_ptr(), dst.data_ptr(), int(acc), s)
             if l > 0:
-                gemm(self.dxl, Wl, "nn", out32=nxt)
-                gemm(self.dxr, Wr, "nn", out32=nxt, accumulate=True)
                 cur, nxt = nxt, cur

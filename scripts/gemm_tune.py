@@ -1,6 +1,10 @@
 #!/usr/bin/env python
-"""Time the MFMA GEMM engine (csrc/ops/mlp.hip) at the DDPG learner's shapes (B = 25,600, Abilene /
-sample agent) for every output tile x K-stage depth, next to hipBLASLt (torch.mm) as a yardstick."""
+"""Time the MFMA GEMM engine (csrc/ops/mlp.hip) at the DDPG learner's shapes for every output tile x
+K-stage depth, next to hipBLASLt (torch.mm) as a yardstick.
+
+    python scripts/gemm_tune.py [abilene|syn200]
+
+abilene: B = 25,600, A = 1,728 (sample agent); syn200: B = 2,048, A = 360,000, 3 topologies (config 5)."""
 import os
 import sys
 
@@ -24,16 +28,29 @@ def t(fn, n=20):
     return s.elapsed_time(e) / n * 1e3
 
 
-B = 25600
+PRESET = sys.argv[1] if len(sys.argv) > 1 else "abilene"
 dev = "cuda"
 bf = torch.bfloat16
-cases = [  # (name, layout, a, b, kwargs)
-    ("actor out  [B,256]x[1728,256]^T -> bf16", "nt", (B, 256), (1728, 256), {}),
-    ("critic act [B,1728]x[64,1728]^T -> f32", "nt", (B, 1728), (64, 1728), {"o32": True}),
-    ("critic dW  [B,64]^T x [B,1728]", "tn", (B, 64), (B, 1728), {"o32": True, "split": True}),
-    ("actor hid  [B,22]x[256,22]^T -> bf16", "nt", (B, 22), (256, 22), {}),
-    ("dX  [B,64]x[64,256] -> bf16", "nn", (B, 64), (64, 256), {}),
-]
+if PRESET == "abilene":
+    B = 25600
+    cases = [  # (name, layout, a, b, kwargs)
+        ("actor out  [B,256]x[1728,256]^T -> bf16", "nt", (B, 256), (1728, 256), {}),
+        ("critic act [B,1728]x[64,1728]^T -> f32", "nt", (B, 1728), (64, 1728), {"o32": True}),
+        ("critic dW  [B,64]^T x [B,1728]", "tn", (B, 64), (B, 1728), {"o32": True, "split": True}),
+        ("actor hid  [B,22]x[256,22]^T -> bf16", "nt", (B, 22), (256, 22), {}),
+        ("dX  [B,64]x[64,256] -> bf16", "nn", (B, 64), (64, 256), {}),
+    ]
+else:
+    B, A, T = 2048, 360000, 3
+    cases = [
+        ("target actor out [B,256]x[A,256]^T -> bf16 (masked, clamped)", "nt", (B, 256), (A, 256), {"mask": True}),
+        ("critic act [B,A]x[64,A]^T -> f32 (split-K)", "nt", (B, A), (64, A), {"o32": True, "split": True}),
+        ("critic dW  [B,64]^T x [B,A]", "tn", (B, 64), (B, A), {"o32": True, "split": True}),
+        ("Mc  [3*64,A]x[A,256] -> f32 (split-K)", "nn", (T * 64, A), (A, 256), {"o32": True, "split": True}),
+        ("actor dW  [3*64,A]^T x [3*64,256]", "tn", (T * 64, A), (T * 64, 256), {"o32": True}),
+    ]
+    masks = (torch.rand(T, A, device=dev) > 0.5).float()
+    topo = torch.randint(0, T, (B,), device=dev, dtype=torch.int32)
 slabs = torch.empty(16 << 20, device=dev)
 for name, lay, sa, sb, kw in cases:
     a = torch.randn(*sa, device=dev, dtype=bf)
@@ -49,8 +66,9 @@ for name, lay, sa, sb, kw in cases:
     res = {}
     for tile in (0, 1, 2, 3):
         for bk in (32, 64):
+            ep = dict(colmask=masks, topo=topo, clamp=(-1.0, 1.0)) if kw.get("mask") else {}
             f = lambda: gemm(a, b, lay, out16=None if kw.get("o32") else o16, out32=o32 if kw.get("o32") else None,
-                             tile=tile, bk=bk, splits=None if kw.get("split") else 1, slabs=slabs)
+                             tile=tile, bk=bk, splits=None if kw.get("split") else 1, slabs=slabs, **ep)
             res[f"t{tile}/bk{bk}"] = t(f)
     ref = {"nt": lambda: torch.mm(a, b.t()), "tn": lambda: torch.mm(a.t(), b), "nn": lambda: torch.mm(a, b)}[lay]
     res["hipblaslt"] = t(ref)
