@@ -24,6 +24,9 @@ namespace py = pybind11;
 namespace gsc {
 
 constexpr float kLwSlope = 0.2f;
+constexpr int LW_U = 4;  // messages per group in the per-node loops (loads in flight together)
+
+__device__ __forceinline__ void lw_stage_rows(const float* __restrict__ src, long r0, int nr, int w, float* dst);
 
 struct LwGraph {
   const int32_t* topo;     // [B]
@@ -100,24 +103,48 @@ __global__ __launch_bounds__(256) void lw_attn_fwd_kernel(LwGraph g, const float
   float* al = alpha + (long)b * g.M;
   // one pass over the in-messages with an online softmax (running max, rescaled sums); the raw
   // scores go to alpha (message q by lane (q - q0) mod NL) and are normalised afterwards
-  float mx = -__builtin_inff(), den = 0.f, acc = 0.f;
-  for (int q = q0; q < q1; ++q) {
-    const float xlj = c < H ? xlb[(long)src[q] * H + c] : 0.f;
-    const float s = lw_sum<NL>(ac * leaky(xlj + xri));
-    if (c == ((q - q0) & (NL - 1))) al[q] = s;  // every lane holds s (xor butterfly)
-    if (s > mx) {
-      const float r = __expf(mx - s);  // 0 on the first message (mx = -inf)
+  // messages in groups of LW_U: the index and x_l row loads of a group are independent (in flight
+  // together), then one rescale per group
+  float mx = -__builtin_inff(), den = 0.f, acc = 0.f, s0 = 0.f, s1 = 0.f;
+  for (int q = q0; q < q1; q += LW_U) {
+    float xv[LW_U], sc[LW_U];
+#pragma unroll
+    for (int u = 0; u < LW_U; ++u) {
+      const int qq = q + u;
+      xv[u] = (qq < q1 && c < H) ? xlb[(long)src[qq] * H + c] : 0.f;
+    }
+    float gm = mx;
+#pragma unroll
+    for (int u = 0; u < LW_U; ++u) {
+      sc[u] = lw_sum<NL>(ac * leaky(xv[u] + xri));
+      if (q + u < q1) {
+        if (c == ((q + u - q0) & (NL - 1))) {  // every lane holds the score (xor butterfly); raw scores
+          const int k = (q + u - q0) / NL;     // stay in registers for the first 2 NL messages
+          if (k == 0) s0 = sc[u];
+          else if (k == 1) s1 = sc[u];
+          else al[q + u] = sc[u];
+        }
+        gm = sc[u] > gm ? sc[u] : gm;
+      }
+    }
+    if (gm > mx) {
+      const float r = __expf(mx - gm);  // 0 on the first group (mx = -inf)
       den *= r;
       acc *= r;
-      mx = s;
+      mx = gm;
     }
-    const float e = __expf(s - mx);
-    den += e;
-    acc += e * xlj;
+#pragma unroll
+    for (int u = 0; u < LW_U; ++u) {
+      if (q + u < q1) {
+        const float e = __expf(sc[u] - mx);
+        den += e;
+        acc += e * xv[u];
+      }
+    }
   }
   const float inv = 1.f / (den + 1e-16f);
-  // each lane rescales the scores it stored itself
-  for (int q = q0 + c; q < q1; q += NL) al[q] = __expf(al[q] - mx) * inv;
+  // each lane normalises the scores it holds (same-lane order for the rare ones kept in memory)
+  for (int q = q0 + c, k = 0; q < q1; q += NL, ++k) al[q] = __expf((k == 0 ? s0 : k == 1 ? s1 : al[q]) - mx) * inv;
   float y = 0.f;
   if (c < H) {
     y = acc * inv / g.deg[(long)t * g.P + i] + bias[c];
@@ -135,6 +162,284 @@ __global__ __launch_bounds__(256) void lw_attn_fwd_kernel(LwGraph g, const float
     if (c < H) {
       nx.xl[node * H + c] = al_;
       nx.xr[node * H + c] = ar_;
+    }
+  }
+}
+
+// Per-graph variant (the graph's x_l / x_r rows fit in LDS): one workgroup per graph stages its
+// P x H x_l and x_r blocks with 16-byte loads, then 256 / NL lane groups take the nodes in turn and
+// gather the message rows from LDS -- the HBM traffic is the coalesced block copies instead of one
+// dependent row gather per message.  Same arithmetic as lw_attn_fwd_kernel.
+template <int NL>
+__global__ __launch_bounds__(256) void lw_graph_attn_fwd_kernel(LwGraph g, const float* __restrict__ xl,
+                                                                const float* __restrict__ xr,
+                                                                const float* __restrict__ att,
+                                                                const float* __restrict__ bias, int relu,
+                                                                float* __restrict__ h_out, float* __restrict__ alpha,
+                                                                LwNext nx) {
+  // LDS: x_l [P][H], x_r [P][H], W_l'^T, W_r'^T [H][H] (when nx.wl), in_ptr [P+1], in_src [M], deg [P]
+  extern __shared__ __attribute__((aligned(16))) float lw_g[];
+  const int H = g.H, P = g.P, PH = P * H;
+  const int b = blockIdx.x;
+  const int t = g.topo[b];
+  float* s_xl = lw_g;
+  float* s_xr = lw_g + PH;
+  float* s_wt = lw_g + 2 * PH;
+  int32_t* iptr = reinterpret_cast<int32_t*>(s_wt + (nx.wl ? 2 * H * H : 0));
+  int32_t* src = iptr + P + 1;
+  float* s_deg = reinterpret_cast<float*>(src + g.M);
+  lw_stage_rows(xl, (long)b * P, P, H, s_xl);
+  lw_stage_rows(xr, (long)b * P, P, H, s_xr);
+  if (nx.wl) {
+    for (int k = threadIdx.x; k < H * H; k += blockDim.x) {
+      const int co = k / H, ci = k - co * H;
+      s_wt[ci * H + co] = nx.wl[k];
+      s_wt[H * H + ci * H + co] = nx.wr[k];
+    }
+  }
+  for (int k = threadIdx.x; k <= P; k += blockDim.x) iptr[k] = g.in_ptr[(long)t * (P + 1) + k];
+  for (int k = threadIdx.x; k < g.M; k += blockDim.x) src[k] = g.in_src[(long)t * g.M + k];
+  for (int k = threadIdx.x; k < P; k += blockDim.x) s_deg[k] = g.deg[(long)t * P + k];
+  __syncthreads();
+  const int n = g.nnodes[t];
+  const int c = threadIdx.x & (NL - 1);
+  const int cc = c < H ? c : 0;
+  const float ac = c < H ? att[c] : 0.f;
+  const float bc = c < H ? bias[c] : 0.f;
+  float* al = alpha + (long)b * g.M;
+  for (int i = threadIdx.x / NL; i < P; i += 256 / NL) {
+    const long node = (long)b * P + i;
+    if (i >= n) {
+      if (c < H) {
+        h_out[node * H + c] = 0.f;
+        if (nx.wl) {
+          nx.xl[node * H + c] = nx.bl[c];
+          nx.xr[node * H + c] = nx.br[c];
+        }
+      }
+      continue;
+    }
+    const int q0 = iptr[i], q1 = iptr[i + 1];
+    const float xri = s_xr[i * H + cc];
+    float mx = -__builtin_inff(), den = 0.f, acc = 0.f, s0 = 0.f, s1 = 0.f;
+    for (int q = q0; q < q1; q += LW_U) {
+      float xv[LW_U], sc[LW_U];
+#pragma unroll
+      for (int u = 0; u < LW_U; ++u) {
+        const int qq = q + u;
+        xv[u] = (qq < q1 && c < H) ? s_xl[src[qq] * H + c] : 0.f;
+      }
+      float gm = mx;
+#pragma unroll
+      for (int u = 0; u < LW_U; ++u) {
+        sc[u] = lw_sum<NL>(ac * leaky(xv[u] + xri));
+        if (q + u < q1) {
+          if (c == ((q + u - q0) & (NL - 1))) {  // raw scores: registers for the first 2 NL messages
+            const int k = (q + u - q0) / NL;
+            if (k == 0) s0 = sc[u];
+            else if (k == 1) s1 = sc[u];
+            else al[q + u] = sc[u];
+          }
+          gm = sc[u] > gm ? sc[u] : gm;
+        }
+      }
+      if (gm > mx) {
+        const float r = __expf(mx - gm);
+        den *= r;
+        acc *= r;
+        mx = gm;
+      }
+#pragma unroll
+      for (int u = 0; u < LW_U; ++u) {
+        if (q + u < q1) {
+          const float e = __expf(sc[u] - mx);
+          den += e;
+          acc += e * xv[u];
+        }
+      }
+    }
+    const float inv = 1.f / (den + 1e-16f);
+    for (int q = q0 + c, k = 0; q < q1; q += NL, ++k) al[q] = __expf((k == 0 ? s0 : k == 1 ? s1 : al[q]) - mx) * inv;
+    float y = 0.f;
+    if (c < H) {
+      y = acc * inv / s_deg[i] + bc;
+      if (relu) y = y > 0.f ? y : 0.f;
+      h_out[node * H + c] = y;
+    }
+    if (nx.wl) {
+      float al_ = c < H ? nx.bl[c] : 0.f, ar_ = c < H ? nx.br[c] : 0.f;
+      for (int k = 0; k < H; ++k) {
+        const float hk = __shfl(y, k, NL);
+        al_ += s_wt[k * H + cc] * hk;
+        ar_ += s_wt[H * H + k * H + cc] * hk;
+      }
+      if (c < H) {
+        nx.xl[node * H + c] = al_;
+        nx.xr[node * H + c] = ar_;
+      }
+    }
+  }
+}
+
+// A lane's H-float row from registers: 8-byte stores when the row is 8-byte aligned (fewer, wider
+// store instructions than one per element), else element stores.
+template <int HV>
+__device__ __forceinline__ void lw_store_row(float* dst, const float (&v)[HV], int H) {
+  if ((((uintptr_t)dst) & 7) == 0 && (H & 1) == 0) {
+#pragma unroll
+    for (int c = 0; c < HV; c += 2)
+      if (c < H) *reinterpret_cast<float2*>(dst + c) = make_float2(v[c], v[c + 1]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < HV; ++c)
+      if (c < H) dst[c] = v[c];
+  }
+}
+
+// Lane-per-node forward (H <= 32): one workgroup per graph, one lane per target node.  The message
+// scores are dot products over the lane's own registers (no cross-lane reductions, no shuffles); the
+// graph's x_l rows sit in LDS with a padded row stride HV (16-byte reads), the raw scores in an LDS
+// slot per message (each message has one target), and the next conv's node linears read W
+// broadcast from LDS.  Same arithmetic as lw_attn_fwd_kernel.
+template <int HV>
+__global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const float* __restrict__ xl,
+                                                               const float* __restrict__ xr,
+                                                               const float* __restrict__ att,
+                                                               const float* __restrict__ bias, int relu,
+                                                               float* __restrict__ h_out, float* __restrict__ alpha,
+                                                               LwNext nx, float* __restrict__ emb) {
+  // LDS: x_l [P][HV], W_l', W_r' [H][HV] (when nx.wl), raw scores [M], deg [P], in_ptr [P+1], in_src [M]
+  // emb (last conv): the graph's mean pool, lane partial sums reduced in a fixed shuffle / wave order
+  __shared__ float red[4][HV];
+  extern __shared__ __attribute__((aligned(16))) float lw_g[];
+  const int H = g.H, P = g.P, M = g.M;
+  const int b = blockIdx.x, t = g.topo[b];
+  float* s_xl = lw_g;
+  float* s_w = s_xl + P * HV;
+  float* s_sc = s_w + (nx.wl ? 2 * H * HV : 0);
+  float* s_deg = s_sc + M;
+  int32_t* iptr = reinterpret_cast<int32_t*>(s_deg + P);
+  int32_t* src = iptr + P + 1;
+  const long base = (long)b * P * H;
+  for (int k = threadIdx.x; k < P * HV; k += 256) {
+    const int r = k / HV, c = k - r * HV;
+    s_xl[k] = c < H ? xl[base + (long)r * H + c] : 0.f;
+  }
+  if (nx.wl) {
+    for (int k = threadIdx.x; k < H * HV; k += 256) {
+      const int r = k / HV, c = k - r * HV;
+      s_w[k] = c < H ? nx.wl[r * H + c] : 0.f;
+      s_w[H * HV + k] = c < H ? nx.wr[r * H + c] : 0.f;
+    }
+  }
+  for (int k = threadIdx.x; k <= P; k += 256) {
+    iptr[k] = g.in_ptr[(long)t * (P + 1) + k];
+    if (k < P) s_deg[k] = g.deg[(long)t * P + k];
+  }
+  for (int k = threadIdx.x; k < M; k += 256) src[k] = g.in_src[(long)t * M + k];
+  __syncthreads();
+  float a_[HV], bi[HV];
+#pragma unroll
+  for (int c = 0; c < HV; ++c) {
+    a_[c] = c < H ? att[c] : 0.f;
+    bi[c] = c < H ? bias[c] : 0.f;
+  }
+  const int n = g.nnodes[t];
+  float* al = alpha + (long)b * M;
+  float ys[HV];
+#pragma unroll
+  for (int c = 0; c < HV; ++c) ys[c] = 0.f;
+  for (int i = threadIdx.x; i < P; i += 256) {
+    const long node = (long)b * P + i;
+    float y[HV];
+    if (i < n) {
+      float xri[HV], acc[HV];
+#pragma unroll
+      for (int c = 0; c < HV; ++c) {
+        xri[c] = c < H ? xr[node * H + c] : 0.f;
+        acc[c] = 0.f;
+      }
+      const int q0 = iptr[i], q1 = iptr[i + 1];
+      float mx = -__builtin_inff(), den = 0.f;
+      for (int q = q0; q < q1; ++q) {
+        const float4* row = reinterpret_cast<const float4*>(s_xl + src[q] * HV);
+        float xj[HV];
+#pragma unroll
+        for (int v = 0; v < HV / 4; ++v) {
+          const float4 f = row[v];
+          xj[4 * v] = f.x;
+          xj[4 * v + 1] = f.y;
+          xj[4 * v + 2] = f.z;
+          xj[4 * v + 3] = f.w;
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < HV; ++c) s += a_[c] * leaky(xj[c] + xri[c]);
+        s_sc[q] = s;
+        if (s > mx) {
+          const float r = __expf(mx - s);  // 0 for the first message
+          den *= r;
+#pragma unroll
+          for (int c = 0; c < HV; ++c) acc[c] *= r;
+          mx = s;
+        }
+        const float e = __expf(s - mx);
+        den += e;
+#pragma unroll
+        for (int c = 0; c < HV; ++c) acc[c] += e * xj[c];
+      }
+      const float inv = 1.f / (den + 1e-16f);
+      for (int q = q0; q < q1; ++q) al[q] = __expf(s_sc[q] - mx) * inv;
+      const float sc = inv / s_deg[i];
+#pragma unroll
+      for (int c = 0; c < HV; ++c) {
+        float v = acc[c] * sc + bi[c];
+        if (relu) v = v > 0.f ? v : 0.f;
+        y[c] = c < H ? v : 0.f;
+        ys[c] += y[c];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < HV; ++c) y[c] = 0.f;
+    }
+    lw_store_row<HV>(h_out + node * H, y, H);
+    if (nx.wl) {  // x_l'[co] = b_l'[co] + W_l'[co] . y  (W rows broadcast from LDS)
+      float ol[HV], orr[HV];
+#pragma unroll
+      for (int co = 0; co < HV; ++co) {
+        ol[co] = 0.f;
+        orr[co] = 0.f;
+        if (co < H) {
+          const float4* wl4 = reinterpret_cast<const float4*>(s_w + co * HV);
+          const float4* wr4 = reinterpret_cast<const float4*>(s_w + H * HV + co * HV);
+          float sl = nx.bl[co], sr = nx.br[co];
+#pragma unroll
+          for (int v = 0; v < HV / 4; ++v) {
+            const float4 fl = wl4[v], fr = wr4[v];
+            sl += fl.x * y[4 * v] + fl.y * y[4 * v + 1] + fl.z * y[4 * v + 2] + fl.w * y[4 * v + 3];
+            sr += fr.x * y[4 * v] + fr.y * y[4 * v + 1] + fr.z * y[4 * v + 2] + fr.w * y[4 * v + 3];
+          }
+          ol[co] = sl;
+          orr[co] = sr;
+        }
+      }
+      lw_store_row<HV>(nx.xl + node * H, ol, H);
+      lw_store_row<HV>(nx.xr + node * H, orr, H);
+    }
+  }
+  if (emb) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < HV; ++c) {
+      float v = ys[c];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) red[w][c] = v;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < H) {
+      const int c = threadIdx.x;
+      emb[(long)b * H + c] = ((red[0][c] + red[1][c]) + (red[2][c] + red[3][c])) / (float)n;
     }
   }
 }
@@ -201,24 +506,40 @@ __global__ __launch_bounds__(256) void lw_attn_bwd_kernel(LwGraph g, float* __re
   float* mb = msg + (long)b * g.M * H;
   const float xri = ch ? xr[node * H + c] : 0.f;
   const float ac = ch ? att[c] : 0.f;
-  // sum_q' alpha_q' dalpha_q'
+  // sum_q' alpha_q' dalpha_q'  (groups of LW_U messages: loads in flight together)
   float sad = 0.f;
-  for (int q = q0; q < q1; ++q) {
-    const int j = src[q];
-    const float da = lw_sum<NL>(ch ? gc * xlb[(long)j * H + c] : 0.f);
-    sad += al[q] * da;
+  for (int q = q0; q < q1; q += LW_U) {
+    float xv[LW_U], a[LW_U];
+#pragma unroll
+    for (int u = 0; u < LW_U; ++u) {
+      const int qq = q + u;
+      xv[u] = (qq < q1 && ch) ? xlb[(long)src[qq] * H + c] : 0.f;
+      a[u] = qq < q1 ? al[qq] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < LW_U; ++u) sad += a[u] * lw_sum<NL>(gc * xv[u]);
   }
   float dxr_acc = 0.f, datt_acc = 0.f;
-  for (int q = q0; q < q1; ++q) {
-    const int j = src[q];
-    const float xlj = ch ? xlb[(long)j * H + c] : 0.f;
-    const float da = lw_sum<NL>(gc * xlj);
-    const float de = al[q] * (da - sad);
-    const float z = xlj + xri;
-    datt_acc += de * leaky(z);
-    const float dz = de * ac * (z > 0.f ? 1.f : kLwSlope);
-    dxr_acc += dz;
-    if (ch) mb[(long)q * H + c] = al[q] * gc + dz;
+  for (int q = q0; q < q1; q += LW_U) {
+    float xv[LW_U], a[LW_U];
+#pragma unroll
+    for (int u = 0; u < LW_U; ++u) {
+      const int qq = q + u;
+      xv[u] = (qq < q1 && ch) ? xlb[(long)src[qq] * H + c] : 0.f;
+      a[u] = qq < q1 ? al[qq] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < LW_U; ++u) {
+      const float da = lw_sum<NL>(gc * xv[u]);
+      const float de = a[u] * (da - sad);
+      const float z = xv[u] + xri;
+      const float dz = de * ac * (z > 0.f ? 1.f : kLwSlope);
+      if (q + u < q1) {
+        datt_acc += de * leaky(z);
+        dxr_acc += dz;
+        if (ch) mb[(long)(q + u) * H + c] = a[u] * gc + dz;
+      }
+    }
   }
   if (ch) {
     dxr[node * H + c] = dxr_acc;
@@ -233,10 +554,18 @@ template <int NL>
 __global__ __launch_bounds__(256) void lw_src_gather_kernel(LwGraph g, const float* __restrict__ msg, float* __restrict__ dxl,
                                                             const float* __restrict__ dxr, const float* __restrict__ wl,
                                                             const float* __restrict__ wr, float* __restrict__ dh) {
+  extern __shared__ float lw_w[];  // [2][H][H]: W_l, W_r (row = output channel)
+  const int H = g.H;
+  if (wl) {
+    for (int k = threadIdx.x; k < H * H; k += blockDim.x) {
+      lw_w[k] = wl[k];
+      lw_w[H * H + k] = wr[k];
+    }
+    __syncthreads();
+  }
   const long node = (long)blockIdx.x * (256 / NL) + (threadIdx.x / NL);
   const int c = threadIdx.x & (NL - 1);
   if (node >= (long)g.B * g.P) return;  // whole node groups exit together
-  const int H = g.H;
   const int b = (int)(node / g.P), j = (int)(node - (long)b * g.P);
   const int t = g.topo[b];
   float s = 0.f;
@@ -244,7 +573,13 @@ __global__ __launch_bounds__(256) void lw_src_gather_kernel(LwGraph g, const flo
     const int p0 = g.out_ptr[(long)t * (g.P + 1) + j], p1 = g.out_ptr[(long)t * (g.P + 1) + j + 1];
     const int32_t* oq = g.out_q + (long)t * g.M;
     const float* mb = msg + (long)b * g.M * H;
-    for (int p = p0; p < p1; ++p) s += mb[(long)oq[p] * H + c];
+    for (int p = p0; p < p1; p += LW_U) {
+      float v[LW_U];
+#pragma unroll
+      for (int u = 0; u < LW_U; ++u) v[u] = p + u < p1 ? mb[(long)oq[p + u] * H + c] : 0.f;
+#pragma unroll
+      for (int u = 0; u < LW_U; ++u) s += v[u];
+    }
   }
   if (c < H) dxl[node * H + c] = s;
   if (wl) {
@@ -253,7 +588,7 @@ __global__ __launch_bounds__(256) void lw_src_gather_kernel(LwGraph g, const flo
     float d = 0.f;
     for (int k = 0; k < H; ++k) {
       const float lk = __shfl(s, k, NL), rk = __shfl(r, k, NL);
-      d += lk * wl[k * H + cc] + rk * wr[k * H + cc];
+      d += lk * lw_w[k * H + cc] + rk * lw_w[H * H + k * H + cc];
     }
     if (c < H) dh[node * H + c] = d;
   }
@@ -263,6 +598,352 @@ __global__ __launch_bounds__(256) void lw_src_gather_kernel(LwGraph g, const flo
 __global__ __launch_bounds__(256) void lw_relu_mask_kernel(float* dh, const float* h, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && !(h[i] > 0.f)) dh[i] = 0.f;
+}
+
+// Per-graph backward (x_l block in LDS): phase 1 = lw_attn_bwd_kernel per target node with the
+// message rows read from LDS; workgroup barrier (the block's global msg / dxr stores are visible to
+// it); phase 2 = lw_src_gather_kernel per source node (+ the input gradient, W_l, W_r in LDS).
+template <int NL>
+__global__ __launch_bounds__(256) void lw_graph_attn_bwd_kernel(LwGraph g, float* __restrict__ dh,
+                                                                const float* __restrict__ h_out,
+                                                                const float* __restrict__ xl,
+                                                                const float* __restrict__ xr,
+                                                                const float* __restrict__ alpha,
+                                                                const float* __restrict__ att, float* __restrict__ dxr,
+                                                                float* __restrict__ msg, float* __restrict__ datt,
+                                                                float* __restrict__ dxl, const float* __restrict__ wl,
+                                                                const float* __restrict__ wr, float* __restrict__ dh_in) {
+  // LDS: x_l [P][H], (W_l, W_r [H][H]), alpha [M], deg [P], in_ptr / out_ptr [P+1], in_src / out_q [M]
+  extern __shared__ __attribute__((aligned(16))) float lw_g[];
+  const int H = g.H, P = g.P, PH = P * H, M = g.M;
+  const int b = blockIdx.x;
+  const int t = g.topo[b];
+  float* s_xl = lw_g;
+  float* s_w = lw_g + PH;
+  float* al = s_w + (wl ? 2 * H * H : 0);
+  float* s_deg = al + M;
+  int32_t* iptr = reinterpret_cast<int32_t*>(s_deg + P);
+  int32_t* optr = iptr + P + 1;
+  int32_t* src = optr + P + 1;
+  int32_t* oq = src + M;
+  lw_stage_rows(xl, (long)b * P, P, H, s_xl);
+  if (wl) {
+    for (int k = threadIdx.x; k < H * H; k += blockDim.x) {
+      s_w[k] = wl[k];
+      s_w[H * H + k] = wr[k];
+    }
+  }
+  for (int k = threadIdx.x; k < M; k += blockDim.x) {
+    al[k] = alpha[(long)b * M + k];
+    src[k] = g.in_src[(long)t * M + k];
+    oq[k] = g.out_q[(long)t * M + k];
+  }
+  for (int k = threadIdx.x; k <= P; k += blockDim.x) {
+    iptr[k] = g.in_ptr[(long)t * (P + 1) + k];
+    optr[k] = g.out_ptr[(long)t * (P + 1) + k];
+    if (k < P) s_deg[k] = g.deg[(long)t * P + k];
+  }
+  __syncthreads();
+  const int n = g.nnodes[t];
+  const int c = threadIdx.x & (NL - 1);
+  const bool ch = c < H;
+  const int cc = ch ? c : 0;
+  const float ac = ch ? att[c] : 0.f;
+  float* mb = msg + (long)b * g.M * H;
+  for (int i = threadIdx.x / NL; i < P; i += 256 / NL) {
+    const long node = (long)b * P + i;
+    if (i >= n) {
+      if (ch) {
+        dh[node * H + c] = 0.f;
+        dxr[node * H + c] = 0.f;
+        datt[node * H + c] = 0.f;
+      }
+      continue;
+    }
+    float dy = ch ? dh[node * H + c] : 0.f;
+    if (h_out && ch && !(h_out[node * H + c] > 0.f)) dy = 0.f;
+    if (ch) dh[node * H + c] = dy;
+    const float gc = dy / s_deg[i];
+    const int q0 = iptr[i], q1 = iptr[i + 1];
+    const float xri = ch ? xr[node * H + c] : 0.f;
+    float sad = 0.f;
+    for (int q = q0; q < q1; q += LW_U) {
+      float xv[LW_U], a[LW_U];
+#pragma unroll
+      for (int u = 0; u < LW_U; ++u) {
+        const int qq = q + u;
+        xv[u] = (qq < q1 && ch) ? s_xl[src[qq] * H + c] : 0.f;
+        a[u] = qq < q1 ? al[qq] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < LW_U; ++u) sad += a[u] * lw_sum<NL>(gc * xv[u]);
+    }
+    float dxr_acc = 0.f, datt_acc = 0.f;
+    for (int q = q0; q < q1; q += LW_U) {
+      float xv[LW_U], a[LW_U];
+#pragma unroll
+      for (int u = 0; u < LW_U; ++u) {
+        const int qq = q + u;
+        xv[u] = (qq < q1 && ch) ? s_xl[src[qq] * H + c] : 0.f;
+        a[u] = qq < q1 ? al[qq] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < LW_U; ++u) {
+        const float da = lw_sum<NL>(gc * xv[u]);
+        const float de = a[u] * (da - sad);
+        const float z = xv[u] + xri;
+        const float dz = de * ac * (z > 0.f ? 1.f : kLwSlope);
+        if (q + u < q1) {
+          datt_acc += de * leaky(z);
+          dxr_acc += dz;
+          if (ch) mb[(long)(q + u) * H + c] = a[u] * gc + dz;
+        }
+      }
+    }
+    if (ch) {
+      dxr[node * H + c] = dxr_acc;
+      datt[node * H + c] = datt_acc;
+    }
+  }
+  __syncthreads();  // msg / dxr of this graph complete
+  for (int j = threadIdx.x / NL; j < P; j += 256 / NL) {
+    const long node = (long)b * P + j;
+    float sum = 0.f;
+    if (j < n && ch) {
+      const int p0 = optr[j], p1 = optr[j + 1];
+      for (int p = p0; p < p1; p += LW_U) {
+        float v[LW_U];
+#pragma unroll
+        for (int u = 0; u < LW_U; ++u) v[u] = p + u < p1 ? mb[(long)oq[p + u] * H + c] : 0.f;
+#pragma unroll
+        for (int u = 0; u < LW_U; ++u) sum += v[u];
+      }
+    }
+    if (ch) dxl[node * H + c] = sum;
+    if (wl) {
+      const float r = ch ? dxr[node * H + c] : 0.f;
+      float d = 0.f;
+      for (int k = 0; k < H; ++k) {
+        const float lk = __shfl(sum, k, NL), rk = __shfl(r, k, NL);
+        d += lk * s_w[k * H + cc] + rk * s_w[H * H + k * H + cc];
+      }
+      if (ch) dh_in[node * H + c] = d;
+    }
+  }
+}
+
+template <int HV>
+__device__ __forceinline__ void lw_load_row(float (&v)[HV], const float* src, int H) {
+  if ((((uintptr_t)src) & 7) == 0 && (H & 1) == 0) {
+#pragma unroll
+    for (int c = 0; c < HV; c += 2) {
+      if (c < H) {
+        const float2 f = *reinterpret_cast<const float2*>(src + c);
+        v[c] = f.x;
+        v[c + 1] = f.y;
+      } else {
+        v[c] = 0.f;
+        v[c + 1] = 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < HV; ++c) v[c] = c < H ? src[c] : 0.f;
+  }
+}
+
+// Lane-per-node backward (H <= 32), one workgroup per graph, no per-message rows in memory:
+// phase 1, lane = target node i -- dY (ReLU gate), g_i = dY / deg_i, the softmax / score terms
+// over its in-messages (x_l rows from LDS): d x_r, d att rows, and per message q the scalar
+// de_q = alpha_q (da_q - sum alpha da) and its target (LDS), g_i rows (LDS); barrier; x_r rows
+// replace x_l in LDS; phase 2, lane = source node j -- d x_l[j] = sum over its out-messages (fixed
+// source-sorted order) of alpha_q g_i + de_q att * LeakyReLU'(x_l[j] + x_r[i]), recomputed from
+// LDS, and with wl the input gradient d x_l W_l + d x_r W_r (W rows broadcast from LDS).  Same
+// arithmetic as lw_attn_bwd_kernel + lw_src_gather_kernel.
+template <int HV>
+__global__ __launch_bounds__(256) void lw_lane_attn_bwd_kernel(LwGraph g, float* __restrict__ dh,
+                                                               const float* __restrict__ h_out,
+                                                               const float* __restrict__ xl,
+                                                               const float* __restrict__ xr,
+                                                               const float* __restrict__ alpha,
+                                                               const float* __restrict__ att, float* __restrict__ dxr,
+                                                               float* __restrict__ datt, float* __restrict__ dxl,
+                                                               const float* __restrict__ wl,
+                                                               const float* __restrict__ wr, float* __restrict__ dh_in) {
+  // LDS: rows [P][HV] (x_l, then x_r), g [P][HV], (W_l, W_r [H][HV]), alpha, de [M], deg [P],
+  //      in_ptr / out_ptr [P+1], in_src / out_q / target [M]
+  extern __shared__ __attribute__((aligned(16))) float lw_g[];
+  const int H = g.H, P = g.P, M = g.M;
+  const int b = blockIdx.x, t = g.topo[b];
+  float* s_rows = lw_g;
+  float* s_g = s_rows + P * HV;
+  float* s_w = s_g + P * HV;
+  float* al = s_w + (wl ? 2 * H * HV : 0);
+  float* s_de = al + M;
+  float* s_deg = s_de + M;
+  int32_t* iptr = reinterpret_cast<int32_t*>(s_deg + P);
+  int32_t* optr = iptr + P + 1;
+  int32_t* src = optr + P + 1;
+  int32_t* oq = src + M;
+  int32_t* tgt = oq + M;
+  const long base = (long)b * P * H;
+  for (int k = threadIdx.x; k < P * HV; k += 256) {
+    const int r = k / HV, c = k - r * HV;
+    s_rows[k] = c < H ? xl[base + (long)r * H + c] : 0.f;
+    s_g[k] = 0.f;
+  }
+  if (wl) {
+    for (int k = threadIdx.x; k < H * HV; k += 256) {
+      const int r = k / HV, c = k - r * HV;
+      s_w[k] = c < H ? wl[r * H + c] : 0.f;
+      s_w[H * HV + k] = c < H ? wr[r * H + c] : 0.f;
+    }
+  }
+  for (int k = threadIdx.x; k < M; k += 256) {
+    al[k] = alpha[(long)b * M + k];
+    src[k] = g.in_src[(long)t * M + k];
+    oq[k] = g.out_q[(long)t * M + k];
+    s_de[k] = 0.f;
+    tgt[k] = 0;
+  }
+  for (int k = threadIdx.x; k <= P; k += 256) {
+    iptr[k] = g.in_ptr[(long)t * (P + 1) + k];
+    optr[k] = g.out_ptr[(long)t * (P + 1) + k];
+    if (k < P) s_deg[k] = g.deg[(long)t * P + k];
+  }
+  __syncthreads();
+  float a_[HV];
+#pragma unroll
+  for (int c = 0; c < HV; ++c) a_[c] = c < H ? att[c] : 0.f;
+  const int n = g.nnodes[t];
+  for (int i = threadIdx.x; i < P; i += 256) {
+    const long node = (long)b * P + i;
+    float d1[HV], d2[HV];  // d x_r, d att
+#pragma unroll
+    for (int c = 0; c < HV; ++c) {
+      d1[c] = 0.f;
+      d2[c] = 0.f;
+    }
+    if (i < n) {
+      float gc[HV], xri[HV];
+      lw_load_row<HV>(gc, dh + node * H, H);
+      if (h_out) {
+        float ho[HV];
+        lw_load_row<HV>(ho, h_out + node * H, H);
+#pragma unroll
+        for (int c = 0; c < HV; ++c) gc[c] = ho[c] > 0.f ? gc[c] : 0.f;
+      }
+      lw_store_row<HV>(dh + node * H, gc, H);  // dY (the bias gradient's rows)
+      const float inv_deg = 1.f / s_deg[i];
+#pragma unroll
+      for (int c = 0; c < HV; ++c) {
+        gc[c] *= inv_deg;
+        s_g[i * HV + c] = gc[c];
+      }
+      lw_load_row<HV>(xri, xr + node * H, H);
+      const int q0 = iptr[i], q1 = iptr[i + 1];
+      float sad = 0.f;
+      for (int q = q0; q < q1; ++q) {
+        const float4* row = reinterpret_cast<const float4*>(s_rows + src[q] * HV);
+        float da = 0.f;
+#pragma unroll
+        for (int v = 0; v < HV / 4; ++v) {
+          const float4 f = row[v];
+          da += gc[4 * v] * f.x + gc[4 * v + 1] * f.y + gc[4 * v + 2] * f.z + gc[4 * v + 3] * f.w;
+        }
+        sad += al[q] * da;
+      }
+      for (int q = q0; q < q1; ++q) {
+        const float4* row = reinterpret_cast<const float4*>(s_rows + src[q] * HV);
+        float xj[HV];
+#pragma unroll
+        for (int v = 0; v < HV / 4; ++v) {
+          const float4 f = row[v];
+          xj[4 * v] = f.x;
+          xj[4 * v + 1] = f.y;
+          xj[4 * v + 2] = f.z;
+          xj[4 * v + 3] = f.w;
+        }
+        float da = 0.f;
+#pragma unroll
+        for (int c = 0; c < HV; ++c) da += gc[c] * xj[c];
+        const float de = al[q] * (da - sad);
+        s_de[q] = de;
+        tgt[q] = i;
+#pragma unroll
+        for (int c = 0; c < HV; ++c) {
+          const float z = xj[c] + xri[c];
+          d2[c] += de * leaky(z);
+          d1[c] += de * a_[c] * (z > 0.f ? 1.f : kLwSlope);
+        }
+      }
+    } else {
+      float z[HV];
+#pragma unroll
+      for (int c = 0; c < HV; ++c) z[c] = 0.f;
+      lw_store_row<HV>(dh + node * H, z, H);
+    }
+    lw_store_row<HV>(dxr + node * H, d1, H);
+    lw_store_row<HV>(datt + node * H, d2, H);
+  }
+  __syncthreads();  // phase 1 done with x_l in LDS; g / de / targets complete
+  for (int k = threadIdx.x; k < P * HV; k += 256) {
+    const int r = k / HV, c = k - r * HV;
+    s_rows[k] = c < H ? xr[base + (long)r * H + c] : 0.f;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < P; j += 256) {
+    const long node = (long)b * P + j;
+    float s[HV];
+#pragma unroll
+    for (int c = 0; c < HV; ++c) s[c] = 0.f;
+    if (j < n) {
+      float xlj[HV];
+      lw_load_row<HV>(xlj, xl + node * H, H);
+      const int p0 = optr[j], p1 = optr[j + 1];
+      for (int p = p0; p < p1; ++p) {
+        const int q = oq[p];
+        const int i = tgt[q];
+        const float aq = al[q], de = s_de[q];
+        const float4* xr4 = reinterpret_cast<const float4*>(s_rows + i * HV);
+        const float4* g4 = reinterpret_cast<const float4*>(s_g + i * HV);
+#pragma unroll
+        for (int v = 0; v < HV / 4; ++v) {
+          const float4 fr = xr4[v], fg = g4[v];
+          const float zr[4] = {fr.x, fr.y, fr.z, fr.w}, gg[4] = {fg.x, fg.y, fg.z, fg.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = 4 * v + e;
+            const float z = xlj[c] + zr[e];
+            s[c] += aq * gg[e] + de * a_[c] * (z > 0.f ? 1.f : kLwSlope);
+          }
+        }
+      }
+    }
+    lw_store_row<HV>(dxl + node * H, s, H);
+    if (wl) {
+      float r[HV], d[HV];
+      lw_load_row<HV>(r, dxr + node * H, H);  // written by this lane in phase 1 (same node)
+#pragma unroll
+      for (int c = 0; c < HV; ++c) d[c] = 0.f;
+#pragma unroll
+      for (int co = 0; co < HV; ++co) {
+        if (co < H) {
+          const float4* wl4 = reinterpret_cast<const float4*>(s_w + co * HV);
+          const float4* wr4 = reinterpret_cast<const float4*>(s_w + H * HV + co * HV);
+#pragma unroll
+          for (int v = 0; v < HV / 4; ++v) {
+            const float4 fl = wl4[v], fr = wr4[v];
+            d[4 * v] += s[co] * fl.x + r[co] * fr.x;
+            d[4 * v + 1] += s[co] * fl.y + r[co] * fr.y;
+            d[4 * v + 2] += s[co] * fl.z + r[co] * fr.z;
+            d[4 * v + 3] += s[co] * fl.w + r[co] * fr.w;
+          }
+        }
+      }
+      lw_store_row<HV>(dh_in + node * H, d, H);
+    }
+  }
 }
 
 // Deterministic column sums of x [R, C] (row stride ldx, C <= 256): phase 1 -- block k sums rows
@@ -304,6 +985,102 @@ __global__ __launch_bounds__(256) void lw_colsum_p2_kernel(const float* __restri
   if (t == 0) out[c] = accumulate ? out[c] + red[0] : red[0];
 }
 
+// First conv's node linears from a narrow input (Fi small, e.g. 3 features): x_l = x W_l^T + b_l and
+// x_r likewise in one pass (thread = (row, channel); the weights are L1-resident).
+__global__ __launch_bounds__(256) void lw_node_linear_kernel(const float* __restrict__ x, long R, int Fi, int H,
+                                                             const float* __restrict__ wl, const float* __restrict__ bl,
+                                                             const float* __restrict__ wr, const float* __restrict__ br,
+                                                             float* __restrict__ xl, float* __restrict__ xr) {
+  const long total = R * H;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / H;
+    const int c = (int)(i - r * H);
+    float a = bl[c], b = br[c];
+    for (int k = 0; k < Fi; ++k) {
+      const float v = x[r * Fi + k];
+      a += wl[c * Fi + k] * v;
+      b += wr[c * Fi + k] * v;
+    }
+    xl[i] = a;
+    xr[i] = b;
+  }
+}
+
+// All parameter gradients of one conv in one pass over its rows (phase 1; phase 2 = lw_colsum_p2 over
+// the C outputs): out = [dW_l = dxl^T h | db_l = 1^T dxl | dW_r = dxr^T h | db_r | d att = 1^T datt |
+// d bias = 1^T dy] -- the conv's block layout in the flat gradient.  Block k takes rows
+// [k chunk, (k+1) chunk) in stages of LW_RB rows: the five row blocks are contiguous in memory and
+// copied to LDS with 16-byte loads; thread t owns outputs t + 256 i and sums the stage rows in order
+// (fp32, deterministic).
+constexpr int LW_RB = 64;
+__device__ __forceinline__ void lw_stage_rows(const float* __restrict__ src, long r0, int nr, int w, float* dst) {
+  const float* p = src + r0 * w;
+  const int n = nr * w;
+  if (((uintptr_t)p & 15) == 0 && ((uintptr_t)dst & 15) == 0 && (n & 3) == 0) {
+    for (int k = threadIdx.x; k < (n >> 2); k += 256)
+      reinterpret_cast<float4*>(dst)[k] = reinterpret_cast<const float4*>(p)[k];
+  } else {
+    for (int k = threadIdx.x; k < n; k += 256) dst[k] = p[k];
+  }
+}
+
+template <int NO>
+__global__ __launch_bounds__(256) void lw_conv_grads_kernel(const float* __restrict__ dxl, const float* __restrict__ dxr,
+                                                            const float* __restrict__ datt, const float* __restrict__ dy,
+                                                            const float* __restrict__ hin, long R, int H, int Fi,
+                                                            long chunk, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lw_rows[];  // [dxl | dxr | datt | dy][LW_RB][H], h [LW_RB][Fi]
+  const int C = 2 * H * Fi + 4 * H, HF = H * Fi, S = LW_RB * H;
+  float* s_h = lw_rows + 4 * S;
+  const long r0 = (long)blockIdx.x * chunk;
+  const long r1 = r0 + chunk < R ? r0 + chunk : R;
+  // output o -> (first factor: block + channel, second factor: h column or none)
+  int fa[NO], fb[NO];
+  float acc[NO];
+#pragma unroll
+  for (int i = 0; i < NO; ++i) {
+    const int o = threadIdx.x + 256 * i;
+    acc[i] = 0.f;
+    fa[i] = 0;
+    fb[i] = -1;
+    if (o < HF) { fa[i] = o / Fi; fb[i] = o % Fi; }
+    else if (o < HF + H) { fa[i] = o - HF; }
+    else if (o < 2 * HF + H) { fa[i] = S + (o - HF - H) / Fi; fb[i] = (o - HF - H) % Fi; }
+    else if (o < 2 * HF + 2 * H) { fa[i] = S + (o - 2 * HF - H); }
+    else if (o < 2 * HF + 3 * H) { fa[i] = 2 * S + (o - 2 * HF - 2 * H); }
+    else if (o < C) { fa[i] = 3 * S + (o - 2 * HF - 3 * H); }
+  }
+  for (long rb = r0; rb < r1; rb += LW_RB) {
+    const int nr = (int)(r1 - rb < LW_RB ? r1 - rb : LW_RB);
+    lw_stage_rows(dxl, rb, nr, H, lw_rows);
+    lw_stage_rows(dxr, rb, nr, H, lw_rows + S);
+    lw_stage_rows(datt, rb, nr, H, lw_rows + 2 * S);
+    lw_stage_rows(dy, rb, nr, H, lw_rows + 3 * S);
+    lw_stage_rows(hin, rb, nr, Fi, s_h);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NO; ++i) {
+      if ((int)threadIdx.x + 256 * i < C) {
+        float a = acc[i];
+        const float* pa = lw_rows + fa[i];
+        if (fb[i] >= 0) {
+          const float* pb = s_h + fb[i];
+          for (int row = 0; row < nr; ++row) a += pa[row * H] * pb[row * Fi];
+        } else {
+          for (int row = 0; row < nr; ++row) a += pa[row * H];
+        }
+        acc[i] = a;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < NO; ++i) {
+    const int o = threadIdx.x + 256 * i;
+    if (o < C) part[(long)blockIdx.x * C + o] = acc[i];
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------
 static LwGraph lw_graph(py::dict t, uintptr_t topo, int B, int P, int H) {
   LwGraph g{};
@@ -330,8 +1107,12 @@ static dim3 node_grid(const LwGraph& g) {
 }
 
 // next = (wl, bl, wr, br, xl_out, xr_out) of the following conv (H -> H), or () for the last conv
+void lw_pool(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t h, uintptr_t emb, uintptr_t stream);
+
+// emb (last conv, optional): also the mean pool into emb [B][H] (fused on the lane-per-node path)
 void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t xl, uintptr_t xr, uintptr_t att,
-                 uintptr_t bias, int relu, uintptr_t h_out, uintptr_t alpha, uintptr_t stream, py::tuple next) {
+                 uintptr_t bias, int relu, uintptr_t h_out, uintptr_t alpha, uintptr_t stream, py::tuple next,
+                 uintptr_t emb) {
   const LwGraph g = lw_graph(tables, topo, B, P, H);
   LwNext nx{};
   if (next.size() == 6) {
@@ -344,12 +1125,37 @@ void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
   } else {
     GSC_CHECK(next.size() == 0, "lw_attn_fwd: next = (wl, bl, wr, br, xl, xr) or ()");
   }
+  if (H <= 32) {  // lane per node
+    const int hv = H <= 8 ? 8 : H <= 16 ? 16 : H <= 24 ? 24 : 32;
+    const size_t lds = sizeof(float) * ((size_t)P * hv + (nx.wl ? 2 * H * hv : 0) + 2 * g.M + 2 * P + 1);
+    if (lds <= 64 * 1024) {
+      auto kl = hv == 8 ? lw_lane_attn_fwd_kernel<8>
+                : hv == 16 ? lw_lane_attn_fwd_kernel<16> : hv == 24 ? lw_lane_attn_fwd_kernel<24>
+                                                           : lw_lane_attn_fwd_kernel<32>;
+      hipLaunchKernelGGL(kl, dim3(B), dim3(256), lds, stream_of(stream), g, ptr<const float>(xl), ptr<const float>(xr),
+                         ptr<const float>(att), ptr<const float>(bias), relu, ptr<float>(h_out), ptr<float>(alpha), nx,
+                         ptr<float>(emb));
+      check_launch();
+      return;
+    }
+  }
+  const size_t graph_lds = sizeof(float) * (2L * P * H + (nx.wl ? 2L * H * H : 0) + (P + 1) + g.M + P);
+  if (graph_lds <= 64 * 1024) {  // per-graph blocks (>= 2 workgroups per CU)
+    auto kg = lanes_per_node(g) == 32 ? lw_graph_attn_fwd_kernel<32> : lw_graph_attn_fwd_kernel<64>;
+    hipLaunchKernelGGL(kg, dim3(B), dim3(256), graph_lds, stream_of(stream), g, ptr<const float>(xl),
+                       ptr<const float>(xr), ptr<const float>(att), ptr<const float>(bias), relu, ptr<float>(h_out),
+                       ptr<float>(alpha), nx);
+    check_launch();
+    if (emb) lw_pool(tables, topo, B, P, H, h_out, emb, stream);
+    return;
+  }
   const size_t lds = nx.wl ? 2 * sizeof(float) * H * H : 0;
   auto k = lanes_per_node(g) == 32 ? lw_attn_fwd_kernel<32> : lw_attn_fwd_kernel<64>;
   hipLaunchKernelGGL(k, node_grid(g), dim3(256), lds, stream_of(stream), g, ptr<const float>(xl),
                      ptr<const float>(xr), ptr<const float>(att), ptr<const float>(bias), relu, ptr<float>(h_out),
                      ptr<float>(alpha), nx);
   check_launch();
+  if (emb) lw_pool(tables, topo, B, P, H, h_out, emb, stream);
 }
 
 void lw_pool(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t h, uintptr_t emb, uintptr_t stream) {
@@ -386,9 +1192,46 @@ void lw_src_gather(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr
   const LwGraph g = lw_graph(tables, topo, B, P, H);
   GSC_CHECK(!wl || (dxr && wr && dh), "lw_src_gather: the input gradient needs dxr, wl, wr, dh");
   auto k = lanes_per_node(g) == 32 ? lw_src_gather_kernel<32> : lw_src_gather_kernel<64>;
-  hipLaunchKernelGGL(k, node_grid(g), dim3(256), 0, stream_of(stream), g, ptr<const float>(msg), ptr<float>(dxl),
+  const size_t lds = wl ? 2 * sizeof(float) * H * H : 0;
+  hipLaunchKernelGGL(k, node_grid(g), dim3(256), lds, stream_of(stream), g, ptr<const float>(msg), ptr<float>(dxl),
                      ptr<const float>(dxr), ptr<const float>(wl), ptr<const float>(wr), ptr<float>(dh));
   check_launch();
+}
+
+// attention backward + source gather (+ input gradient when wl): one per-graph launch when the
+// graph's x_l block fits the LDS budget, else the per-node kernels
+void lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t dh, uintptr_t h_out, uintptr_t xl,
+                        uintptr_t xr, uintptr_t alpha, uintptr_t att, uintptr_t dxr, uintptr_t msg, uintptr_t datt,
+                        uintptr_t dxl, uintptr_t wl, uintptr_t wr, uintptr_t dh_in, uintptr_t stream) {
+  const LwGraph g = lw_graph(tables, topo, B, P, H);
+  GSC_CHECK(!wl || (wr && dh_in), "lw_attn_bwd_gather: the input gradient needs wl, wr, dh_in");
+  if (H <= 32) {  // lane per node
+    const int hv = H <= 8 ? 8 : H <= 16 ? 16 : H <= 24 ? 24 : 32;
+    const size_t ll = sizeof(float) * (2 * (size_t)P * hv + (wl ? 2 * H * hv : 0) + 5 * g.M + P + 2 * (P + 1));
+    if (ll <= 80 * 1024) {  // >= 2 workgroups per CU
+      auto kl = hv == 8 ? lw_lane_attn_bwd_kernel<8>
+                : hv == 16 ? lw_lane_attn_bwd_kernel<16> : hv == 24 ? lw_lane_attn_bwd_kernel<24>
+                                                           : lw_lane_attn_bwd_kernel<32>;
+      hipLaunchKernelGGL(kl, dim3(B), dim3(256), ll, stream_of(stream), g, ptr<float>(dh), ptr<const float>(h_out),
+                         ptr<const float>(xl), ptr<const float>(xr), ptr<const float>(alpha), ptr<const float>(att),
+                         ptr<float>(dxr), ptr<float>(datt), ptr<float>(dxl), ptr<const float>(wl),
+                         ptr<const float>(wr), ptr<float>(dh_in));
+      check_launch();
+      return;
+    }
+  }
+  const size_t lds = sizeof(float) * ((size_t)P * H + (wl ? 2 * H * H : 0) + g.M + P + 2 * (P + 1) + 2 * g.M);
+  if (lds <= 64 * 1024) {
+    auto k = lanes_per_node(g) == 32 ? lw_graph_attn_bwd_kernel<32> : lw_graph_attn_bwd_kernel<64>;
+    hipLaunchKernelGGL(k, dim3(B), dim3(256), lds, stream_of(stream), g, ptr<float>(dh), ptr<const float>(h_out),
+                       ptr<const float>(xl), ptr<const float>(xr), ptr<const float>(alpha), ptr<const float>(att),
+                       ptr<float>(dxr), ptr<float>(msg), ptr<float>(datt), ptr<float>(dxl), ptr<const float>(wl),
+                       ptr<const float>(wr), ptr<float>(dh_in));
+    check_launch();
+    return;
+  }
+  lw_attn_bwd(tables, topo, B, P, H, dh, h_out, xl, xr, alpha, att, dxr, msg, datt, stream);
+  lw_src_gather(tables, topo, B, P, H, msg, dxl, stream, dxr, wl, wr, dh_in);
 }
 
 void lw_relu_mask(uintptr_t dh, uintptr_t h, long n, uintptr_t stream) {
@@ -409,11 +1252,53 @@ void lw_colsum(uintptr_t x, long R, int C, long ldx, uintptr_t part, uintptr_t o
   check_launch();
 }
 
+void lw_node_linear(uintptr_t x, long R, int Fi, int H, uintptr_t wl, uintptr_t bl, uintptr_t wr, uintptr_t br,
+                    uintptr_t xl, uintptr_t xr, uintptr_t stream) {
+  long g = (R * H + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(lw_node_linear_kernel, dim3((unsigned)g), dim3(256), 0, stream_of(stream), ptr<const float>(x), R, Fi,
+                     H, ptr<const float>(wl), ptr<const float>(bl), ptr<const float>(wr), ptr<const float>(br),
+                     ptr<float>(xl), ptr<float>(xr));
+  check_launch();
+}
+
+// part must hold >= min(R, 1024) x (2 H Fi + 4 H) floats; out = the conv's gradient block
+void lw_conv_grads(uintptr_t dxl, uintptr_t dxr, uintptr_t datt, uintptr_t dy, uintptr_t hin, long R, int H, int Fi,
+                   uintptr_t part, long part_floats, uintptr_t out, int accumulate, uintptr_t stream) {
+  const int C = 2 * H * Fi + 4 * H;
+  const long chunk = R <= 1024 ? 1 : (R + 1023) / 1024;
+  const int K = (int)((R + chunk - 1) / chunk);
+  GSC_CHECK((long)K * C <= part_floats, "lw_conv_grads: partials buffer too small");
+  const int no = (C + 255) / 256;
+  const size_t lds = sizeof(float) * LW_RB * (4 * H + Fi);  // 4 S is a multiple of 4 floats: s_h stays aligned
+  const hipStream_t s = stream_of(stream);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(K), dim3(256), lds, s, ptr<const float>(dxl), ptr<const float>(dxr),
+                       ptr<const float>(datt), ptr<const float>(dy), ptr<const float>(hin), R, H, Fi, chunk,
+                       ptr<float>(part));
+  };
+  if (no <= 1) go(lw_conv_grads_kernel<1>);
+  else if (no <= 2) go(lw_conv_grads_kernel<2>);
+  else if (no <= 5) go(lw_conv_grads_kernel<5>);
+  else if (no <= 9) go(lw_conv_grads_kernel<9>);
+  else if (no <= 17) go(lw_conv_grads_kernel<17>);
+  else {
+    GSC_CHECK(no <= 36, "lw_conv_grads: at most 64 channels");
+    go(lw_conv_grads_kernel<36>);
+  }
+  check_launch();
+  hipLaunchKernelGGL(lw_colsum_p2_kernel, dim3(C), dim3(256), 0, s, ptr<const float>(part), K, C, ptr<float>(out),
+                     accumulate);
+  check_launch();
+}
+
 void register_gnn_lw(py::module_& m) {
+  m.def("lw_node_linear", &lw_node_linear, "layer-wise GATv2: first conv's node linears (narrow input)");
+  m.def("lw_conv_grads", &lw_conv_grads, "layer-wise GATv2: every parameter gradient of one conv (one pass)");
   m.def("lw_attn_fwd", &lw_attn_fwd, "layer-wise GATv2: attention + aggregation (+ReLU), alpha saved; optionally "
         "the next conv's node linears", py::arg("tables"), py::arg("topo"), py::arg("B"), py::arg("P"), py::arg("H"),
         py::arg("xl"), py::arg("xr"), py::arg("att"), py::arg("bias"), py::arg("relu"), py::arg("h_out"),
-        py::arg("alpha"), py::arg("stream"), py::arg("next") = py::tuple());
+        py::arg("alpha"), py::arg("stream"), py::arg("next") = py::tuple(), py::arg("emb") = 0);
   m.def("lw_pool", &lw_pool, "layer-wise GATv2: mean pool over real nodes");
   m.def("lw_pool_bwd", &lw_pool_bwd, "layer-wise GATv2: mean-pool backward");
   m.def("lw_attn_bwd", &lw_attn_bwd, "layer-wise GATv2: attention backward per target node");
@@ -421,6 +1306,8 @@ void register_gnn_lw(py::module_& m) {
         py::arg("tables"), py::arg("topo"), py::arg("B"), py::arg("P"), py::arg("H"), py::arg("msg"), py::arg("dxl"),
         py::arg("stream"), py::arg("dxr") = 0, py::arg("wl") = 0, py::arg("wr") = 0, py::arg("dh") = 0);
   m.def("lw_relu_mask", &lw_relu_mask, "dh *= (h > 0)");
+  m.def("lw_attn_bwd_gather", &lw_attn_bwd_gather,
+        "layer-wise GATv2: attention backward + source gather (+ input gradient), per graph when it fits");
   m.def("lw_colsum", &lw_colsum, "deterministic column sums (two phases)");
 }
 

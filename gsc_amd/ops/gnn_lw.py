@@ -2,12 +2,12 @@
 kernels (``gnn_fits`` false: e.g. the 200-node synthetic topologies of BASELINE config 5).
 
 Per conv (``csrc/ops/gnn_lw.hip``): node linears ``x_l = h W_l^T + b_l``, ``x_r = h W_r^T + b_r``
-(first conv: the MFMA GEMM engine over all ``B x P`` node rows; later convs: in the previous
-attention kernel's epilogue); attention + online segment softmax + mean aggregation (+ bias, ReLU) per
+(first conv: one pass over all ``B x P`` node rows -- the MFMA GEMM engine for inputs wider than 8
+features; later convs: in the previous attention kernel's epilogue); attention + online segment softmax + mean aggregation (+ bias, ReLU) per
 target node; mean pool per graph.  Backward: attention backward per target node (``d x_r`` gathered
 per target, ``d x_l`` per source through the source-sorted CSR, with the input gradient
-``dX W`` in the same gather), weight gradients ``dW = dX^T h`` (split-K GEMM, deterministic
-reduction), vector gradients by deterministic column sums.  Same semantics as ``gatv2_dense_reference``
+``dX W`` in the same gather), weight every parameter gradient of the conv (``dW = dX^T h``, bias / attention vectors) in one pass over its
+rows with a deterministic two-phase reduction.  Same semantics as ``gatv2_dense_reference``
 (reference ``src/rlsp/agents/models.py:10-53``).
 
 A :class:`LayerwiseGAT` owns the workspaces of one batch size; ``forward`` keeps every conv's
@@ -54,6 +54,7 @@ class LayerwiseGAT:
         self.dxl, self.dxr, self.datt = mk(R, H), mk(R, H), mk(R, H)
         self.msg = mk(self.B * M, H)
         self.part = mk(1024 * max(H, 32))
+        self.part_conv = mk(1024 * (2 * H * max(H, Fin) + 4 * H))   # per-block partials of lw_conv_grads
         self.slabs = mk(max(4 << 20, 64 * H * max(H, Fin)))
         self.topo32 = None
 
@@ -92,8 +93,12 @@ class LayerwiseGAT:
         for l, blk in enumerate(self.layer_of):
             Fi, Wl, bl, Wr, br, att, bias = self._params(flat, blk)
             if l == 0:   # later convs' node linears come from the previous attention kernel
-                gemm(h, Wl, "nt", out32=self.xl[l], bias=bl)
-                gemm(h, Wr, "nt", out32=self.xr[l], bias=br)
+                if Fi <= 8:
+                    nat.lw_node_linear(h.data_ptr(), B * P, Fi, H, Wl.data_ptr(), bl.data_ptr(), Wr.data_ptr(),
+                                       br.data_ptr(), self.xl[l].data_ptr(), self.xr[l].data_ptr(), s)
+                else:
+                    gemm(h, Wl, "nt", out32=self.xl[l], bias=bl)
+                    gemm(h, Wr, "nt", out32=self.xr[l], bias=br)
             nxt = ()
             if l + 1 < self.L:
                 _, Wl2, bl2, Wr2, br2, _, _ = self._params(flat, self.layer_of[l + 1])
@@ -101,9 +106,8 @@ class LayerwiseGAT:
                        self.xr[l + 1].data_ptr())
             nat.lw_attn_fwd(t, topo32.data_ptr(), B, P, H, self.xl[l].data_ptr(), self.xr[l].data_ptr(),
                             att.data_ptr(), bias.data_ptr(), int(self._relu(l)), self.hout[l].data_ptr(),
-                            self.alpha[l].data_ptr(), s, nxt)
-            h = self.hout[l]
-        nat.lw_pool(t, topo32.data_ptr(), B, P, H, self.hout[self.L - 1].data_ptr(), emb.data_ptr(), s)
+                            self.alpha[l].data_ptr(), s, nxt, emb.data_ptr() if l + 1 == self.L else 0)
+            h = self.hout[l]   # the last conv also writes the mean pool into emb
 
     def backward(self, flat: torch.Tensor, demb: torch.Tensor, grad: torch.Tensor) -> None:
         """Gradients of the last ``forward`` into ``grad`` (fp32, module order; overwritten)."""
@@ -120,16 +124,16 @@ class LayerwiseGAT:
             acc = blk in seen
             seen.add(blk)
             hin = self.x.view(R, self.Fin) if l == 0 else self.hout[l - 1]
-            nat.lw_attn_bwd(t, tp, B, P, H, cur.data_ptr(), self.hout[l].data_ptr() if self._relu(l) else 0,
-                            self.xl[l].data_ptr(), self.xr[l].data_ptr(), self.alpha[l].data_ptr(), att.data_ptr(),
-                            self.dxr.data_ptr(), self.msg.data_ptr(), self.datt.data_ptr(), s)
-            # l > 0: the gather also writes the input gradient dxl W_l + dxr W_r into nxt
-            nat.lw_src_gather(t, tp, B, P, H, self.msg.data_ptr(), self.dxl.data_ptr(), s, self.dxr.data_ptr(),
-                              Wl.data_ptr() if l > 0 else 0, Wr.data_ptr() if l > 0 else 0,
-                              nxt.data_ptr() if l > 0 else 0)
-            gemm(self.dxl, hin, "tn", out32=gWl, splits=None, slabs=self.slabs, accumulate=acc)
-            gemm(self.dxr, hin, "tn", out32=gWr, splits=None, slabs=self.slabs, accumulate=acc)
-            for src, dst in ((self.dxl, gbl), (self.dxr, gbr), (self.datt, gatt), (cur, gbias)):
-                nat.lw_colsum(src.data_ptr(), R, H, H, self.part.data_ptr(), dst.data_ptr(), int(acc), s)
+            # attention backward + d x_l gather; l > 0: also the input gradient dxl W_l + dxr W_r into nxt
+            nat.lw_attn_bwd_gather(t, tp, B, P, H, cur.data_ptr(), self.hout[l].data_ptr() if self._relu(l) else 0,
+                                   self.xl[l].data_ptr(), self.xr[l].data_ptr(), self.alpha[l].data_ptr(),
+                                   att.data_ptr(), self.dxr.data_ptr(), self.msg.data_ptr(), self.datt.data_ptr(),
+                                   self.dxl.data_ptr(), Wl.data_ptr() if l > 0 else 0, Wr.data_ptr() if l > 0 else 0,
+                                   nxt.data_ptr() if l > 0 else 0, s)
+            # dW_l | db_l | dW_r | db_r | d att | d bias in one pass (the block's layout in the flat gradient)
+            assert gWl.data_ptr() == grad.data_ptr() + 4 * _block_offset(blk, self.Fin, H)
+            nat.lw_conv_grads(self.dxl.data_ptr(), self.dxr.data_ptr(), self.datt.data_ptr(), cur.data_ptr(),
+                              hin.data_ptr(), R, H, Fi, self.part_conv.data_ptr(), self.part_conv.numel(),
+                              gWl.data_ptr(), int(acc), s)
             if l > 0:
                 cur, nxt = nxt, cur

@@ -1,5 +1,5 @@
-"""GPU: layer-wise GATv2 kernels (MFMA GEMM node linears + per-node attention kernels) vs the fp32
-PyTorch reference -- the native path for graphs beyond one CU's LDS (200-node syn topologies,
+"""GPU: layer-wise GATv2 kernels (node linears, per-graph / per-node attention kernels, one-pass conv
+gradients) vs the fp32 PyTorch reference -- the native path for graphs beyond one CU's LDS (200-node syn topologies,
 BASELINE config 5); also exercised on 50-node and Abilene graphs by calling it directly."""
 import pytest
 import torch
@@ -94,3 +94,10 @@ def test_layerwise_wide_hidden(hidden):
     gs = GraphSet([load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml")),
                    load_topology(cfg_path("networks", "bteurope", "bteurope-in4-rand-cap0-2.graphml"))], 24, DEV)
     _check(gs, 24, 333, hidden=hidden, direct=True)
+
+
+def test_layerwise_200_nodes_wide_hidden_per_node_kernel():
+    """200 nodes x 64 channels: the graph's x_l / x_r block (100 KB) exceeds the per-graph kernel's LDS
+    budget, so the forward takes the per-node attention kernel."""
+    gs = GraphSet([load_topology(p) for p in SYN200[:2]], 200, DEV)
+    _check(gs, 200, 24, hidden=64, direct=True)
