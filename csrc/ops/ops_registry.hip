@@ -9,6 +9,7 @@ void register_mlp(py::module_& m);
 void register_streams(py::module_& m);
 void register_replay(py::module_& m);
 void register_gnn_lw(py::module_& m);
+void register_actor_proj(py::module_& m);
 void register_ops(py::module_& m) {
   register_explore(m);
   register_gnn(m);
@@ -17,5 +18,6 @@ void register_ops(py::module_& m) {
   register_streams(m);
   register_replay(m);
   register_gnn_lw(m);
+  register_actor_proj(m);
 }
 }  // namespace gsc

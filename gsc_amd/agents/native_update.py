@@ -104,6 +104,11 @@ class NativeDDPGUpdate:
         c1 = self.critic.width(0)
         self.compose = (os.environ.get("GSC_COMPOSE", "1") != "0" and self.actor.nh >= 1
                         and T * c1 <= min(B, 1024))
+        # TD target: target actor output layer + target critic action projection in one kernel
+        # (csrc/ops/actor_proj.hip, no [B, A] action matrix)
+        hl0 = self.actor.width(self.actor.nh - 1) if self.actor.nh else 0
+        self.fuse_target = (os.environ.get("GSC_FUSE_TARGET", "1") != "0" and self.actor.nh >= 1 and T <= 4
+                            and c1 <= 64 and hl0 in (64, 128, 256) and A % 8 == 0)
         self.graphs = L.graphs
         self.tables = _tables(L.graphs)
         self.layer_of = _layer_of(L.actor.embedder)
@@ -114,7 +119,8 @@ class NativeDDPGUpdate:
         self.hid_a = [mk(B, self.actor.width(i), dt=BF16) for i in range(self.actor.nh)]
         self.hid_ta = [mk(B, self.actor.width(i), dt=BF16) for i in range(self.actor.nh)]
         self.hid_c = [mk(B, self.critic.width(i), dt=BF16) for i in range(self.critic.nh)]
-        self.act_buf = mk(B, A, dt=BF16)                     # target action / materialised actor output
+        # target action / materialised actor output (neither exists with the fused target + composed loss)
+        self.act_buf = mk(B, A, dt=BF16) if not (self.fuse_target and self.compose) else None
         cmax = max(self.critic.width(i) for i in range(self.critic.nh))
         amax = max([self.actor.width(i) for i in range(self.actor.nh)] + [1])
         wmax = max(cmax, amax)
@@ -217,10 +223,11 @@ class NativeDDPGUpdate:
                         colmask.data_ptr() if colmask is not None else 0, self._stream())
         return dst
 
-    def _first(self, net: _Net, emb, rowtab, out16, extra=None, wa=None, extra_rowtab=None):
-        """h0 = relu(emb W_d^T + b + rowtab[topo] (+ extra wa^T + extra_rowtab[topo])) -> out16."""
+    def _first(self, net: _Net, emb, rowtab, out16, extra=None, wa=None, extra_rowtab=None, acc_ready=False):
+        """h0 = relu(emb W_d^T + b + rowtab[topo] (+ extra wa^T + extra_rowtab[topo])) -> out16.
+        ``acc_ready``: ``hacc`` already holds the action projection (fused target path)."""
         h0 = net.width(0)
-        acc = False
+        acc = acc_ready
         if extra is not None:
             if extra_rowtab is not None:
                 gemm(extra, wa, "nt", out32=self.hacc[:, :h0], rowtab=extra_rowtab, topo=self.topo32)
@@ -300,11 +307,21 @@ class NativeDDPGUpdate:
         self._first(ta, self.emb["ta"], self._rowtab(ta, "ta"), self.hid_ta[0])
         self._hidden_fwd(ta, self.hid_ta)
         last = ta.nh
-        gemm(self.hid_ta[last - 1], ta.w16(last), "nt", out16=self.act_buf, bias=ta.b32(last), colmask=self.masks,
-             topo=self.topo32, clamp=(-1.0, 1.0))
-        # target critic on (s', a')
-        self._first(tc, self.emb["tc"], self._rowtab(tc, "tc"), self.hid_c[0], extra=self.act_buf,
-                    wa=self._wa(tc, "tc"))
+        if self.fuse_target:
+            # a' W_a'^T with a' = clamp(mask * (h W^T + b), -1, 1) tile by tile in LDS -> hacc
+            h, w, wa, c1 = self.hid_ta[last - 1], ta.w16(last), self._wa(tc, "tc"), tc.width(0)
+            self.nat.actor_proj(h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), ta.b32(last).data_ptr(),
+                                self.masks.data_ptr(), self.masks.stride(0), self.T, self.topo32.data_ptr(),
+                                wa.data_ptr(), wa.stride(0), self.B, h.shape[1], A, c1, -1.0, 1.0,
+                                self.slabs.data_ptr(), self.slabs.numel(), self.hacc.data_ptr(), self.hacc.stride(0),
+                                self._stream())
+            self._first(tc, self.emb["tc"], self._rowtab(tc, "tc"), self.hid_c[0], acc_ready=True)
+        else:
+            gemm(self.hid_ta[last - 1], ta.w16(last), "nt", out16=self.act_buf, bias=ta.b32(last), colmask=self.masks,
+                 topo=self.topo32, clamp=(-1.0, 1.0))
+            # target critic on (s', a')
+            self._first(tc, self.emb["tc"], self._rowtab(tc, "tc"), self.hid_c[0], extra=self.act_buf,
+                        wa=self._wa(tc, "tc"))
         self._hidden_fwd(tc, self.hid_c)
         self._critic_tail(tc, self.hid_c, 0, None, b)
         # critic on (s, a): loss + gradients

@@ -52,6 +52,26 @@ else:
     masks = (torch.rand(T, A, device=dev) > 0.5).float()
     topo = torch.randint(0, T, (B,), device=dev, dtype=torch.int32)
 slabs = torch.empty(16 << 20, device=dev)
+if PRESET != "abilene":   # the TD target's actor output + critic projection: materialised vs fused
+    from gsc_amd.native import load as load_native
+    nat = load_native()
+    h = torch.randn(B, 256, device=dev, dtype=bf)
+    w = torch.randn(A, 256, device=dev, dtype=bf) * 0.05
+    bias = torch.zeros(A, device=dev)
+    wa = torch.randn(64, A, device=dev, dtype=bf) * 0.05
+    act = torch.empty(B, A, device=dev, dtype=bf)
+    z = torch.empty(B, 64, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def materialised():
+        gemm(h, w, "nt", out16=act, bias=bias, colmask=masks, topo=topo, clamp=(-1.0, 1.0), tile=1)
+        gemm(act, wa, "nt", out32=z, splits=None, slabs=slabs, tile=1)
+
+    def fused():
+        nat.actor_proj(h.data_ptr(), 256, w.data_ptr(), 256, bias.data_ptr(), masks.data_ptr(), A, T, topo.data_ptr(),
+                       wa.data_ptr(), A, B, 256, A, 64, -1.0, 1.0, slabs.data_ptr(), slabs.numel(), z.data_ptr(), 64, st)
+    print(f"TD-target projection [B,256] -> [B,A] -> [B,64]: materialised {t(materialised):.1f} us  "
+          f"fused {t(fused):.1f} us", flush=True)
 for name, lay, sa, sb, kw in cases:
     a = torch.randn(*sa, device=dev, dtype=bf)
     b = torch.randn(*sb, device=dev, dtype=bf)
