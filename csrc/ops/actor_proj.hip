@@ -215,7 +215,9 @@ int actor_proj(uintptr_t h, long ldh, uintptr_t w, long ldw, uintptr_t bias, uin
             "actor_proj: 16-byte aligned bf16 rows, A >= 8");
   const int rbs = (M + BM - 1) / BM;
   const int tiles = (A + BN - 1) / BN;
-  int S = ((256 + rbs - 1) / rbs + 7) / 8 * 8;  // >= 256 workgroups, a multiple of 8 (XCD grouping)
+  // enough row blocks (large batches): one split, H read once and the whole W stream shared through
+  // L2; else >= 256 workgroups with S a multiple of 8 (XCD grouping)
+  int S = rbs >= 128 ? 1 : ((256 + rbs - 1) / rbs + 7) / 8 * 8;
   while (S > 8 && (long)S * M * J > slab_floats) S -= 8;
   GSC_CHECK((long)S * M * J <= slab_floats, "actor_proj: slabs too small");
   if (S > tiles) S = tiles;
