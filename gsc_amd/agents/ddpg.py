@@ -460,17 +460,19 @@ class BatchedTrainer:
 
     @staticmethod
     def auto_sim_cus(sim) -> int:
-        """CUs for one round of the simulator's env workgroups, at most 3 envs (waves) per CU so every
+        """CUs for one round of the simulator's env workgroups, at most 4 envs (waves) per CU so every
         simulator wave keeps a SIMD to itself, rounded up to whole XCDs (MI355X: 8 XCDs x 32 CUs, each
         with its own L2; contiguous CU-mask bits fill one XCD after the other), capped at half the device.
-        Measured on MI355X, 256 Abilene envs (env-steps/s): 96 CUs (3 whole XCDs) 104.1k; 88 CUs 78.2k
-        and 104 CUs 71.1k (an XCD shared between simulator and learner); 128 CUs 93.0k (the learner
-        becomes the longer chain); 64 CUs 56.6k (4 envs per CU do not fit LDS: two rounds)."""
+        Measured on MI355X, 256 Abilene envs, 39.9 KB of LDS per env (env-steps/s, round 3): 64 CUs (two
+        XCDs, 4 envs per CU) 113.3k; 96 CUs 111.0k; 128 CUs 96.4k (the learner becomes the longer
+        chain); 72 / 80 / 88 / 112 CUs 71-84k (an XCD shared between simulator and learner); 32 CUs
+        57.8k (two rounds).  Round 2, when an env took more LDS than 40 KB, 3 envs per CU (96 CUs) was
+        the optimum."""
         nat = sim.native
         n = nat.cu_count()
         xcd = max(n // 8, 8)
         lds = max(int(sim.ctx.lds_per_env), 1)
-        per_cu = max(1, min(3, (160 * 1024) // lds))
+        per_cu = max(1, min(4, (160 * 1024) // lds))
         need = -(-sim.E // per_cu)
         k = xcd * -(-need // xcd)
         return int(min(max(k, xcd), n // 2))
