@@ -4,7 +4,7 @@
 //   Z[m][j] = sum_n P[m][n] Wa[j][n],   P[m][n] = clamp((H[m] . W[n] + b[n]) * mask[topo[m]][n], lo, hi)
 //
 // H [M][K] is the actor's last hidden layer (bf16), W [A][K] its output weight, Wa [J][A] the
-// critic's action block (J <= 64 units).  The [M, A] action matrix P is never written: per 64-column
+// critic's action block (J <= 64 units; rows zero-padded to a multiple of 8 columns, any A).  The [M, A] action matrix P is never written: per 64-column
 // tile it lives in LDS between the two MFMA products (v_mfma_f32_32x32x16_bf16), so the HBM traffic
 // is W and Wa once per XCD instead of writing and re-reading M x A bf16 (1.5 GB at M = 2048,
 // A = 360,000: the materialised path took ~4 ms of the syn200 update).
@@ -50,6 +50,7 @@ struct Args {
   long ldwa;
   float* slabs;       // [S][M][J]
   int M, A, J, T, S, tiles, per_split;
+  int A8;             // A rounded up to 8: Wa rows hold zero padding up to here (whole 16-byte chunks)
   float lo, hi;
 };
 
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(NT) void actor_proj_kernel(Args a) {
       wreg[d][i] = load_chunk(a.w, a.ldw, n0 + r, a.A, 8 * c, K);
     }
     const int r = tid >> 3, c = tid & 7;  // NJ x 8 chunks = 512
-    areg[d] = load_chunk(a.wa, a.ldwa, r, a.J, n0 + 8 * c, a.A);
+    areg[d] = load_chunk(a.wa, a.ldwa, r, a.J, n0 + 8 * c, a.A8);
   };
   auto store_stage = [&](int d, int buf) {
 #pragma unroll
@@ -213,6 +214,10 @@ int actor_proj(uintptr_t h, long ldh, uintptr_t w, long ldw, uintptr_t bias, uin
   GSC_CHECK(K == 64 || K == 128 || K == 256, "actor_proj: actor width 64, 128 or 256");
   GSC_CHECK(A >= 8 && h % 16 == 0 && w % 16 == 0 && wa % 16 == 0 && ldh % 8 == 0 && ldw % 8 == 0 && ldwa % 8 == 0,
             "actor_proj: 16-byte aligned bf16 rows, A >= 8");
+  // Wa's columns A .. round8(A) are read as part of the last 16-byte chunk: the caller keeps them zero
+  // (rows padded to the stride), so ldwa >= round8(A)
+  const int A8 = (A + 7) / 8 * 8;
+  GSC_CHECK(ldwa >= A8, "actor_proj: Wa rows padded (zeros) to a multiple of 8 columns");
   const int rbs = (M + BM - 1) / BM;
   const int tiles = (A + BN - 1) / BN;
   // enough row blocks (large batches): one split, H read once and the whole W stream shared through
@@ -235,6 +240,7 @@ int actor_proj(uintptr_t h, long ldh, uintptr_t w, long ldw, uintptr_t bias, uin
   a.slabs = ptr<float>(slabs);
   a.M = M;
   a.A = A;
+  a.A8 = A8;
   a.J = J;
   a.T = T;
   a.S = S;

@@ -13,6 +13,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <tuple>
 #include <vector>
@@ -81,6 +82,7 @@ struct RCol {
   const char* src;
   char* dst;
   long row_g;
+  long drow_g;  // insert: destination row length in the same units (>= row_g; padded ring rows)
   int gsz, kind;
 };
 struct RCols {
@@ -99,36 +101,88 @@ __device__ __forceinline__ void copy_granule(const char* s, char* d, int gsz) {
   }
 }
 
-// dst_c[b] = src_c[idx[b]] for every column; block 0 also advances the draw counter (the index
-// kernel that consumed it has completed)
-__global__ __launch_bounds__(256) void gather_cols_kernel(RCols cs, const int32_t* __restrict__ idx, int B,
-                                                          ReplayState* st) {
-  if (st != nullptr && blockIdx.x == 0 && threadIdx.x == 0) st->draws += 1;
-  const long total = cs.start[cs.n];
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int c = 0;
-    while (i >= cs.start[c + 1]) ++c;
-    const RCol& col = cs.c[c];
-    const long j = i - cs.start[c], b = j / col.row_g, k = j - b * col.row_g;
-    const long sr = (long)idx[b] * col.row_g + k;
-    if (col.kind == 3) reinterpret_cast<int32_t*>(col.dst)[j] = (int32_t)reinterpret_cast<const long long*>(col.src)[sr];
-    else copy_granule(col.src + sr * col.gsz, col.dst + j * col.gsz, col.gsz);
+// One grid row (blockIdx.y) per column, a grid-stride loop over its rows x granules with the (row,
+// granule) pair stepped incrementally: no per-element 64-bit division / modulo, and the granule width
+// a compile-time type (a 1.5 GB syn200 action gather went through one division per 16 bytes).
+template <class G, class F>
+__device__ __forceinline__ void col_loop(long rows, long rg, F&& f) {
+  const long total = rows * rg;
+  const long S = (long)gridDim.x * blockDim.x;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  long r = i / rg, k = i - r * rg;
+  const long sr = S / rg, sk = S - sr * rg;
+  for (; i < total; i += S) {
+    f(r, k);
+    k += sk;
+    r += sr;
+    if (k >= rg) { k -= rg; ++r; }
   }
-  (void)B;
 }
 
-__global__ __launch_bounds__(256) void insert_cols_kernel(RCols cs, const ReplayState* __restrict__ st, long long cap) {
+template <class G>
+__device__ __forceinline__ void gather_col(const RCol& col, const int32_t* __restrict__ idx, int B) {
+  const G* __restrict__ src = reinterpret_cast<const G*>(col.src);
+  G* __restrict__ dst = reinterpret_cast<G*>(col.dst);
+  const long rg = col.row_g;
+  col_loop<G>(B, rg, [&](long b, long k) { dst[b * rg + k] = src[(long)idx[b] * rg + k]; });
+}
+
+// dst_c[b] = src_c[idx[b]] for every column (blockIdx.y = column); block (0, 0) also advances the draw
+// counter (the index kernel that consumed it has completed)
+__global__ __launch_bounds__(256) void gather_cols_kernel(RCols cs, const int32_t* __restrict__ idx, int B,
+                                                          ReplayState* st) {
+  if (st != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) st->draws += 1;
+  const RCol& col = cs.c[blockIdx.y];
+  if (col.kind == 3) {
+    const long long* src = reinterpret_cast<const long long*>(col.src);
+    int32_t* dst = reinterpret_cast<int32_t*>(col.dst);
+    col_loop<int>(B, 1, [&](long b, long) { dst[b] = (int32_t)src[idx[b]]; });
+    return;
+  }
+  switch (col.gsz) {
+    case 16: gather_col<int4>(col, idx, B); break;
+    case 8: gather_col<int2>(col, idx, B); break;
+    case 4: gather_col<int>(col, idx, B); break;
+    case 2: gather_col<short>(col, idx, B); break;
+    default: gather_col<char>(col, idx, B); break;
+  }
+}
+
+// insert: source row e -> ring row (pos + e) mod cap (pos + e < 2 cap: one conditional subtract)
+template <class G>
+__device__ __forceinline__ void insert_col(const RCol& col, long long pos, long long cap, int E) {
+  const G* __restrict__ src = reinterpret_cast<const G*>(col.src);
+  G* __restrict__ dst = reinterpret_cast<G*>(col.dst);
+  const long rg = col.row_g, dg = col.drow_g;
+  col_loop<G>(E, rg, [&](long e, long k) {
+    long r = pos + e;
+    if (r >= cap) r -= cap;
+    dst[r * dg + k] = src[e * rg + k];
+  });
+}
+
+__global__ __launch_bounds__(256) void insert_cols_kernel(RCols cs, const ReplayState* __restrict__ st, long long cap,
+                                                          int E) {
   const long long pos = st->pos;
-  const long total = cs.start[cs.n];
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    int c = 0;
-    while (i >= cs.start[c + 1]) ++c;
-    const RCol& col = cs.c[c];
-    const long j = i - cs.start[c], e = j / col.row_g, k = j - e * col.row_g;
-    const long d = ((pos + e) % cap) * col.row_g + k;
-    if (col.kind == 1) reinterpret_cast<__bf16*>(col.dst)[d] = (__bf16)reinterpret_cast<const float*>(col.src)[j];
-    else if (col.kind == 2) reinterpret_cast<float*>(col.dst)[d] = (float)reinterpret_cast<const uint8_t*>(col.src)[j];
-    else copy_granule(col.src + j * col.gsz, col.dst + d * col.gsz, col.gsz);
+  const RCol& col = cs.c[blockIdx.y];
+  if (col.kind == 1 || col.kind == 2) {
+    const long rg = col.row_g, dg = col.drow_g;
+    col_loop<char>(E, rg, [&](long e, long k) {
+      long r = pos + e;
+      if (r >= cap) r -= cap;
+      const long d = r * dg + k, j = e * rg + k;
+      if (col.kind == 1) reinterpret_cast<__bf16*>(col.dst)[d] = (__bf16)reinterpret_cast<const float*>(col.src)[j];
+      else reinterpret_cast<float*>(col.dst)[d] = (float)reinterpret_cast<const uint8_t*>(col.src)[j];
+    });
+    return;
+  }
+  switch (col.gsz) {
+    case 16: insert_col<int4>(col, pos, cap, E); break;
+    case 8: insert_col<int2>(col, pos, cap, E); break;
+    case 4: insert_col<int>(col, pos, cap, E); break;
+    case 2: insert_col<short>(col, pos, cap, E); break;
+    default: insert_col<char>(col, pos, cap, E); break;
   }
 }
 
@@ -141,6 +195,12 @@ __global__ void replay_advance_kernel(ReplayState* st, int E, long long cap) {
 static int grid_for(long n) {
   long g = (n + 255) / 256;
   return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+}
+// blocks per column of the column kernels: ~4 granules per thread for the largest column, at most
+// 16K blocks (the loop strides over the rest)
+static int cols_grid(long most) {
+  long g = (most + 1023) / 1024;
+  return (int)(g < 16384 ? (g > 0 ? g : 1) : 16384);
 }
 
 template <class F>
@@ -192,13 +252,14 @@ void replay_gather(bool device, uintptr_t src, uintptr_t dst, uintptr_t idx, int
 
 // kind as in insert_rows_kernel; row_n = elements per row (kind 0: bytes per row)
 void replay_insert(bool device, uintptr_t state, uintptr_t src, uintptr_t dst, int E, long row_n, long long cap,
-                   int kind, uintptr_t stream) {
+                   int kind, uintptr_t stream, long dst_row_n = 0) {
+  const long drow = dst_row_n > 0 ? dst_row_n : row_n;
   if (!device) {
     const long long pos = ptr<ReplayState>(state)->pos;
     for (int e = 0; e < E; ++e) {
       const long r = (long)((pos + e) % cap);
       for (long k = 0; k < row_n; ++k) {
-        const long i = (long)e * row_n + k, d = r * row_n + k;
+        const long i = (long)e * row_n + k, d = r * drow + k;
         if (kind == 0) ptr<char>(dst)[d] = ptr<const char>(src)[i];
         else if (kind == 1) {
           // round-to-nearest-even float -> bf16 (same as the device conversion)
@@ -213,6 +274,7 @@ void replay_insert(bool device, uintptr_t state, uintptr_t src, uintptr_t dst, i
     }
     return;
   }
+  GSC_CHECK(drow == row_n, "replay_insert: padded rows only through replay_insert_cols");
   const hipStream_t s = stream_of(stream);
   if (kind == 0) {
     by_granule(row_n, src, dst, [&](auto g, long row_g) {
@@ -271,7 +333,9 @@ void replay_sample_cols(bool device, uintptr_t state, uint32_t seed, int B, long
   const hipStream_t s = stream_of(stream);
   hipLaunchKernelGGL(replay_index_kernel, dim3((B + 255) / 256), dim3(256), 0, s, ptr<const ReplayState>(state), seed,
                      B, cap, ptr<int32_t>(idx));
-  hipLaunchKernelGGL(gather_cols_kernel, dim3(grid_for(cs.start[cs.n])), dim3(256), 0, s, cs, ptr<const int32_t>(idx), B,
+  long most = 0;
+  for (int i = 0; i < cs.n; ++i) most = std::max(most, cs.start[i + 1] - cs.start[i]);
+  hipLaunchKernelGGL(gather_cols_kernel, dim3(cols_grid(most), cs.n), dim3(256), 0, s, cs, ptr<const int32_t>(idx), B,
                      ptr<ReplayState>(state));
   check_launch();
 }
@@ -279,7 +343,7 @@ void replay_sample_cols(bool device, uintptr_t state, uint32_t seed, int B, long
 // One insert of E rows at the cursor for every column, then the cursor advance.
 // cols: (src, dst, row_n, kind) as replay_insert.
 void replay_insert_cols(bool device, uintptr_t state, int E, long long cap,
-                        const std::vector<std::tuple<uintptr_t, uintptr_t, long, int>>& cols, uintptr_t stream);
+                        const std::vector<std::tuple<uintptr_t, uintptr_t, long, int, long>>& cols, uintptr_t stream);
 
 void replay_advance(bool device, uintptr_t state, int E, long long cap, uintptr_t stream) {
   if (!device) {
@@ -331,12 +395,15 @@ void step_metrics(bool device, uintptr_t stats, int nstats, uintptr_t ep_return,
   check_launch();
 }
 
+// cols: (src, dst, row_n, kind, dst_row_n) -- dst_row_n: the ring's row length (0: = row_n; larger for
+// ring rows padded to a 16-byte multiple, e.g. bf16 actions of A % 8 != 0 columns)
 void replay_insert_cols(bool device, uintptr_t state, int E, long long cap,
-                        const std::vector<std::tuple<uintptr_t, uintptr_t, long, int>>& cols, uintptr_t stream) {
+                        const std::vector<std::tuple<uintptr_t, uintptr_t, long, int, long>>& cols, uintptr_t stream) {
   GSC_CHECK(!cols.empty() && (int)cols.size() <= kMaxCols, "replay_insert_cols: 1..8 columns");
   if (!device) {
     for (const auto& c : cols)
-      replay_insert(false, state, std::get<0>(c), std::get<1>(c), E, std::get<2>(c), cap, std::get<3>(c), 0);
+      replay_insert(false, state, std::get<0>(c), std::get<1>(c), E, std::get<2>(c), cap, std::get<3>(c), 0,
+                    std::get<4>(c));
     replay_advance(false, state, E, cap, 0);
     return;
   }
@@ -349,15 +416,20 @@ void replay_insert_cols(bool device, uintptr_t state, int E, long long cap,
     r.src = ptr<const char>(std::get<0>(c));
     r.dst = ptr<char>(std::get<1>(c));
     r.kind = std::get<3>(c);
-    const long rn = std::get<2>(c);
-    GSC_CHECK(r.kind >= 0 && r.kind <= 2, "replay_insert_cols: kind 0..2");
+    const long rn = std::get<2>(c), drn = std::get<4>(c) > 0 ? std::get<4>(c) : rn;
+    GSC_CHECK(r.kind >= 0 && r.kind <= 2 && drn >= rn, "replay_insert_cols: kind 0..2, dst rows >= src rows");
     r.gsz = r.kind == 0 ? granule_of(rn, std::get<0>(c), std::get<1>(c)) : 1;
+    if (r.kind == 0) r.gsz = std::min(r.gsz, granule_of(drn, 0, 0));
     r.row_g = r.kind == 0 ? rn / r.gsz : rn;
+    r.drow_g = r.kind == 0 ? drn / r.gsz : drn;
     cs.start[i + 1] = cs.start[i] + (long)E * r.row_g;
   }
   const hipStream_t s = stream_of(stream);
-  hipLaunchKernelGGL(insert_cols_kernel, dim3(grid_for(cs.start[cs.n])), dim3(256), 0, s, cs,
-                     ptr<const ReplayState>(state), cap);
+  GSC_CHECK(E <= cap, "replay_insert_cols: more rows than the ring holds");
+  long most = 0;
+  for (int i = 0; i < cs.n; ++i) most = std::max(most, cs.start[i + 1] - cs.start[i]);
+  hipLaunchKernelGGL(insert_cols_kernel, dim3(cols_grid(most), cs.n), dim3(256), 0, s, cs,
+                     ptr<const ReplayState>(state), cap, E);
   hipLaunchKernelGGL(replay_advance_kernel, dim3(1), dim3(1), 0, s, ptr<ReplayState>(state), E, cap);
   check_launch();
 }
@@ -369,7 +441,8 @@ int replay_index_host(uint32_t seed, long long draw, int b, long long pos, long 
 void register_replay(py::module_& m) {
   m.def("replay_sample_indices", &replay_sample_indices);
   m.def("replay_gather", &replay_gather);
-  m.def("replay_insert", &replay_insert);
+  m.def("replay_insert", &replay_insert, py::arg("device"), py::arg("state"), py::arg("src"), py::arg("dst"),
+        py::arg("E"), py::arg("row_n"), py::arg("cap"), py::arg("kind"), py::arg("stream"), py::arg("dst_row_n") = 0);
   m.def("replay_advance", &replay_advance);
   m.def("replay_sample_cols", &replay_sample_cols, "Philox indices + every column gathered in one kernel");
   m.def("replay_insert_cols", &replay_insert_cols, "every column inserted in one kernel + cursor advance");

@@ -154,8 +154,13 @@ struct Dims {
 struct Layout {
   int hdr, node_cap, node_rem, inter_arr, max_usage, run_drop_node, mmpp_state, sf_load, sf_start, proc_traffic,
       requested, drop_locs, link_rem, link_passed, link_next, rel, flows, procs, events, flow_free, proc_free,
-      sf_present, placement, hot, sched, wrr, total;
+      sf_present, placement, hot, sched, wrr, pmask, total;
 };
+
+// Topologies beyond one wave of destinations keep, per schedule row (src, c, sf), the bitset of its
+// positive destinations (4 x 64 bits, n <= 256): the device placement walk ORs rows instead of
+// re-reading them (see controller_prologue).  Absent (0 rows) for n <= 64.
+__host__ __device__ constexpr int pmask_rows(const Dims& d) { return d.N > 64 ? d.N * d.C * d.S : 0; }
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
 
@@ -189,6 +194,7 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   L.hot = o;
   GSC_TAKE(sched, 8 * d.N * d.C * d.S * d.N);
   GSC_TAKE(wrr, 4 * d.N * d.C * d.S * d.N);
+  GSC_TAKE(pmask, 32 * pmask_rows(d));
 #undef GSC_TAKE
   L.total = o;
   return L;
@@ -201,6 +207,7 @@ struct Env {
   double *node_cap, *node_rem, *inter_arr, *max_usage, *sf_load, *sf_start, *proc_traffic, *requested, *sched,
       *link_rem, *link_passed, *link_next;
   int32_t *run_drop_node, *mmpp_state, *drop_locs, *wrr;
+  uint64_t* pmask;
   Release* rel;
   Flow* flows;
   Proc* procs;
@@ -225,6 +232,7 @@ struct Env {
     drop_locs = (int32_t*)(base + L.drop_locs);
     sched = (double*)(cb + L.sched);
     wrr = (int32_t*)(cb + L.wrr);
+    pmask = (uint64_t*)(cb + L.pmask);
     link_rem = (double*)(base + L.link_rem);
     link_passed = (double*)(base + L.link_passed);
     link_next = (double*)(base + L.link_next);
@@ -1093,11 +1101,42 @@ GSC_HD_CALL void controller_prologue(Env& S, const SimConst& K, const TopoDev& T
     const int lane = wave_lane();
     for (int i = lane; i < N * Sd; i += 64) S.placement[i] = 0;
     lanes_sync(64);
+    const bool masks = n > 64 && pmask_rows(S.d) > 0;  // row bitsets written by load_action
     for (int c = 0; c < K.C; ++c) {
       uint64_t f[4] = {0, 0, 0, 0};  // node bitset (n <= 256)
       for (int i = 0; i < T.n_ing; ++i) {
         const int v = GSC_UNI(T.ingress[i]);
         if (GSC_UNI(S.inter_arr[v] == S.inter_arr[v])) f[v >> 6] |= 1ull << (v & 63);
+      }
+      if (masks) {
+        // next frontier = OR of the frontier rows' bitsets: one source per lane (all loads of a pass
+        // in flight), OR-reduced across the wave; placement from the result
+        for (int k = 0; k < K.chain_len[c]; ++k) {
+          const int sf = K.chain[c * kMaxF + k];
+          uint64_t nf[4] = {0, 0, 0, 0};
+          uint64_t w[4] = {0, 0, 0, 0};  // this lane's OR over its sources (all loads in flight)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int src = 64 * q + lane;
+            if (src < n && ((f[q] >> lane) & 1)) {
+              const uint64_t* m = S.pmask + 4L * ((src * C + c) * Sd + sf);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) w[j] |= m[j];
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t lo = dpp_red_u32((uint32_t)w[j], 0u, [](uint32_t a, uint32_t b) { return a | b; });
+            const uint32_t hi = dpp_red_u32((uint32_t)(w[j] >> 32), 0u, [](uint32_t a, uint32_t b) { return a | b; });
+            nf[j] = ((uint64_t)hi << 32) | lo;
+          }
+          for (int d0 = 0; d0 < n; d0 += 64) {
+            const int dst = d0 + lane;
+            if (dst < n && ((nf[d0 >> 6] >> lane) & 1)) S.placement[dst * Sd + sf] = 1;
+          }
+          for (int j = 0; j < 4; ++j) f[j] = nf[j];
+        }
+        continue;
       }
       for (int k = 0; k < K.chain_len[c]; ++k) {
         const int sf = K.chain[c * kMaxF + k];
@@ -1305,6 +1344,49 @@ GSC_HD void write_stats(const Env& S, float* st) {
 // Copy this step's (post-processed) action block into the schedule table.
 GSC_HD void load_action(Env& S, const SimConst& K, const TopoDev& T, const float* act, int lane, int nlanes) {
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n, P = K.n_pad;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (n > 16 && nlanes == 64) {
+    const bool masks = pmask_rows(S.d) > 0;
+    // schedule rows with the destinations over the lanes (no index divisions), kG rows per pass with
+    // all their loads in flight before the first use (one HBM round trip per pass, not per row); each
+    // row's positive destinations' bitset from the same pass's ballots
+    constexpr int kG = 8;
+    const int rows = n * C * Sd;
+    int src = 0, c = 0, sf = 0;
+    for (int r0 = 0; r0 < rows; r0 += kG) {
+      float v[kG][4];
+      int ra[kG], rs[kG];
+#pragma unroll
+      for (int g = 0; g < kG; ++g) {
+        ra[g] = (src * K.C + c) * K.F + sf;  // action row / schedule row of row r0 + g
+        rs[g] = (src * C + c) * Sd + sf;
+        if (++sf == Sd) { sf = 0; if (++c == C) { c = 0; ++src; } }
+      }
+#pragma unroll
+      for (int g = 0; g < kG; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int dst = 64 * q + lane;
+          v[g][q] = (r0 + g < rows && dst < n) ? act[(long)ra[g] * P + dst] : 0.f;
+        }
+#pragma unroll
+      for (int g = 0; g < kG; ++g) {
+        if (r0 + g >= rows) break;
+        double* srow = S.sched + (long)rs[g] * N;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int dst = 64 * q + lane;
+          if (dst < n) srow[dst] = (double)v[g][q];
+          if (masks) {
+            const uint64_t b = (uint64_t)__ballot(v[g][q] > 0.f);
+            if (lane == q) S.pmask[4L * rs[g] + q] = b;
+          }
+        }
+      }
+    }
+    return;
+  }
+#endif
   const int total = n * C * Sd * n;
   for (int i = lane; i < total; i += nlanes) {
     const int dst = i % n;

@@ -140,7 +140,7 @@ class DDPGLearner:
         g, masks = self.graphs, self.masks
         y = self._target(b)
         with self._autocast():
-            q = self.critic(b.obs, b.topo, g, masks, b.actions).float().view(-1)
+            q = self.critic(b.obs, b.topo, g, masks, b.actions[:, :self.actor.action_dim]).float().view(-1)
             lq = F.mse_loss(q, y)
         grads = torch.autograd.grad(lq, self.critic_flat.params)
         self.critic_flat.set_grads(grads)
@@ -392,8 +392,10 @@ class BatchedTrainer:
                                            if self.device.type == "cuda" else 4e9)
         cap = int(min(cap, budget // per))
         # on the GPU actions are stored in bf16: the critic consumes them as bf16 GEMM operands
+        # (bf16 rows padded to 8 columns: 16-byte aligned operand rows for the native learner's GEMMs)
         self.replay = DeviceReplay(max(cap, self.E), sim.n_pad, sim.n_obs, sim.action_dim, self.device,
-                                   action_dtype=adt, seed=tcfg.seed + 7919 * self.dist.rank)
+                                   action_dtype=adt, seed=tcfg.seed + 7919 * self.dist.rank,
+                                   action_row_align=8 if adt == torch.bfloat16 else 1)
         self.batch_size = tcfg.batch_size or 100 * self.E
         self.learning_starts = (tcfg.learning_starts if tcfg.learning_starts is not None
                                 else int(cfg.get("nb_steps_warmup_critic", 200)))

@@ -108,7 +108,10 @@ class NativeDDPGUpdate:
         # (csrc/ops/actor_proj.hip, no [B, A] action matrix)
         hl0 = self.actor.width(self.actor.nh - 1) if self.actor.nh else 0
         self.fuse_target = (os.environ.get("GSC_FUSE_TARGET", "1") != "0" and self.actor.nh >= 1 and T <= 4
-                            and c1 <= 64 and hl0 in (64, 128, 256) and A % 8 == 0)
+                            and c1 <= 64 and hl0 in (64, 128, 256))
+        # [*, A] bf16 operands get rows padded to 8 columns (zeros): 16-byte aligned rows, so the GEMM
+        # engine stages them with vector loads also when A % 8 != 0 (50-node topologies: A = 22,500)
+        self.A8 = A8 = -(-A // 8) * 8
         self.graphs = L.graphs
         self.tables = _tables(L.graphs)
         self.layer_of = _layer_of(L.actor.embedder)
@@ -129,9 +132,9 @@ class NativeDDPGUpdate:
         self.dh = [mk(B, wmax, dt=BF16), mk(B, wmax, dt=BF16)]
         self.dact = mk(B, A, dt=BF16) if not self.compose else None
         self.demb = mk(B, H)
-        self.wa = {k: mk(c1, A, dt=BF16) for k in ("c", "tc")}   # aligned critic action blocks
+        self.wa = {k: mk(c1, A8, dt=BF16) for k in ("c", "tc")}  # aligned critic action blocks
         # per-topology masked blocks W_a diag(m_t), stacked [T * c1, A] (composed actor loss)
-        self.wam = mk(T * c1, A, dt=BF16) if self.compose else None
+        self.wam = mk(T * c1, A8, dt=BF16)[:, :A] if self.compose else None
         self.rowtab = {k: mk(T, wmax) for k in ("a", "ta", "c", "tc")}
         self.aug = mk(wmax, max(H + 1 + T, 1))
         hl = self.actor.width(self.actor.nh - 1) if self.actor.nh else 1
@@ -215,13 +218,14 @@ class NativeDDPGUpdate:
         return out
 
     def _wa(self, net: _Net, key: str, colmask: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Aligned copy of the critic's action block W[:, H+A:] (optionally column-masked)."""
+        """Aligned copy of the critic's action block W[:, H+A:] (optionally column-masked): the [c1, A]
+        view of rows padded to A8 columns (the padding stays zero)."""
         w = net.w16(0)
         dst = self.wa[key]
         H, A = self.H, self.A
         self.nat.copy2d(w.data_ptr() + 2 * (H + A), w.stride(0), dst.data_ptr(), dst.stride(0), dst.shape[0], A,
                         colmask.data_ptr() if colmask is not None else 0, self._stream())
-        return dst
+        return dst[:, :A]
 
     def _first(self, net: _Net, emb, rowtab, out16, extra=None, wa=None, extra_rowtab=None, acc_ready=False):
         """h0 = relu(emb W_d^T + b + rowtab[topo] (+ extra wa^T + extra_rowtab[topo])) -> out16.
@@ -326,14 +330,15 @@ class NativeDDPGUpdate:
         self._critic_tail(tc, self.hid_c, 0, None, b)
         # critic on (s, a): loss + gradients
         self._gnn_fwd(c, b.obs, self.emb["c"], self.blob["c"], key="c")
-        self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], extra=b.actions, wa=self._wa(c, "c"))
+        acts = b.actions[:, :A]   # replay rows are padded to 8 columns (16-byte aligned)
+        self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], extra=acts, wa=self._wa(c, "c"))
         self._hidden_fwd(c, self.hid_c)
         C = c.width(c.nh - 1)
         dh = self.dh[0][:, :C]
         self._critic_tail(c, self.hid_c, 1, dh, b)
         self._head_reduce(c, C, 1)
         dh0 = self._hidden_bwd(c, self.hid_c, dh, grads=True)
-        self._first_bwd(c, self.emb["c"], dh0, extra=b.actions)
+        self._first_bwd(c, self.emb["c"], dh0, extra=acts)
         self._gnn_bwd(c, b.obs, self.demb, self.blob["c"], key="c")
 
     def stage_actor_fwd(self, b) -> None:

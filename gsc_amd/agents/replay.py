@@ -21,7 +21,8 @@ import torch
 class Batch(NamedTuple):
     obs: torch.Tensor        # [B, n_pad, F]
     topo: torch.Tensor       # [B] int64
-    actions: torch.Tensor    # [B, A] (bf16 on the GPU, float32 on CPU)
+    actions: torch.Tensor    # [B, A] (bf16 on the GPU, float32 on CPU); rows may carry zero padding
+                             # columns beyond A (DeviceReplay action_row_align): use actions[:, :A]
     rewards: torch.Tensor    # [B]
     next_obs: torch.Tensor   # [B, n_pad, F]
     dones: torch.Tensor      # [B]
@@ -35,7 +36,7 @@ class DeviceReplay:
     ``seed`` (rank-specific) and the draw counter -- the same stream on the host path."""
 
     def __init__(self, capacity: int, n_pad: int, n_obs: int, action_dim: int, device,
-                 action_dtype=torch.float32, seed: int = 0):
+                 action_dtype=torch.float32, seed: int = 0, action_row_align: int = 1):
         from gsc_amd.native import load as load_native
         self.nat = load_native()
         self.capacity = int(capacity)
@@ -45,7 +46,13 @@ class DeviceReplay:
         self.obs = torch.zeros((self.capacity, n_pad, n_obs), dtype=torch.float32, device=dev)
         self.next_obs = torch.zeros_like(self.obs)
         self.topo = torch.zeros(self.capacity, dtype=torch.int64, device=dev)
-        self.actions = torch.zeros((self.capacity, action_dim), dtype=action_dtype, device=dev)
+        # ``action_row_align``: ring (and sampled batch) rows padded to a multiple of that many columns
+        # (zeros), so every action row starts 16-byte aligned for the native learner's vector loads
+        # (A % 8 != 0 at 50-node topologies); consumers use ``actions[:, :action_dim]``
+        self.action_dim = int(action_dim)
+        al = max(1, int(action_row_align))
+        self.action_cols = -(-self.action_dim // al) * al
+        self.actions = torch.zeros((self.capacity, self.action_cols), dtype=action_dtype, device=dev)
         self.rewards = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
         self.dones = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
         self.state = torch.zeros(4, dtype=torch.int64, device=dev)   # pos, full, draws, -
@@ -75,21 +82,23 @@ class DeviceReplay:
         topo = topo.to(torch.int64).contiguous()
         rewards = rewards.contiguous().float()
         ob = obs[0].numel() * 4
-        cols = [(obs.data_ptr(), self.obs.data_ptr(), ob, 0), (next_obs.data_ptr(), self.next_obs.data_ptr(), ob, 0),
-                (topo.data_ptr(), self.topo.data_ptr(), 8, 0), (rewards.data_ptr(), self.rewards.data_ptr(), 4, 0)]
-        A = self.actions.shape[1]
+        cols = [(obs.data_ptr(), self.obs.data_ptr(), ob, 0, 0),
+                (next_obs.data_ptr(), self.next_obs.data_ptr(), ob, 0, 0),
+                (topo.data_ptr(), self.topo.data_ptr(), 8, 0, 0), (rewards.data_ptr(), self.rewards.data_ptr(), 4, 0, 0)]
+        A, Ap = self.action_dim, self.action_cols
         if self.actions.dtype == torch.bfloat16 and actions.dtype == torch.float32:
             a = actions.contiguous()
-            cols.append((a.data_ptr(), self.actions.data_ptr(), A, 1))
+            cols.append((a.data_ptr(), self.actions.data_ptr(), A, 1, Ap))
         else:
             a = actions.to(self.actions.dtype).contiguous()
-            cols.append((a.data_ptr(), self.actions.data_ptr(), A * a.element_size(), 0))
+            es = a.element_size()
+            cols.append((a.data_ptr(), self.actions.data_ptr(), A * es, 0, Ap * es))
         if dones.dtype in (torch.uint8, torch.bool):
             d = dones.contiguous().view(torch.uint8)
-            cols.append((d.data_ptr(), self.dones.data_ptr(), 1, 2))
+            cols.append((d.data_ptr(), self.dones.data_ptr(), 1, 2, 0))
         else:
             d = dones.contiguous().float()
-            cols.append((d.data_ptr(), self.dones.data_ptr(), 4, 0))
+            cols.append((d.data_ptr(), self.dones.data_ptr(), 4, 0, 0))
         # every column in one kernel, then the cursor advance (csrc/ops/replay.hip insert_cols_kernel)
         nat.replay_insert_cols(dev, st, E, cap, cols, s)
         new = self.pos + E
@@ -144,13 +153,15 @@ class DeviceReplay:
     def state_dict(self) -> dict:
         n = len(self)
         return {"pos": self.pos, "full": self.full, "obs": self.obs[:n].cpu(), "next_obs": self.next_obs[:n].cpu(),
-                "topo": self.topo[:n].cpu(), "actions": self.actions[:n].cpu(), "rewards": self.rewards[:n].cpu(),
+                "topo": self.topo[:n].cpu(), "actions": self.actions[:n, :self.action_dim].cpu(),
+                "rewards": self.rewards[:n].cpu(),
                 "dones": self.dones[:n].cpu()}
 
     def load_state_dict(self, sd: dict) -> None:
         n = sd["obs"].shape[0]
-        for k in ("obs", "next_obs", "topo", "actions", "rewards", "dones"):
+        for k in ("obs", "next_obs", "topo", "rewards", "dones"):
             getattr(self, k)[:n].copy_(sd[k].to(self.device))
+        self.actions[:n, :self.action_dim].copy_(sd["actions"].to(self.device))
         self.pos, self.full = int(sd["pos"]), bool(sd["full"])
         self.state[0] = self.pos
         self.state[1] = int(self.full)

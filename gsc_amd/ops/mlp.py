@@ -51,12 +51,18 @@ def pick_tile(M: int, N: int) -> int:
 
 def auto_splits(M: int, N: int, K: int, tile: int, cap: int) -> int:
     """Split-K count for long reductions (weight gradients, K = batch): ~512 blocks, >= 256 K per split,
-    at most ``cap`` fp32 slab elements."""
+    at most ``cap`` fp32 slab elements.  Products that still leave each block a K loop longer than 4,096
+    (the critic's action projection and its weight gradient at large A: [B, A] x [A, 64] with a few
+    hundred output blocks) split further, to <= 4,096 K per split."""
     if K < 1024:
         return 1
     bm, bn = _TILES[tile]
     blocks = -(-M // bm) * -(-N // bn)
-    return max(1, min(512 // blocks, K // 256, 256, cap // max(M * N, 1)))
+    lim = cap // max(M * N, 1)
+    s = max(1, min(512 // blocks, K // 256, 256, lim))
+    if K // s > 4096 and blocks < 1024:
+        s = max(s, min(-(-K // 4096), 256, lim))
+    return max(1, s)
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, layout: str = "nt", *, out16: Optional[torch.Tensor] = None,

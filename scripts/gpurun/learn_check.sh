@@ -1,13 +1,13 @@
 #!/bin/bash
-# Learning check: composed vs materialised actor loss, fp32 learner + fp32 reference embedder,
-# 3 seeds each, 10 lockstep episodes of 256 envs; plus the reference update ratio (E updates of 100).
+# learner / replay / simulator-prologue changes: GPU tests against the fp32 reference and the host
+# path, the simulator's per-preset profile, then the three benchmark presets
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/learn
+OUT=$R/gpurun_out
 mkdir -p $OUT
-EP=${EP:-10}
-for seed in 0 1 2; do
-  GSC_GNN_NATIVE=0 timeout -k 10 200 python -u $R/scripts/train_curve.py --fp32 --episodes $EP --seed $seed --tag "compose s$seed" >> $OUT/compose.txt 2>&1 || exit 1
-  GSC_COMPOSE=0 GSC_GNN_NATIVE=0 timeout -k 10 200 python -u $R/scripts/train_curve.py --fp32 --episodes $EP --seed $seed --tag "material s$seed" >> $OUT/material.txt 2>&1 || exit 1
-done
-timeout -k 10 400 python -u $R/scripts/train_curve.py --episodes $EP --envs 32 --ref-ratio --tag "refratio" >> $OUT/refratio.txt 2>&1
+timeout -k 10 600 python -u -m pytest $R/tests/test_gpu_sim.py $R/tests/test_gpu_replay.py $R/tests/test_gpu_learner.py $R/tests/test_gpu_mlp.py -x -v --timeout 120 --timeout-method thread > $OUT/learn_tests.log 2>&1 &&
+timeout -k 10 200 python $R/scripts/sim_throughput.py --preset syn200 --steps 6 --envs 128 --profile > $OUT/sim_prof_syn200.txt 2>&1 &&
+timeout -k 10 200 python $R/scripts/sim_throughput.py --preset syn50 --steps 10 --profile > $OUT/sim_prof_syn50.txt 2>&1 &&
+timeout -k 10 300 python $R/bench.py --preset syn50 --steps 10 --warmup 3 > $OUT/bench_syn50.json 2> $OUT/bench_syn50.err &&
+timeout -k 10 300 python $R/bench.py --steps 40 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err &&
+timeout -k 10 400 python $R/bench.py --preset syn200 --steps 25 --warmup 5 > $OUT/bench_syn200.json 2> $OUT/bench_syn200.err

@@ -25,14 +25,14 @@ def _cfg(actor=(256,), critic=(64,)):
     return cfg
 
 
-def _batch(B, T, device, seed=11):
+def _batch(B, T, device, seed=11, P=24):
     from gsc_amd.agents import Batch
     g = torch.Generator().manual_seed(seed)
-    obs = torch.rand(B, 24, 3, generator=g)
+    obs = torch.rand(B, P, 3, generator=g)
     obs[:, 11:] = 0
-    nxt = torch.rand(B, 24, 3, generator=g)
+    nxt = torch.rand(B, P, 3, generator=g)
     nxt[:, 11:] = 0
-    act = torch.rand(B, 1728, generator=g)
+    act = torch.rand(B, P * 3 * P, generator=g)
     topo = torch.randint(0, T, (B,), generator=g)
     b = Batch(obs, topo, act, torch.rand(B, generator=g) - 0.5, nxt, (torch.rand(B, generator=g) < 0.2).float())
     if device == "cpu":
@@ -40,13 +40,14 @@ def _batch(B, T, device, seed=11):
     return Batch(*(t.to(device) for t in b[:2]), b.actions.to(device).bfloat16(), *(t.to(device) for t in b[3:]))
 
 
-def _learners(cfg, T):
+def _learners(cfg, T, P=24):
     from gsc_amd.agents import DDPGLearner
     from gsc_amd.coordsim.reader import load_topology
     from gsc_amd.models import GraphSet
     topos = [load_topology(ABILENE)] * T if T < 3 else [load_topology(p) for p in THREE]
-    ref = DDPGLearner(cfg, 3, 1728, GraphSet(topos, 24, "cpu"), 1, 3, "cpu", amp_bf16=False, seed=3)
-    gpu = DDPGLearner(cfg, 3, 1728, GraphSet(topos, 24, "cuda"), 1, 3, "cuda", seed=3)
+    A = P * 3 * P
+    ref = DDPGLearner(cfg, 3, A, GraphSet(topos, P, "cpu"), 1, 3, "cpu", amp_bf16=False, seed=3)
+    gpu = DDPGLearner(cfg, 3, A, GraphSet(topos, P, "cuda"), 1, 3, "cuda", seed=3)
     assert gpu.native_ok
     assert torch.equal(ref.actor_flat.flat, gpu.actor_flat.flat.cpu())
     return ref, gpu
@@ -63,30 +64,32 @@ def _per_param_err(flat_ref, flat_gpu, what="grad"):
     return out
 
 
-@pytest.mark.parametrize("case", ["composed", "two_topologies", "three_topologies", "deep"])
+@pytest.mark.parametrize("case", ["composed", "two_topologies", "three_topologies", "deep", "odd_actions"])
 def test_native_update_matches_fp32_reference(case):
     """Tolerance: per tensor max(3 %, 2.5x the error of the PyTorch bf16-autocast path on the same
     batch) -- deeper nets amplify bf16 rounding through ReLU gates, for either implementation.  The
     deep case's floor is 4 %: the embedder gradients inherit the ~3.5 % bf16 error of the embedding
     gradient after three hidden layers (every embedder tensor, against 2 % for autocast), and the
     fp32-accumulated bias sums of one tensor land at 3.2 % where autocast happens to reach 0.8 %.
-    three_topologies (different action masks): the critic is frozen (learning rate 0).  With it
+    odd_actions: n_pad 25, A = 1,875 (A % 8 != 0): the fused TD-target projection reads zero-padded
+    critic action rows.  three_topologies (different action masks): the critic is frozen (learning rate 0).  With it
     training, the first critic step makes the trajectories chaotic -- Adam's first step is lr * sign(g)
     for every weight and the 1,728 action-block weights of each critic unit move coherently (qf1 jumps
     0.09 -> 4.2) -- so the actor gradients of any two bf16 implementations then differ by 10-20 %
     (autocast included); through a frozen critic ours and autocast agree per tensor (within 0.5 %
     absolute of each other against fp32, scripts/diag/learner_t3.py)."""
     T = {"two_topologies": 2, "three_topologies": 3}.get(case, 1)
+    P = 25 if case == "odd_actions" else 24         # A = 1,875: A % 8 != 0 (padded action rows)
     cfg = _cfg(actor=(128, 96), critic=(64, 32)) if case == "deep" else _cfg()
-    ref, gpu = _learners(cfg, T)
-    _, auto = _learners(cfg, T)
+    ref, gpu = _learners(cfg, T, P)
+    _, auto = _learners(cfg, T, P)
     auto.native_ok = False                               # autograd + hipBLASLt bf16 path
     if case == "three_topologies":
         for l in (ref, gpu, auto):
             l.critic_opt.lr = 0.0
     B = 512
     for k in range(3):
-        bc, bg = _batch(B, T, "cpu", seed=11 + k), _batch(B, T, "cuda", seed=11 + k)
+        bc, bg = _batch(B, T, "cpu", seed=11 + k, P=P), _batch(B, T, "cuda", seed=11 + k, P=P)
         ref.update(bc)
         gpu.update(bg)
         auto.update(bg)
@@ -106,7 +109,7 @@ def test_native_update_matches_fp32_reference(case):
             r, g, au = float(ref.last[key]), float(gpu.last[key]), float(auto.last[key])
             assert abs(r - g) <= max(0.03 * abs(r) + 1e-3, 2.5 * abs(r - au)), (k, key, r, g, au)
     # parameter trajectories: delta directions agree
-    a0, _ = _learners(cfg, T)
+    a0, _ = _learners(cfg, T, P)
     for nm in ("actor_flat", "critic_flat"):
         fr, fg, fa, f0 = (getattr(x, nm) for x in (ref, gpu, auto, a0))
         dr = fr.flat - f0.flat

@@ -7,10 +7,12 @@ from gsc_amd.agents.replay import DeviceReplay
 pytestmark = pytest.mark.gpu
 
 
-def test_device_replay_matches_host():
+@pytest.mark.parametrize("A,align", [(1728, 1), (22500, 8)])
+def test_device_replay_matches_host(A, align):
     torch.manual_seed(0)
-    E, cap, A = 96, 500, 1728
-    rs = [DeviceReplay(cap, 24, 3, A, d, action_dtype=torch.bfloat16, seed=42) for d in ("cpu", "cuda")]
+    E, cap = 96, 500
+    rs = [DeviceReplay(cap, 24, 3, A, d, action_dtype=torch.bfloat16, seed=42, action_row_align=align)
+          for d in ("cpu", "cuda")]
     for step in range(7):
         obs, nxt = torch.rand(E, 24, 3), torch.rand(E, 24, 3)
         act, rew = torch.rand(E, A), torch.randn(E)

@@ -98,3 +98,24 @@ def test_fused_sample_writes_int32_topology_ids():
     b = r.sample(64, topo32=t32)
     assert torch.equal(t32, b.topo.to(torch.int32))
     assert torch.equal(b.topo, topo[r.last_indices(64).long()])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_padded_action_rows(dtype):
+    """action_row_align: ring / batch rows padded with zero columns (16-byte aligned bf16 rows for the
+    native learner at A % 8 != 0); the first A columns hold the actions, checkpoints keep [.., :A]."""
+    A = 13
+    r = DeviceReplay(10, 4, 2, A, "cpu", action_dtype=dtype, seed=5, action_row_align=8)
+    assert r.actions.shape == (10, 16) and r.action_dim == A
+    act = torch.rand(6, A)
+    r.add(torch.rand(6, 4, 2), torch.zeros(6, dtype=torch.long), act, torch.rand(6), torch.rand(6, 4, 2),
+          torch.zeros(6, dtype=torch.uint8))
+    assert torch.equal(r.actions[:6, :A], act.to(dtype)) and not r.actions[:, A:].any()
+    b = r.sample(32)
+    assert b.actions.shape == (32, 16)
+    assert torch.equal(b.actions[:, :A], r.actions[r.last_indices(32).long(), :A]) and not b.actions[:, A:].any()
+    sd = r.state_dict()
+    assert sd["actions"].shape == (6, A)
+    q = DeviceReplay(10, 4, 2, A, "cpu", action_dtype=dtype, seed=5, action_row_align=8)
+    q.load_state_dict(sd)
+    assert torch.equal(q.actions, r.actions)
