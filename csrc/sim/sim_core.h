@@ -106,6 +106,8 @@ struct TopoDev {
   const int16_t* plen;      // [n*n]
   const int16_t* pnodes;    // [n*n*H]
   const int16_t* pedges;    // [n*n*H] edge id of each path hop (from the previous path node)
+  const double* phd;        // [n*n*H] delay of each path hop (pdelay[previous path node][hop]); null when
+                            // the topology is staged in LDS (pdelay is a cheap LDS lookup there)
   const int16_t* edge_id;   // [n*n]
   const double* edge_cap;   // [E]
   const int16_t* ingress;   // [n_ing]
@@ -631,6 +633,10 @@ GSC_HD_CALL void run_handle(Env& S, const SimConst& K, const TopoDev& T, int pid
 }
 
 // DefaultDecisionMaker.decide_next_node (default_decision_maker.py:18-81): weighted round robin.
+// BIG (device kernels whose state is not LDS-resident: 50 / 200 nodes): counters + weights are loaded
+// in one round trip (the rows are in HBM); the LDS-resident kernels compile the original two-pass scan
+// (their register allocation is sensitive to any change).
+template <bool BIG = false>
 GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P, const Flow& f) {
   if (GSC_UNI(P.state) == D_INIT) {
     S.procs[pid].state = D_RUN;
@@ -657,15 +663,46 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
   // destinations over the lanes: total by a DPP sum, the first destination with the largest
   // (weight - served ratio) by a DPP max + ballot (== the serial strict-greater scan)
   const int lane = wave_lane();
-  int part = 0;
-  for (int d = lane; d < n; d += 64) part += cnt[d];
-  const int total = wave_sum_i32(part);
   double lbest = -1e300;
   int lidx = 0x7fffffff;
-  for (int d = lane; d < n; d += 64) {
-    const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0;
-    const double diff = p[d] > 0 ? p[d] - ratio : -1.0;
-    if (diff > lbest) { lbest = diff; lidx = d; }
+  if constexpr (BIG) {
+    if (n <= 256) {
+      int c4[4];
+      double p4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = lane + 64 * j;
+        const bool in = d < n;
+        c4[j] = in ? cnt[d] : 0;
+        p4[j] = in ? p[d] : 0.0;
+      }
+      const int total = wave_sum_i32(c4[0] + c4[1] + c4[2] + c4[3]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = lane + 64 * j;
+        const double ratio = total > 0 ? (double)c4[j] / (double)total : 0.0;
+        const double diff = p4[j] > 0 ? p4[j] - ratio : -1.0;
+        if (d < n && diff > lbest) { lbest = diff; lidx = d; }
+      }
+    } else {
+      int part = 0;
+      for (int d = lane; d < n; d += 64) part += cnt[d];
+      const int total = wave_sum_i32(part);
+      for (int d = lane; d < n; d += 64) {
+        const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0;
+        const double diff = p[d] > 0 ? p[d] - ratio : -1.0;
+        if (diff > lbest) { lbest = diff; lidx = d; }
+      }
+    }
+  } else {
+    int part = 0;
+    for (int d = lane; d < n; d += 64) part += cnt[d];
+    const int total = wave_sum_i32(part);
+    for (int d = lane; d < n; d += 64) {
+      const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0;
+      const double diff = p[d] > 0 ? p[d] - ratio : -1.0;
+      if (diff > lbest) { lbest = diff; lidx = d; }
+    }
   }
   const double best_v = wave_max_f64(lbest);
   // lanes holding the max: the smallest destination index among them
@@ -688,6 +725,8 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
 }
 
 // DefaultFlowForwarder.forward_flow (default_forwarder.py:21-90); return_link_resources -> ledger_push.
+// BIG: unstaged topology tables (HBM): the hop delay comes from the per-hop table (T.phd).
+template <bool BIG = false>
 GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P0, const Flow& f0) {
   Proc P = P0;
   const int fid = GSC_UNI(P.flow);
@@ -730,6 +769,9 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
   const int hop = GSC_UNI(T.pnodes[pidx]);
   const int cur = GSC_UNI(f.node);
   const int e = GSC_UNI(T.pedges[pidx]);  // == edge_id[cur * n + hop]
+  // hop delay: from the per-hop table (HBM: issued with the hop's node / edge loads, not after them)
+  // or the LDS-staged APSP table
+  const double hd_tab = (BIG && T.phd) ? T.phd[pidx] : 0.0;
   Flow& fm = S.flows[fid];
   fm.node = f.node;
   ledger_apply(S, e);
@@ -742,7 +784,7 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
     return;
   }
   S.link_passed[e] += f.dr;
-  const double hd = T.pdelay[cur * n + hop];
+  const double hd = (BIG && T.phd) ? hd_tab : T.pdelay[cur * n + hop];
   if (GSC_UNI(hop == f.egress && f.fwd_eg)) fm.departed = 1;
   P.state = F_AFTER_HOP;
   P.ret = (int16_t)hop;
@@ -992,6 +1034,7 @@ GSC_HD_CALL void run_trace(Env& S, const SimConst& K, const TopoDev& T, int pid)
 
 // Resume process pid; `fid` = its flow as carried by the event (-1: none).  The process record and
 // the flow record are loaded together (one LDS round trip instead of two dependent ones).
+template <bool BIG = false>
 GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid, int fid) {
   const Proc P = S.procs[pid];
   Flow f;
@@ -999,8 +1042,8 @@ GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid, int f
   if (GSC_UNI(P.flow) != fid) S.h->flags |= FLAG_BAD_STATE;  // event / process flow mismatch
   switch (GSC_UNI(P.type)) {
     case P_HANDLE: run_handle(S, K, T, pid, P, f); break;
-    case P_DECIDE: run_decide(S, K, T, pid, P, f); break;
-    case P_FORWARD: run_forward(S, K, T, pid, P, f); break;
+    case P_DECIDE: run_decide<BIG>(S, K, T, pid, P, f); break;
+    case P_FORWARD: run_forward<BIG>(S, K, T, pid, P, f); break;
     case P_PROCESS: run_process(S, K, T, pid, P, f); break;
     case P_REQUEST: run_request(S, K, pid, P, f); break;
     case P_FINISH: run_finish(S, K, pid, P, f); break;
@@ -1092,6 +1135,7 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
 
 // SimulatorWrapper.apply (placement derivation) + DurationController.get_next_state prologue.
 // The schedule table S.sched must already hold this step's action.
+template <bool BIG = false>
 GSC_HD_CALL void controller_prologue(Env& S, const SimConst& K, const TopoDev& T) {
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1101,7 +1145,7 @@ GSC_HD_CALL void controller_prologue(Env& S, const SimConst& K, const TopoDev& T
     const int lane = wave_lane();
     for (int i = lane; i < N * Sd; i += 64) S.placement[i] = 0;
     lanes_sync(64);
-    const bool masks = n > 64 && pmask_rows(S.d) > 0;  // row bitsets written by load_action
+    const bool masks = BIG && n > 64 && pmask_rows(S.d) > 0;  // row bitsets written by load_action
     for (int c = 0; c < K.C; ++c) {
       uint64_t f[4] = {0, 0, 0, 0};  // node bitset (n <= 256)
       for (int i = 0; i < T.n_ing; ++i) {
@@ -1342,49 +1386,52 @@ GSC_HD void write_stats(const Env& S, float* st) {
 }
 
 // Copy this step's (post-processed) action block into the schedule table.
+template <bool BIG = false>
 GSC_HD void load_action(Env& S, const SimConst& K, const TopoDev& T, const float* act, int lane, int nlanes) {
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n, P = K.n_pad;
 #if defined(__HIP_DEVICE_COMPILE__)
-  if (n > 16 && nlanes == 64) {
-    const bool masks = pmask_rows(S.d) > 0;
-    // schedule rows with the destinations over the lanes (no index divisions), kG rows per pass with
-    // all their loads in flight before the first use (one HBM round trip per pass, not per row); each
-    // row's positive destinations' bitset from the same pass's ballots
-    constexpr int kG = 8;
-    const int rows = n * C * Sd;
-    int src = 0, c = 0, sf = 0;
-    for (int r0 = 0; r0 < rows; r0 += kG) {
-      float v[kG][4];
-      int ra[kG], rs[kG];
+  if constexpr (BIG) {
+    if (n > 16 && nlanes == 64) {
+      const bool masks = pmask_rows(S.d) > 0;
+      // schedule rows with the destinations over the lanes (no index divisions), kG rows per pass with
+      // all their loads in flight before the first use (one HBM round trip per pass, not per row); each
+      // row's positive destinations' bitset from the same pass's ballots
+      constexpr int kG = 8;
+      const int rows = n * C * Sd;
+      int src = 0, c = 0, sf = 0;
+      for (int r0 = 0; r0 < rows; r0 += kG) {
+        float v[kG][4];
+        int ra[kG], rs[kG];
 #pragma unroll
-      for (int g = 0; g < kG; ++g) {
-        ra[g] = (src * K.C + c) * K.F + sf;  // action row / schedule row of row r0 + g
-        rs[g] = (src * C + c) * Sd + sf;
-        if (++sf == Sd) { sf = 0; if (++c == C) { c = 0; ++src; } }
-      }
-#pragma unroll
-      for (int g = 0; g < kG; ++g)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int dst = 64 * q + lane;
-          v[g][q] = (r0 + g < rows && dst < n) ? act[(long)ra[g] * P + dst] : 0.f;
+        for (int g = 0; g < kG; ++g) {
+          ra[g] = (src * K.C + c) * K.F + sf;  // action row / schedule row of row r0 + g
+          rs[g] = (src * C + c) * Sd + sf;
+          if (++sf == Sd) { sf = 0; if (++c == C) { c = 0; ++src; } }
         }
 #pragma unroll
-      for (int g = 0; g < kG; ++g) {
-        if (r0 + g >= rows) break;
-        double* srow = S.sched + (long)rs[g] * N;
+        for (int g = 0; g < kG; ++g)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int dst = 64 * q + lane;
-          if (dst < n) srow[dst] = (double)v[g][q];
-          if (masks) {
-            const uint64_t b = (uint64_t)__ballot(v[g][q] > 0.f);
-            if (lane == q) S.pmask[4L * rs[g] + q] = b;
+          for (int q = 0; q < 4; ++q) {
+            const int dst = 64 * q + lane;
+            v[g][q] = (r0 + g < rows && dst < n) ? act[(long)ra[g] * P + dst] : 0.f;
+          }
+#pragma unroll
+        for (int g = 0; g < kG; ++g) {
+          if (r0 + g >= rows) break;
+          double* srow = S.sched + (long)rs[g] * N;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int dst = 64 * q + lane;
+            if (dst < n) srow[dst] = (double)v[g][q];
+            if (masks) {
+              const uint64_t b = (uint64_t)__ballot(v[g][q] > 0.f);
+              if (lane == q) S.pmask[4L * rs[g] + q] = b;
+            }
           }
         }
       }
+      return;
     }
-    return;
   }
 #endif
   const int total = n * C * Sd * n;

@@ -179,6 +179,7 @@ __device__ __forceinline__ TopoDev stage_topo(const TopoDev& g, char* dst, int l
   t.pdelay = (const double*)put(g.pdelay, 8 * n2);
   t.plen = (const int16_t*)put(g.plen, 2 * n2);
   t.pnodes = (const int16_t*)put(g.pnodes, 2 * n2 * g.H);
+  t.phd = nullptr;  // staged: the hop delay is an LDS pdelay lookup
   if (pedges) t.pedges = (const int16_t*)put(g.pedges, 2 * n2 * g.H);
   t.edge_id = (const int16_t*)put(g.edge_id, 2 * n2);
   t.edge_cap = (const double*)put(g.edge_cap, 8 * (g.E > 0 ? g.E : 1));
@@ -297,7 +298,7 @@ struct BucketLayout {
   static constexpr Layout L = make_layout(B::dims());
 };
 
-template <class B, int QS, bool PROF>
+template <class B, int QS, bool PROF, bool BIG>
 __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst& K, char* base, char* topo_lds,
                                                 int env, int lane, char* cold = nullptr) {
   const unsigned long long t_entry = PROF ? __builtin_amdgcn_s_memtime() : 0;
@@ -312,14 +313,15 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   S.h = &h_reg;
   const TopoDev T = a.topo_stage ? stage_topo(a.topos[S.h->topo], topo_lds, lane, a.stage_pedges)
                                  : a.topos[S.h->topo];
-  load_action(S, K, T, a.actions + (long)env * a.action_stride, lane, 64);
+  load_action<BIG>(S, K, T, a.actions + (long)env * a.action_stride, lane, 64);
   __syncthreads();
+  const unsigned long long t_act = PROF ? __builtin_amdgcn_s_memtime() : 0;
   // pending events -> sorted register queue; S.events then serves as the handlers' inbox
   RegQueue<QS> q;
   rq_init(q);
   rq_merge_inbox<QS>(q, S, lane);
   __syncthreads();  // every lane writes the same placement/sf tables: order the reads
-  controller_prologue(S, K, T);
+  controller_prologue<BIG>(S, K, T);
   schedule_stop(S, K);
   __syncthreads();
   rq_merge_inbox<QS>(q, S, lane);
@@ -360,7 +362,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
         S.h->cur_key = k;
         const unsigned long long td = prof ? __builtin_amdgcn_s_memtime() : 0;
         const int ptype = prof ? S.procs[p].type * 4 + (S.procs[p].state < 3 ? S.procs[p].state : 3) : 0;
-        dispatch(S, K, T, p, pf);
+        dispatch<BIG>(S, K, T, p, pf);
         ++n_disp;
         if (prof && lane == 0) {
           a.prof_types[((long)env * 64 + ptype) * 2] += __builtin_amdgcn_s_memtime() - td;
@@ -412,6 +414,8 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     pr[3] += n_ev;
     a.prof_types[((long)env * 64 + 62) * 2] += t_begin - t_entry;  // prologue (topology stage, action, inbox)
     a.prof_types[((long)env * 64 + 62) * 2 + 1] += 1;
+    a.prof_types[((long)env * 64 + 57) * 2] += t_act - t_entry;    // of which: topology stage + action load
+    a.prof_types[((long)env * 64 + 57) * 2 + 1] += 1;
   }
   __syncthreads();
   // write the queue back (sorted) as the persistent pending-event array
@@ -494,7 +498,7 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
     copy16(smem, g, sbytes, lane);
     __syncthreads();
     const unsigned long long t1 = PROF ? __builtin_amdgcn_s_memtime() : 0;
-    device_step_env<B, QSETS, PROF>(a, *Ks, smem, topo_lds, env, lane, LDS_STATE == 2 ? g : nullptr);
+    device_step_env<B, QSETS, PROF, LDS_STATE == 2>(a, *Ks, smem, topo_lds, env, lane, LDS_STATE == 2 ? g : nullptr);
     const unsigned long long t2 = PROF ? __builtin_amdgcn_s_memtime() : 0;
     copy16(g, smem, sbytes, lane);
     if (PROF && lane == 0) {  // state blob HBM -> LDS / LDS -> HBM
@@ -505,7 +509,7 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
     }
   } else {
     __syncthreads();
-    device_step_env<B, QSETS, false>(a, *Ks, g, topo_lds, env, lane);
+    device_step_env<B, QSETS, false, true>(a, *Ks, g, topo_lds, env, lane);
   }
   if (PROF && lane == 0) {
     a.prof_types[((long)env * 64 + 58) * 2] += __builtin_amdgcn_s_memtime() - c_begin;
@@ -585,6 +589,7 @@ class SimContext {
       td.plen = ptr<const int16_t>(t["plen"].cast<uintptr_t>());
       td.pnodes = ptr<const int16_t>(t["pnodes"].cast<uintptr_t>());
       td.pedges = ptr<const int16_t>(t["pedges"].cast<uintptr_t>());
+      td.phd = ptr<const double>(t["phd"].cast<uintptr_t>());
       td.edge_id = ptr<const int16_t>(t["edge_id"].cast<uintptr_t>());
       td.edge_cap = ptr<const double>(t["edge_cap"].cast<uintptr_t>());
       td.ingress = ptr<const int16_t>(t["ingress"].cast<uintptr_t>());

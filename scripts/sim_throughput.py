@@ -66,9 +66,10 @@ if args.profile:
     ty = pr[args.envs * 4:].view(args.envs, 64, 2).sum(0)
     names = ["free", "writer", "mmpp", "trace", "arrival", "handle", "decide", "forward", "process", "request",
              "finish", "retlink"]
-    phases = {60: "copy-in (state HBM->LDS)", 61: "copy-out (LDS->HBM)", 62: "prologue", 63: "epilogue"}
-    tot = ty[:58, 0].sum()
-    for i in range(58):
+    phases = {60: "copy-in (state HBM->LDS)", 61: "copy-out (LDS->HBM)", 62: "prologue",
+              57: "  of which topology stage + action load", 63: "epilogue"}
+    tot = ty[:57, 0].sum()
+    for i in range(57):
         if ty[i, 1] > 0:
             print(f"  {names[i // 4]:8s} state {i % 4} events/env-step={ty[i, 1] / (args.envs * args.steps):7.1f} "
                   f"cycles/dispatch={ty[i, 0] / ty[i, 1]:7.0f} share={ty[i, 0] / tot:.3f}")
