@@ -221,9 +221,11 @@ int actor_proj(uintptr_t h, long ldh, uintptr_t w, long ldw, uintptr_t bias, uin
   const int rbs = (M + BM - 1) / BM;
   const int tiles = (A + BN - 1) / BN;
   // enough row blocks (large batches): one split, H read once and the whole W stream shared through
-  // L2; else >= 256 workgroups with S a multiple of 8 (XCD grouping)
-  int S = rbs >= 128 ? 1 : ((256 + rbs - 1) / rbs + 7) / 8 * 8;
-  while (S > 8 && (long)S * M * J > slab_floats) S -= 8;
+  // L2 -- unless the action space is long (>= 128 tiles: 50-node A = 22,500 is 352), where one split
+  // left 200 workgroups walking every tile (1.2 ms at B = 25,600): 8 splits, one per XCD.  Small
+  // batches: >= 256 workgroups with S a multiple of 8 (XCD grouping).
+  int S = rbs >= 128 ? (tiles >= 128 ? 8 : 1) : ((256 + rbs - 1) / rbs + 7) / 8 * 8;
+  while (S > 1 && (long)S * M * J > slab_floats) S = S > 8 ? S - 8 : 1;
   GSC_CHECK((long)S * M * J <= slab_floats, "actor_proj: slabs too small");
   if (S > tiles) S = tiles;
   Args a{};

@@ -202,10 +202,13 @@ def test_splitk_linear_matches_linear():
         assert (o - r).abs().max() <= 2e-2 * r.abs().max()
 
 
-@pytest.mark.parametrize("M,K,A,J,T", [(300, 256, 1000, 64, 3), (128, 128, 4096, 48, 1), (77, 64, 136, 64, 4)])
+@pytest.mark.parametrize("M,K,A,J,T", [(300, 256, 1000, 64, 3), (128, 128, 4096, 48, 1), (77, 64, 136, 64, 4),
+                                       (300, 256, 1001, 64, 2), (16384, 256, 8200, 64, 3)])
 def test_actor_proj_matches_reference(M, K, A, J, T):
     """Fused actor output layer + critic action projection (csrc/ops/actor_proj.hip) against fp32
-    PyTorch: Z = bf16(clamp((H W^T + b) * mask[topo], -1, 1)) Wa^T (edge tiles in M, A and J)."""
+    PyTorch: Z = bf16(clamp((H W^T + b) * mask[topo], -1, 1)) Wa^T (edge tiles in M, A and J).
+    A % 8 != 0: Wa rows zero-padded to a multiple of 8 columns (the caller's contract); 16,384 rows x
+    129 tiles: the large-batch, long-action-space split (8 splits)."""
     from gsc_amd.native import load
     nat = load()
     g = torch.Generator(device="cuda").manual_seed(0)
@@ -215,10 +218,12 @@ def test_actor_proj_matches_reference(M, K, A, J, T):
     mask = (torch.rand(T, A, device="cuda", generator=g) > 0.3).float()
     topo = torch.randint(0, T, (M,), device="cuda", generator=g, dtype=torch.int32)
     wa = (torch.randn(J, A, device="cuda", generator=g) * 0.05).bfloat16()
-    slabs = torch.empty(1 << 22, device="cuda")
+    wa_pad = torch.zeros(J, -(-A // 8) * 8, device="cuda", dtype=torch.bfloat16)
+    wa_pad[:, :A] = wa
+    slabs = torch.empty(1 << 24, device="cuda")
     z = torch.full((M, 80), float("nan"), device="cuda")
     nat.actor_proj(h.data_ptr(), h.stride(0), w.data_ptr(), w.stride(0), b.data_ptr(), mask.data_ptr(), mask.stride(0),
-                   T, topo.data_ptr(), wa.data_ptr(), wa.stride(0), M, K, A, J, -1.0, 1.0, slabs.data_ptr(),
+                   T, topo.data_ptr(), wa_pad.data_ptr(), wa_pad.stride(0), M, K, A, J, -1.0, 1.0, slabs.data_ptr(),
                    slabs.numel(), z.data_ptr(), z.stride(0), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     p = ((h.float() @ w.float().t() + b) * mask[topo.long()]).clamp(-1, 1).bfloat16().float()
