@@ -381,10 +381,15 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* slabs, 
 // Grid (N, S): workgroup (n, z) reads row n of W once over its A-chunk for TT topologies at a time (W is
 // the HBM stream; the x rows stay in L2), bf16 pairs when the row is 4-byte aligned.  S > 1 writes
 // partials [S][T][N] for splitk_reduce (fixed order: deterministic).
-template <int TT>
+// BITS: x is a 0/1 matrix given as packed bits (uint32 words, bit a % 32 of word a / 32, ldx words per
+// row): the mask fold reads 1/32 of the fp32 mask bytes per W element (at A = 360,000 the fp32 masks,
+// re-read from L2 by every row n, were the kernel's main traffic).  x_a w_a with x_a in {0, 1} is w_a
+// or zero exactly, so the sums equal the fp32 path's (up to the sign of zero).
+template <int TT, bool BITS>
 __global__ __launch_bounds__(256) void rowdot_kernel(const float* x, long ldx, int T, const __hip_bfloat16* W,
                                                      long ldw, int N, int A, int achunk, int pair, float* out,
                                                      long ldo) {
+  const uint32_t* xb = reinterpret_cast<const uint32_t*>(x);
   __shared__ float red[4][TT];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n = blockIdx.x, z = blockIdx.y;
@@ -401,8 +406,13 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* x, long ldx, i
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
           if (t0 + t < T) {
-            const float2 xv = *reinterpret_cast<const float2*>(x + (long)(t0 + t) * ldx + a);
-            s[t] += xv.x * w0 + xv.y * w1;
+            if constexpr (BITS) {
+              const uint32_t wd = xb[(long)(t0 + t) * ldx + (a >> 5)] >> (a & 31);  // a even: a + 1 in the same word
+              s[t] += ((wd & 1u) ? w0 : 0.f) + ((wd & 2u) ? w1 : 0.f);
+            } else {
+              const float2 xv = *reinterpret_cast<const float2*>(x + (long)(t0 + t) * ldx + a);
+              s[t] += xv.x * w0 + xv.y * w1;
+            }
           }
         }
       }
@@ -410,8 +420,11 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* x, long ldx, i
       for (int a = a0 + (int)threadIdx.x; a < a1; a += 256) {
         const float w0 = __bfloat162float(wr[a]);
 #pragma unroll
-        for (int t = 0; t < TT; ++t)
-          if (t0 + t < T) s[t] += x[(long)(t0 + t) * ldx + a] * w0;
+        for (int t = 0; t < TT; ++t) {
+          if (t0 + t >= T) continue;
+          if constexpr (BITS) s[t] += ((xb[(long)(t0 + t) * ldx + (a >> 5)] >> (a & 31)) & 1u) ? w0 : 0.f;
+          else s[t] += x[(long)(t0 + t) * ldx + a] * w0;
+        }
       }
     }
 #pragma unroll
@@ -738,7 +751,7 @@ void cast2d(uintptr_t src, long lds_, uintptr_t dst, long ldd, int R, int C, uin
 
 // ws (optional, >= S T N floats): A split over S workgroups per row when N alone gives a small grid.
 void rowdot(uintptr_t x, long ldx, int T, uintptr_t W, long ldw, int N, int A, uintptr_t out, long ldo,
-            uintptr_t stream, uintptr_t ws, long ws_floats) {
+            uintptr_t stream, uintptr_t ws, long ws_floats, uintptr_t xbits, long ldb) {
   if ((long)T * N <= 0) return;
   int S = 1;
   if (ws) {
@@ -750,17 +763,27 @@ void rowdot(uintptr_t x, long ldx, int T, uintptr_t W, long ldw, int N, int A, u
   int achunk = (A + S - 1) / S;
   achunk = (achunk + 1) & ~1;
   S = (A + achunk - 1) / achunk;
-  const int pair = (W % 4 == 0) && (ldw % 2 == 0) && (x % 8 == 0) && (ldx % 2 == 0) && (A % 2 == 0);
+  const bool bits = xbits != 0;
+  const int pair = (W % 4 == 0) && (ldw % 2 == 0) && (A % 2 == 0) && (bits || ((x % 8 == 0) && (ldx % 2 == 0)));
   const hipStream_t s = stream_of(stream);
   float* dst = S > 1 ? ptr<float>(ws) : ptr<float>(out);
+  const float* xs = bits ? ptr<const float>(xbits) : ptr<const float>(x);
+  const long lx = bits ? ldb : ldx;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)N, (unsigned)S), dim3(256), 0, s, ptr<const float>(x), ldx, T,
+    hipLaunchKernelGGL(kern, dim3((unsigned)N, (unsigned)S), dim3(256), 0, s, xs, lx, T,
                        ptr<const __hip_bfloat16>(W), ldw, N, A, achunk, pair, dst, ldo);
   };
-  if (T <= 1) go(rowdot_kernel<1>);
-  else if (T <= 2) go(rowdot_kernel<2>);
-  else if (T <= 4) go(rowdot_kernel<4>);
-  else go(rowdot_kernel<8>);
+  if (bits) {
+    if (T <= 1) go(rowdot_kernel<1, true>);
+    else if (T <= 2) go(rowdot_kernel<2, true>);
+    else if (T <= 4) go(rowdot_kernel<4, true>);
+    else go(rowdot_kernel<8, true>);
+  } else {
+    if (T <= 1) go(rowdot_kernel<1, false>);
+    else if (T <= 2) go(rowdot_kernel<2, false>);
+    else if (T <= 4) go(rowdot_kernel<4, false>);
+    else go(rowdot_kernel<8, false>);
+  }
   check_launch();
   if (S > 1) splitk_reduce(ws, (long)T * N, S, T, N, N, out, ldo, 1.f, 0, stream);
 }
@@ -783,7 +806,8 @@ void register_mlp(py::module_& m) {
   m.def("cast2d", &mlp::cast2d, "fp32 -> bf16 strided 2-D copy");
   m.def("rowdot", &mlp::rowdot, "out[t][n] = sum_a x[t][a] W[n][a] (mask fold of a first layer, small GEMVs)",
         py::arg("x"), py::arg("ldx"), py::arg("T"), py::arg("W"), py::arg("ldw"), py::arg("N"), py::arg("A"),
-        py::arg("out"), py::arg("ldo"), py::arg("stream"), py::arg("ws") = 0, py::arg("ws_floats") = 0);
+        py::arg("out"), py::arg("ldo"), py::arg("stream"), py::arg("ws") = 0, py::arg("ws_floats") = 0,
+        py::arg("xbits") = 0, py::arg("ldb") = 0);
   m.def("topo_expand", &mlp::topo_expand, "dst[r][t C + c] = (topo[r] == t) src[r][c] (bf16 per-topology blocks)");
   m.def("mlp_head", &mlp::head, "critic output layer + TD target / critic loss / actor loss (fused)");
   m.def("first_layer_grad", &mlp::first_layer_grad, "first-layer weight/bias/mask-block gradient from the aug GEMM");

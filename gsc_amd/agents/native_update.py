@@ -38,6 +38,21 @@ from gsc_amd.native import load as load_native
 from gsc_amd.ops.gnn import _layer_of, _tables, gnn_use_fused
 from gsc_amd.ops.mlp import auto_splits, gemm
 
+
+def mask_bits(masks: torch.Tensor) -> Optional[torch.Tensor]:
+    """Pack 0/1 action masks [T, A] into uint32 words (bit a % 32 of word a // 32, as int32) for the
+    bit variant of the mask-fold kernel (``rowdot(..., xbits=)``); None when a mask is not exactly 0/1."""
+    import numpy as np
+    m = masks.detach().float().cpu()
+    if not bool(((m == 0) | (m == 1)).all()):
+        return None
+    T, A = m.shape
+    W = -(-A // 32)
+    b = np.zeros((T, W * 32), np.uint8)
+    b[:, :A] = m.numpy().astype(np.uint8)
+    packed = np.packbits(b.reshape(T, W, 4, 8), axis=-1, bitorder="little").reshape(T, W * 4)
+    return torch.from_numpy(packed.view(np.int32).copy()).to(masks.device)
+
 BF16 = torch.bfloat16
 F32 = torch.float32
 
@@ -93,6 +108,7 @@ class NativeDDPGUpdate:
         self.H = H = L.actor.embedder.hidden_dim
         self.A = A = L.actor.action_dim
         self.masks = L.masks.float().contiguous()          # [T, A]
+        self.mbits = mask_bits(self.masks)                 # packed 0/1 masks for the mask fold
         self.T = T = self.masks.shape[0]
         self.gamma = float(L.gamma)
         self.actor = _Net(L.actor, L.actor_flat, True, H, A, False)
@@ -212,9 +228,11 @@ class NativeDDPGUpdate:
         h0 = net.width(0)
         out = self.rowtab[key][:, :h0]
         w = net.w16(0)
+        mb = self.mbits
         self.nat.rowdot(self.masks.data_ptr(), self.masks.stride(0), self.T, w.data_ptr() + 2 * self.H, w.stride(0),
                         h0, self.A, out.data_ptr(), out.stride(0), self._stream(), self.slabs.data_ptr(),
-                        self.slabs.numel())
+                        self.slabs.numel(), mb.data_ptr() if mb is not None else 0,
+                        mb.shape[1] if mb is not None else 0)
         return out
 
     def _wa(self, net: _Net, key: str, colmask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -442,6 +460,7 @@ class NativeAct:
         self.hid = [torch.zeros(E, n.width(i), device=dev, dtype=BF16) for i in range(n.nh)]
         self.rowtab = torch.zeros(self.T, n.width(0), device=dev)
         self.rowdot_ws = torch.zeros(64 * self.T * n.width(0), device=dev)   # split-A partials of the fold
+        self.mbits = mask_bits(self.masks)
         self.out = torch.zeros(E, self.A, device=dev)
         self.topo32 = torch.zeros(E, dtype=torch.int32, device=dev)
         self._topo_ref, self._topo_ver = None, -1
@@ -465,7 +484,8 @@ class NativeAct:
         w = n.w16(0)
         self.nat.rowdot(self.masks.data_ptr(), self.masks.stride(0), self.T, w.data_ptr() + 2 * self.H, w.stride(0),
                         n.width(0), self.A, self.rowtab.data_ptr(), self.rowtab.stride(0), s, self.rowdot_ws.data_ptr(),
-                        self.rowdot_ws.numel())
+                        self.rowdot_ws.numel(), self.mbits.data_ptr() if self.mbits is not None else 0,
+                        self.mbits.shape[1] if self.mbits is not None else 0)
         self.rowtab_dirty = False
 
     def __call__(self, obs: torch.Tensor, topo: torch.Tensor) -> torch.Tensor:

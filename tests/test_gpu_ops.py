@@ -231,3 +231,28 @@ def test_actor_proj_matches_reference(M, K, A, J, T):
     err = float((z[:, :J] - ref).norm() / ref.norm())
     assert err < 5e-3, err
     assert torch.isnan(z[:, J:]).all()          # only the J columns are written
+
+
+@pytest.mark.parametrize("T,N,A", [(3, 256, 360000), (1, 64, 1875), (2, 64, 1001)])
+def test_rowdot_mask_fold_bits_match_fp32(T, N, A):
+    """Mask fold out[t][n] = sum_a mask[t][a] W[n][a] (csrc/ops/mlp.hip rowdot): the packed-bit mask
+    variant equals the fp32-mask variant (0/1 weights: identical terms), and both match fp32 PyTorch."""
+    from gsc_amd.agents.native_update import mask_bits
+    from gsc_amd.native import load
+    nat = load()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    masks = (torch.rand(T, A, device="cuda", generator=g) > 0.5).float()
+    W = (torch.randn(N, A + (8 if T == 3 else 7), device="cuda", generator=g) * 0.05).bfloat16()  # pair / scalar path
+    bits = mask_bits(masks)
+    ws = torch.zeros(64 * T * N, device="cuda")
+    outs = []
+    for xb in (None, bits):
+        o = torch.full((T, N), float("nan"), device="cuda")
+        nat.rowdot(masks.data_ptr(), masks.stride(0), T, W.data_ptr(), W.stride(0), N, A, o.data_ptr(), o.stride(0),
+                   torch.cuda.current_stream().cuda_stream, ws.data_ptr(), ws.numel(),
+                   xb.data_ptr() if xb is not None else 0, xb.shape[1] if xb is not None else 0)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = masks @ W[:, :A].float().t()
+    assert float((outs[1] - ref).norm() / ref.norm()) < 1e-5
