@@ -49,7 +49,7 @@ struct MtLayout {
   int hTrows0, hTrows;           // rows of the per-tile [k][node] images: encoder input (Fin -> 4), hidden
   // per-graph region (byte offsets)
   int xl, xr, xlT, E, sc, mx, sm, topo, pool;  // forward (E doubles as E^T in the backward)
-  int hR[2], hTs;                // forward: ping-pong node images [NV][kMfRS]; save: per-tile h^T staging
+  int hR[2];                     // forward: ping-pong node images [NV][kMfRS] (save: h^T staged in dead rows)
   int ld, ldw;                   // backward: per-wave loaded layer images (own rows + own h^T), bytes per wave
   int al, da, dy, dyT[2], U, ss; // backward
   int encW, encK;                // backward: per-wave encoder dW image
@@ -131,9 +131,13 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
     mt_load_topo(T, a, a.topo[g], w);
     const int n = T.n, nl = n - 32 * w;  // real rows of the own tile (may be <= 0)
     // own rows: clear E, input features -> bf16 rows (and the saved per-tile transposed image)
+    // save staging of the per-tile transposed image h^T (HPF x kMtTS bf16 <= one tile's 32 x kMfRS
+    // rows): the own rows of the ping-pong buffer that holds nothing live -- hR[1] before layer 0, the
+    // current layer's input (read only by its node linears) in each layer's epilogue.  No extra LDS, so
+    // the saving forward keeps the plain forward's three workgroups per CU (was two at +3.8 KB).
     {
       __bf16* hA = reinterpret_cast<__bf16*>(G + m.hR[0]) + 32 * w * kMfRS;
-      __bf16* hT = reinterpret_cast<__bf16*>(G + m.hTs) + w * HPF * kMtTS;
+      __bf16* hT = reinterpret_cast<__bf16*>(G + m.hR[1]) + 32 * w * kMfRS;
       const float* xg = a.x + ((long)g * a.P + 32 * w) * a.Fin;
       for (int i = lane; i < 32 * 32; i += 64) {
         const int v = i >> 5, k = i & 31;
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
     if (SAVE) {  // layer-0 input chunk of the own tile
       char* dst = reinterpret_cast<char*>(a.blob) + (long)g * m.blob + m.bl_layer[0] + w * m.bl_tile[0];
       const uint4* s0 = reinterpret_cast<const uint4*>(G + m.hR[0] + 32 * w * kMfRS * 2);
-      const uint4* s1 = reinterpret_cast<const uint4*>(G + m.hTs + w * HPF * kMtTS * 2);
+      const uint4* s1 = reinterpret_cast<const uint4*>(G + m.hR[1] + 32 * w * kMfRS * 2);
       const int n0 = mt_tile_hR_bytes() / 16, n1 = m.hTrows0 * kMtTS * 2 / 16;
       for (int i = lane; i < n0 + n1; i += 64)
         reinterpret_cast<uint4*>(dst)[i] = i < n0 ? s0[i] : s1[i - n0];
@@ -235,12 +239,12 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
           hb[((i & 3) + 8 * (i >> 2)) * kMfRS] = (__bf16)o[i];
         }
         if (SAVE) {
-          __bf16* hT = reinterpret_cast<__bf16*>(G + m.hTs) + w * HPF * kMtTS;
+          __bf16* hT = reinterpret_cast<__bf16*>(G + m.hR[cur]) + 32 * w * kMfRS;  // dead input rows
           mt_store_T(o, hT, kMtTS, 0, HPF, lane, false);
           cl_wave_sync();
           char* dst = reinterpret_cast<char*>(a.blob) + (long)g * m.blob + m.bl_layer[l + 1] + w * m.bl_tile[l + 1];
           const uint4* s0 = reinterpret_cast<const uint4*>(G + m.hR[cur ^ 1] + 32 * w * kMfRS * 2);
-          const uint4* s1 = reinterpret_cast<const uint4*>(G + m.hTs + w * HPF * kMtTS * 2);
+          const uint4* s1 = reinterpret_cast<const uint4*>(G + m.hR[cur] + 32 * w * kMfRS * 2);
           const int n0 = mt_tile_hR_bytes() / 16, n1 = m.hTrows * kMtTS * 2 / 16;
           for (int i = lane; i < n0 + n1; i += 64)
             reinterpret_cast<uint4*>(dst)[i] = i < n0 ? s0[i] : s1[i - n0];
@@ -600,7 +604,7 @@ static MtLayout mt_layout(const ClArgs& a, int kind, int HPF) {
     m.mx = take(m.NV * 4);
     m.sm = take(m.NV * 4);
     m.pool = take(m.NT * 32 * 4);
-    if (kind == kMtSave) m.hTs = take(m.NT * HPF * kMtTS * 2);
+    static_assert(32 * kMtTS <= 32 * kMfRS, "the h^T staging must fit one tile's rows of hR");
   } else {
     m.ldw = (mt_tile_hR_bytes() + HPF * kMtTS * 2 + 15) & ~15;
     m.ld = take(m.NT * m.ldw);
