@@ -407,6 +407,7 @@ class BatchedTrainer:
         self.schedule = list(network_schedule) if network_schedule else [0]
         self.period = int(period) if period else 0
         self.sim.set_topologies(self.schedule[0])
+        self._sched_idx = 0  # schedule entry last written to the simulator's next-reset topologies
         # acting actions are double-buffered by step parity and observations triple-buffered: with the
         # simulator overlapped, step t's replay insert runs after step t+1's simulator launch (off the
         # sim -> act -> sim critical path) and still reads step t's buffers, while the simulator writes
@@ -491,7 +492,9 @@ class BatchedTrainer:
         if (self.global_step + 1) % steps == 0:
             nxt = self.episode + 1
             idx = (nxt // self.period) % len(self.schedule) if self.period else 0
-            self.sim.set_topologies(self.schedule[idx])
+            if idx != self._sched_idx:  # unchanged: the device table already holds it (no host copy)
+                self.sim.set_topologies(self.schedule[idx])
+                self._sched_idx = idx
 
     @property
     def obs(self) -> torch.Tensor:
@@ -697,5 +700,6 @@ class BatchedTrainer:
         self.sim.seeds.copy_(torch.from_numpy(g.integers(1, 2**31 - 1, size=self.E).astype(np.uint32)
                                               .view(np.int32)).to(self.device))
         self.sim.set_topologies(self.topo.to(torch.int32))
+        self._sched_idx = None  # per-env table written directly: the next scheduled entry is rewritten
         self._obs_bufs[self.global_step % 3].copy_(self.sim.reset())
         self.replay.reseed(int(seed) * 7919 + self.global_step)
