@@ -17,7 +17,10 @@
 //
 // Fused epilogue (in order): alpha, + bias[n], + rowtab[topo[m]][n] (per-topology mask fold of the
 // first layer), + C32 (accumulate a previous K segment), * (gate[m][n] > 0) (ReLU derivative of a
-// saved activation), ReLU, * colmask[topo[m]][n] (actor output mask), clamp; bf16 and/or fp32 out.
+// saved activation), ReLU, sigmoid (bounded actor output; its derivative s (1 - s) * colmask optionally
+// written to dsig), * colmask[topo[m]][n] (actor output mask), * gmul[m][n] (a saved elementwise
+// derivative: the sigmoid gate of the actor backward; may alias the bf16 output), clamp; bf16 and/or
+// fp32 out.
 // Split-K (gridDim.z > 1) writes raw fp32 slabs, summed by splitk_reduce in a fixed order
 // (deterministic weight gradients, no atomics).
 //
@@ -65,7 +68,11 @@ struct Epilogue {
   const __hip_bfloat16* gate;  // [M][ld_gate]: multiply by (gate > 0)
   long ld_gate;
   const float* rowscale;  // [M]: multiply row m
-  int relu, clamp, accumulate;
+  const __hip_bfloat16* gmul;  // [M][ld_gmul]: multiply by gmul (read before c16 is written: may alias it)
+  long ld_gmul;
+  __hip_bfloat16* dsig;  // [M][ld_dsig]: sigmoid derivative s (1 - s) (* colmask) of the sigmoid epilogue
+  long ld_dsig;
+  int relu, clamp, accumulate, sigmoid;
   int single_topo;       // rowtab / colmask have one row (every topo[m] == 0): no per-row gathers
   int vec16;             // c16 base 16-byte aligned and ldc16 % 8 == 0: staged 16-byte row stores
   float lo, hi;
@@ -312,7 +319,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         if (e.accumulate) v += c32[m * e.ldc32 + n];
         if (e.gate && !(__bfloat162float(e.gate[m * e.ld_gate + n]) > 0.f)) v = 0.f;
         if (e.relu) v = v > 0.f ? v : 0.f;
+        if (e.sigmoid) {
+          v = 1.f / (1.f + __expf(-v));
+          if (e.dsig) e.dsig[m * e.ld_dsig + n] = __float2bfloat16(e.colmask ? v * (1.f - v) * cm[r] : v * (1.f - v));
+        }
         if (e.colmask) v *= cm[r];
+        if (e.gmul) v *= __bfloat162float(e.gmul[m * e.ld_gmul + n]);
         if (e.rowscale) v *= e.rowscale[m];
         if (e.clamp) v = fminf(fmaxf(v, e.lo), e.hi);
         if (c32) c32[m * e.ldc32 + n] = v;
@@ -690,6 +702,11 @@ void gemm(int layout, int M, int N, int K, uintptr_t a, long lda, int adt, uintp
   e.gate = ptr<const __hip_bfloat16>(gp("gate"));
   e.ld_gate = gl("ld_gate", N);
   e.rowscale = ptr<const float>(gp("rowscale"));
+  e.gmul = ptr<const __hip_bfloat16>(gp("gmul"));
+  e.ld_gmul = gl("ld_gmul", N);
+  e.dsig = ptr<__hip_bfloat16>(gp("dsig"));
+  e.ld_dsig = gl("ld_dsig", N);
+  e.sigmoid = ep.contains("sigmoid") ? ep["sigmoid"].cast<int>() : 0;
   e.relu = ep.contains("relu") ? ep["relu"].cast<int>() : 0;
   e.clamp = ep.contains("clamp") ? 1 : 0;
   if (e.clamp) {
@@ -716,6 +733,8 @@ void gemm(int layout, int M, int N, int K, uintptr_t a, long lda, int adt, uintp
   GSC_CHECK(!(e.rowtab || e.colmask) || e.topo, "rowtab/colmask need topo");
   GSC_CHECK(!(g.aug_n0 >= 0) || (layout == 1 || layout == 2), "aug columns need a B_KN operand");
   GSC_CHECK(!(e.accumulate && splits > 1), "accumulate with split-K: accumulate in splitk_reduce");
+  GSC_CHECK(!(e.dsig && !e.sigmoid), "dsig needs the sigmoid epilogue");
+  GSC_CHECK(splits == 1 || !(e.sigmoid || e.gmul), "sigmoid / gmul epilogues do not run with split-K");
   const hipStream_t s = stream_of(stream);
   switch (layout) {
     case 0: launch_layout<false, false>(g, tile, BK, splits, s); break;  // A_ROW, B_NK

@@ -85,7 +85,7 @@ class DDPGLearner:
         self.compose_actor_critic = os.environ.get("GSC_COMPOSE", "1") != "0"
         # GPU: the update runs on hand-written kernels only (native_update.py); GSC_NATIVE_LEARNER=0
         # selects the autograd + PyTorch path (the CPU path, and the reference for the GPU tests)
-        self.native_ok = (self.device.type == "cuda" and self.amp and not self.actor.squash and self.actor.graph_mode
+        self.native_ok = (self.device.type == "cuda" and self.amp and self.actor.graph_mode
                           and os.environ.get("GSC_NATIVE_LEARNER", "1") != "0")
         self._native = None
         self._topo_ready = False

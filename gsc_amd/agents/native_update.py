@@ -115,16 +115,20 @@ class NativeDDPGUpdate:
         self.critic = _Net(L.critic, L.critic_flat, True, H, A, True)
         self.tactor = _Net(L.target_actor, L.target_actor_flat, False, H, A, False)
         self.tcritic = _Net(L.target_critic, L.target_critic_flat, False, H, A, True)
-        if L.actor.squash:
-            raise NotImplementedError("native update: sigmoid-squashed actor output")
+        # bounded actor (actor_output_activation: sigmoid): a = sigmoid(h W^T + b) * mask.  The critic's
+        # action projection cannot be re-associated through the sigmoid, so the [B, A] actor output is
+        # materialised; its GEMM epilogue also writes the gate s (1 - s) * mask into the action-gradient
+        # buffer, which the backward's dL/da GEMM multiplies in place (no extra pass, no autograd)
+        self.squash = bool(L.actor.squash)
         c1 = self.critic.width(0)
         self.compose = (os.environ.get("GSC_COMPOSE", "1") != "0" and self.actor.nh >= 1
-                        and T * c1 <= min(B, 1024))
+                        and T * c1 <= min(B, 1024) and not self.squash)
         # TD target: target actor output layer + target critic action projection in one kernel
         # (csrc/ops/actor_proj.hip, no [B, A] action matrix)
         hl0 = self.actor.width(self.actor.nh - 1) if self.actor.nh else 0
         self.fuse_target = (os.environ.get("GSC_FUSE_TARGET", "1") != "0" and self.actor.nh >= 1 and T <= 4
-                            and c1 <= 64 and hl0 in (64, 128, 256))
+                            and c1 <= 64 and hl0 in (64, 128, 256) and A >= 8  # actor_proj.hip: A >= 8
+                            and not self.squash)
         # [*, A] bf16 operands get rows padded to 8 columns (zeros): 16-byte aligned rows, so the GEMM
         # engine stages them with vector loads also when A % 8 != 0 (50-node topologies: A = 22,500)
         self.A8 = A8 = -(-A // 8) * 8
@@ -340,7 +344,7 @@ class NativeDDPGUpdate:
             self._first(tc, self.emb["tc"], self._rowtab(tc, "tc"), self.hid_c[0], acc_ready=True)
         else:
             gemm(self.hid_ta[last - 1], ta.w16(last), "nt", out16=self.act_buf, bias=ta.b32(last), colmask=self.masks,
-                 topo=self.topo32, clamp=(-1.0, 1.0))
+                 topo=self.topo32, clamp=(-1.0, 1.0), sigmoid=self.squash)
             # target critic on (s', a')
             self._first(tc, self.emb["tc"], self._rowtab(tc, "tc"), self.hid_c[0], extra=self.act_buf,
                         wa=self._wa(tc, "tc"))
@@ -399,7 +403,9 @@ class NativeDDPGUpdate:
             self._first(c, self.emb["c2"], rt_c, self.hid_c[0], extra=hx, wa=self.mccat, extra_rowtab=self.cb)
         else:
             wa = self._wa(c, "c")
-            gemm(hl, a.w16(last), "nt", out16=self.act_buf, bias=a.b32(last), colmask=self.masks, topo=self.topo32)
+            # sigmoid actor: dact <- s (1 - s) * mask, consumed by the dL/da GEMM below
+            gemm(hl, a.w16(last), "nt", out16=self.act_buf, bias=a.b32(last), colmask=self.masks, topo=self.topo32,
+                 sigmoid=self.squash, dsig=self.dact if self.squash else None)
             self._first(c, self.emb["c2"], rt_c, self.hid_c[0], extra=self.act_buf, wa=wa)
         self._hidden_fwd(c, self.hid_c)
         C = c.width(c.nh - 1)
@@ -421,7 +427,8 @@ class NativeDDPGUpdate:
             gemm(self.wam, self.dmc[:, hw:hw + 1], "tn", out32=a.gb(last).view(-1, 1))
             gemm(dh0x, self.mc16, "nn", out16=dz, gate=hl)
         else:
-            gemm(dh0, wa, "nn", out16=self.dact, colmask=self.masks, topo=self.topo32)   # dL/da (masked)
+            gemm(dh0, wa, "nn", out16=self.dact, colmask=self.masks, topo=self.topo32,   # dL/da (masked)
+                 gmul=self.dact if self.squash else None)                             # (* sigmoid gate)
             gemm(self.dact, hl, "tn", out32=a.gw(last), splits=self.splits, slabs=self.slabs)
             gemm(self.dact, hl[:, :0], "tn", out32=a.gb(last).view(-1, 1), aug_t=0, aug_topo=self.topo32)
             gemm(self.dact, a.w16(last), "nn", out16=dz, gate=hl)
@@ -509,5 +516,5 @@ class NativeAct:
         for i in range(1, n.nh):
             gemm(self.hid[i - 1], n.w16(i), "nt", out16=self.hid[i], bias=n.b32(i), relu=True)
         gemm(self.hid[n.nh - 1], n.w16(n.nh), "nt", out32=self.out, bias=n.b32(n.nh), colmask=self.masks,
-             topo=self.topo32)
+             topo=self.topo32, sigmoid=bool(self.L.actor.squash))
         return self.out

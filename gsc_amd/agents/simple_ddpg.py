@@ -350,8 +350,13 @@ class SimpleDDPG(RLSPAgent):
         stamp (global step, episode, world size), and the ranks meet at a barrier once all are written,
         so a save interrupted between two ranks' writes is detected on resume."""
         sd = self.state_dict()
+        nonce = ckpt.new_nonce()
+        if self._per_rank():
+            from gsc_amd.parallel.dist import sync_string
+            nonce = sync_string(nonce)  # rank 0's: one stamp for every file of this save
+        stamp = ckpt.save_stamp(sd, self.dist.world_size, nonce)
         meta = {"experiment_id": self.agent_helper.experiment_id, "time": time.time(), "rank": self.dist.rank,
-                "world_size": self.dist.world_size, "stamp": ckpt.save_stamp(sd, self.dist.world_size)}
+                "world_size": self.dist.world_size, "stamp": stamp}
         if self._per_rank() and self.dist.rank > 0:
             sd["trainer"].pop("learner", None)       # replicas are identical: rank 0's file holds the learner
             ckpt.save_checkpoint(ckpt.rank_path(path, self.dist.rank), sd, meta=meta, rank=0)
@@ -366,12 +371,13 @@ class SimpleDDPG(RLSPAgent):
         sd = d0["state"]
         if self._per_rank() and self.dist.rank > 0:
             rp = ckpt.rank_path(path, self.dist.rank)
-            stamp = ckpt.save_stamp(sd, self.dist.world_size)
+            stamp = d0.get("meta", {}).get("stamp") or {}
             why = "missing"
             if os.path.exists(rp):
                 dr = ckpt.load_checkpoint(rp)
                 got = dr.get("meta", {}).get("stamp")
-                if got == stamp and d0.get("meta", {}).get("stamp") == stamp:
+                want = ckpt.save_stamp(sd, self.dist.world_size, stamp.get("nonce", ""))
+                if got == stamp and stamp == want:
                     local = dr["state"]
                     local["trainer"]["learner"] = sd["trainer"]["learner"]
                     self.load_state_dict(local)

@@ -32,6 +32,7 @@ from .graphs import GraphSet
 NEG_SLOPE = 0.2
 # GSC_GNN_NATIVE=0: the PyTorch reference embedder on the GPU too (fp32 learning checks)
 _NATIVE_GNN = os.environ.get("GSC_GNN_NATIVE", "1") != "0"
+MAX_NATIVE_HIDDEN = 64  # widest GNN_features any native kernel family covers (csrc/ops/gnn_lw.hip)
 
 
 def glorot_(t: torch.Tensor) -> torch.Tensor:
@@ -121,6 +122,10 @@ class GNNEmbedder(nn.Module):
         if use_native is None:
             use_native = x.is_cuda and _NATIVE_GNN
         if use_native:
+            if self.hidden_dim > MAX_NATIVE_HIDDEN:
+                raise ValueError(f"GNN_features={self.hidden_dim}: the native GATv2 kernels cover at most "
+                                 f"{MAX_NATIVE_HIDDEN} channels (MFMA <= 32, layer-wise <= 64); use a smaller "
+                                 "GNN_features or GSC_GNN_NATIVE=0 (PyTorch reference embedder)")
             from gsc_amd.ops.gnn import gnn_embed, gnn_embed_layerwise, gnn_use_fused
             if gnn_use_fused(self, graphs, x.shape[1], x.shape[2]):
                 return gnn_embed(self, x, topo, graphs)

@@ -69,7 +69,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str = "nt", *, out16: Optiona
          out32: Optional[torch.Tensor] = None, alpha: float = 1.0, bias: Optional[torch.Tensor] = None,
          rowtab: Optional[torch.Tensor] = None, topo: Optional[torch.Tensor] = None,
          colmask: Optional[torch.Tensor] = None, gate: Optional[torch.Tensor] = None,
-         rowscale: Optional[torch.Tensor] = None, relu: bool = False,
+         rowscale: Optional[torch.Tensor] = None, relu: bool = False, sigmoid: bool = False,
+         dsig: Optional[torch.Tensor] = None, gmul: Optional[torch.Tensor] = None,
          clamp=None, accumulate: bool = False, splits: Optional[int] = 1, slabs: Optional[torch.Tensor] = None,
          aug_t: int = -1, aug_topo: Optional[torch.Tensor] = None, tile: Optional[int] = None,
          bk: Optional[int] = None, stream: Optional[int] = None) -> None:
@@ -115,6 +116,14 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str = "nt", *, out16: Optiona
         ep["rowscale"] = rowscale.data_ptr()
     if relu:
         ep["relu"] = 1
+    if sigmoid:  # a = sigmoid(.) (* colmask); dsig <- s (1 - s) (* colmask), the actor backward's gate
+        ep["sigmoid"] = 1
+        if dsig is not None:
+            assert dsig.dtype == torch.bfloat16
+            ep.update(dsig=dsig.data_ptr(), ld_dsig=_ld(dsig))
+    if gmul is not None:  # elementwise factor (may alias out16: each element is read before it is written)
+        assert gmul.dtype == torch.bfloat16
+        ep.update(gmul=gmul.data_ptr(), ld_gmul=_ld(gmul))
     if clamp is not None:
         ep["clamp"] = (float(clamp[0]), float(clamp[1]))
     tile = pick_tile(M, N) if tile is None else int(tile)
@@ -130,7 +139,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str = "nt", *, out16: Optiona
         ep["accumulate"] = 1
     if eff > 1:
         assert (bias is None and rowtab is None and colmask is None and gate is None and rowscale is None and not relu
-                and clamp is None), "split-K supports alpha/accumulate only"
+                and clamp is None and not sigmoid and gmul is None), "split-K supports alpha/accumulate only"
         assert slabs is not None and slabs.numel() >= eff * M * N, "split-K needs fp32 slabs"
         ep.update(c32=slabs.data_ptr(), ldc32=N, slab=M * N, splits=splits)
     else:

@@ -120,7 +120,7 @@ def sim_config_from_files(sim_config: dict, sfc_list: dict, sf_list: dict, agent
     return cfg, trace, sf_names, sfc_names
 
 
-def _default_caps(topos: Sequence[Topology], cfg: dict) -> dict:
+def _default_caps(topos: Sequence[Topology], cfg: dict, trace: Optional[dict] = None) -> dict:
     """Pool capacities sized from the arrival rate (flows alive within one TTL), with margin."""
     max_ing = max(len(t.ingress) for t in topos)
     mean = cfg["inter_arr_mean"]
@@ -129,18 +129,37 @@ def _default_caps(topos: Sequence[Topology], cfg: dict) -> dict:
     ttl = max(cfg["ttl"])
     # flows alive at once <= arrivals within one TTL (every flow ends by its TTL): per ingress
     # ttl / mean, x 2.5 for Poisson bursts, + 8.  Measured peaks on the shipped configs (random
-    # schedules) are 5-12x below this; pools are LDS (a 50-node env's pools fit two envs per CU)
-    per_node = ttl / max(mean, 1e-3) * (1.0 if cfg["det_arrival"] else 2.5) + 8
+    # schedules) are >= 4x below this (tests/test_batched_sim_diff.py::test_default_caps_headroom); pools
+    # are LDS (a 50-node env's pools fit two envs per CU)
+    burst = 1.0 if cfg["det_arrival"] else 2.5
+    rate = burst / max(mean, 1e-3)  # arrivals per ms and ingress, with burst margin
+    if trace is not None and len(trace["mean"]):
+        tm = np.asarray(trace["mean"], np.float64)
+        tm = tm[np.isfinite(tm)]
+        if len(tm):  # a trace sets the inter-arrival means: its busiest row (already a peak) may exceed the margin
+            rate = max(rate, 1.0 / max(float(tm.min()), 1e-3))
+    mean = burst / rate
+    per_node = ttl * rate + 8
     flows = int(min(4096, max(64, max_ing * per_node)))
+    # processes and link returns outlive their flow by its duration (finish_processing and
+    # return_link_resources hold `duration` = size / dr * 1000 ms): the arrivals within one duration
+    # hold up to F finish processes and one return per hop each
+    dr_low = max(cfg["dr_mean"] - 2.0 * cfg["dr_std"], 0.1 * cfg["dr_mean"], 1e-6)
+    if cfg["det_size"]:
+        size = cfg["size_shape"]
+    else:  # Pareto(shape) + 1: mean shape / (shape - 1); heavy tails are capped by the pool limits below
+        a = cfg["size_shape"]
+        size = a / (a - 1.0) if a > 1.0 else 8.0
+    dur = size / dr_low * 1000.0
+    hold = max_ing * (dur / max(mean, 1e-3) * burst + 4) if dur > 1.0 else 0.0
+    hops = max(t.max_hops for t in topos)
     # the pending-event queue lives in VGPRs on the device (64 per set); observed peaks on the reference
     # configs are 30-60 events, so 128 leaves 2x headroom (overflow is flagged, never silent)
-    # link-capacity returns are a ledger, not processes (csrc/sim/sim_core.h ledger_push): pending returns
-    # are bounded like the flows holding links (overflow is flagged, never silent)
     # pending link returns: one per hop a flow took within its duration -- long paths (200 nodes:
     # 12 hops) hold several per flow
-    hops = max(t.max_hops for t in topos)
-    return dict(flow_cap=flows, proc_cap=min(32000, 2 * flows + 32), event_cap=128 if max_ing <= 8 else 256,
-                rel_cap=int(min(16384, 2 * flows * max(1.0, hops / 4))))
+    return dict(flow_cap=flows, proc_cap=int(min(32000, 2 * flows + 32 + cfg["F"] * hold)),
+                event_cap=128 if max_ing <= 8 else 256,
+                rel_cap=int(min(16384, 2 * flows * max(1.0, hops / 4) + hops * hold)))
 
 
 class BatchedSimulator:
@@ -209,7 +228,7 @@ class BatchedSimulator:
                 d[k] = v.data_ptr()
             topo_dicts.append(d)
         self._keep = keep
-        caps = dict(caps or _default_caps(self.topologies, cfg))
+        caps = dict(caps or _default_caps(self.topologies, cfg, trace if cfg["n_trace"] else None))
         dims = dict(N=N, S=self.S, C=self.C, E=max(1, max(t.num_edges for t in self.topologies)), **caps)
         self.dims = dims
         self.ctx = self.native.SimContext(dims, cfg, topo_dicts, self.is_device, host_threads)

@@ -94,10 +94,16 @@ def load_checkpoint(path: str) -> dict:
     return d
 
 
-def save_stamp(state: dict, world_size: int) -> dict:
-    """Identity of one data-parallel save: every rank's file of the same save carries the same stamp."""
+def save_stamp(state: dict, world_size: int, nonce: str = "") -> dict:
+    """Identity of one data-parallel save: every rank's file of the same save carries the same stamp.
+    ``nonce`` (drawn by rank 0 and broadcast) tells apart two saves at the same step, e.g. a resumed run
+    re-saving into the same directory next to a stale rank file."""
     return {"global_step": int(state["global_step"]), "episode": int(state["episode"]),
-            "world_size": int(world_size)}
+            "world_size": int(world_size), "nonce": str(nonce)}
+
+
+def new_nonce() -> str:
+    return os.urandom(8).hex()
 
 
 def save_agent_helper(path: str, helper) -> None:

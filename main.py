@@ -139,9 +139,11 @@ def cli(agent_config, network, service, sim_config, scheduler, episodes, seed, t
         stats = agent.train(episodes)
         h.result.runtime_stop()
         log.info(f"training done: {stats}")
+        # the checkpoint save is collective (data parallel: every rank writes its rank-local trainer state
+        # and the ranks meet at a barrier); the actor / helper / result files are rank 0's
+        agent.save_actor(os.path.join(h.config_dir, "trained_actor.pt"))
+        agent.save_checkpoint(os.path.join(h.config_dir, "checkpoint.pt"))
         if info.is_main:
-            agent.save_actor(os.path.join(h.config_dir, "trained_actor.pt"))
-            agent.save_checkpoint(os.path.join(h.config_dir, "checkpoint.pt"))
             save_agent_helper(os.path.join(h.config_dir, "agent_helper.obj"), h)
             h.result.agent_config = dict(h.config)
             h.result.write_to_file(h.result_file)

@@ -24,6 +24,8 @@ ap.add_argument("--profile", action="store_true")
 ap.add_argument("--simcfg", default="configs/config/simulator/sample_config.yaml")
 ap.add_argument("--cus", type=int, default=0, help="run on a stream CU-masked to this many CUs (0: all)")
 ap.add_argument("--preset", default=None, help="bench.py preset (network / service / simulator / agent config)")
+ap.add_argument("--episode-steps", type=int, default=None, help="override the agent config's episode length "
+                "(default: the preset's, else the config's)")
 args = ap.parse_args()
 if args.preset:
     from bench import PRESETS
@@ -32,6 +34,9 @@ if args.preset:
 else:
     nets, svc, agent = [args.net], "configs/service_functions/abc.yaml", "configs/config/agent/sample_agent.yaml"
 cfg = yaml.safe_load(open(agent))
+ep = args.episode_steps or (pre.get("episode_steps") if args.preset else None)
+if ep:
+    cfg["episode_steps"] = int(ep)
 sim = load_batched_from_paths(nets, svc, args.simcfg, cfg, args.envs, device=args.device)
 n, P = sim.topologies[0].n, sim.n_pad
 rng = np.random.default_rng(0)

@@ -117,3 +117,32 @@ def test_stochastic_configs_match_in_distribution(simcfg):
         D += out.stats[:, 1].sum().item()
     sim.check_flags()
     assert abs(S / (S + D) - s / (s + d)) < 0.02
+
+
+@pytest.mark.parametrize("simcfg", ["sample_config", "rand-arrival10_det-size001_duration100",
+                                    "rand-arrival10_det-size001_duration100_trace_0_100_inall_chrate2_scale00005",
+                                    "rand-mmp-arrival12-8_det-size001_dur100", "pareto-size"])
+def test_default_caps_headroom(simcfg, tmp_path):
+    """Default pool capacities keep >= 2x headroom over the peaks of every shipped simulator config (and a
+    Pareto-size config whose finish processes / link returns outlive their flows by seconds) under dense
+    random schedules -- an overflow aborts a run (check_flags), so the margins must hold for bursty
+    (MMPP, trace) as well as deterministic arrivals."""
+    if simcfg == "pareto-size":
+        c = yaml.safe_load(open(SAMPLE))
+        c.update(deterministic_arrival=False, deterministic_size=False, flow_size_shape=2.5, flow_dr_stdev=0.2)
+        p = tmp_path / "pareto.yaml"
+        p.write_text(yaml.safe_dump(c))
+        p = str(p)
+    else:
+        p = cfg_path("config", "simulator", simcfg + ".yaml")
+    E = 8
+    sim = load_batched_from_paths([NETS["abilene"]], ABC, p, agent_cfg(), E, device="cpu", seed=2, host_threads=4)
+    sim.reset()
+    rng = np.random.default_rng(0)
+    mx = torch.zeros(16)
+    for _ in range(60):
+        o = sim.step(torch.from_numpy(rng.random((E, sim.action_dim), dtype=np.float32)))
+        mx = torch.maximum(mx, o.stats.max(0).values)
+    assert mx[12] == 0, f"flags {mx[12]}"
+    d = sim.dims
+    assert 2 * mx[13] <= d["event_cap"] and 2 * mx[14] <= d["proc_cap"] and 2 * mx[15] <= d["flow_cap"], (d, mx[13:])

@@ -160,8 +160,9 @@ def _resume_worker(rank, port, out_dir, stale=False):
         import shutil
         if rank == 1:
             shutil.copy(os.path.join(out_dir, "ck.rank1.pt"), os.path.join(out_dir, "old.pt"))
-        a.train(1)
-        a.save_checkpoint(path)
+        if stale != "same_step":
+            a.train(1)
+        a.save_checkpoint(path)  # same_step: a re-save at the same step (equal step / episode / world size)
         if rank == 1:
             shutil.copy(os.path.join(out_dir, "old.pt"), os.path.join(out_dir, "ck.rank1.pt"))
         torch.distributed.barrier()
@@ -209,6 +210,48 @@ def test_dp_resume_rejects_stale_rank_file():
     assert r[0]["replay_len"] > 0
     assert r[1]["replay_len"] == 0
     assert r[1]["learning_starts"] > r[1]["step"]
+
+
+def test_dp_resume_rejects_stale_rank_file_from_same_step():
+    """Two saves at the same step (e.g. a resumed run re-saving into the same directory) carry different
+    nonces: a stale rank file of the first is still rejected."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_resume_worker, args=(_free_port(), d, "same_step"), nprocs=WORLD, join=True,
+                           start_method="spawn")
+        r = [torch.load(os.path.join(d, f"res{i}.pt"), weights_only=True) for i in range(WORLD)]
+    assert r[0]["replay_len"] > 0
+    assert r[1]["replay_len"] == 0
+
+
+def test_dp_main_cli_train_save_exit(tmp_path):
+    """main.py under torchrun (2 gloo ranks): train, the collective final checkpoint save (every rank writes
+    its file, one barrier), the test episode on rank 0 and the shutdown barrier all complete; the rank files
+    of the final save carry the same stamp."""
+    import subprocess
+    import sys
+    cfg = _cfg()
+    cfg.update(episode_steps=4, nb_steps_warmup_critic=3, mem_limit=64)
+    agent = tmp_path / "agent.yaml"
+    agent.write_text(yaml.safe_dump(cfg))
+    sched = tmp_path / "sched.yaml"
+    sched.write_text(yaml.safe_dump({"training_network_files": [ABILENE], "inference_network": ABILENE,
+                                     "period": 10}))
+    root = tmp_path / "results"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(WORLD),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "main.py"),
+           str(agent), ABILENE, cfg_path("service_functions", "abc.yaml"),
+           cfg_path("config", "simulator", "sample_config.yaml"), str(sched), "2", "--seed", "21", "--backend",
+           "batched", "--envs", "2", "--device", "cpu", "--results-root", str(root)]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    runs = [os.path.join(dp, f) for dp, _, fs in os.walk(root) for f in fs if f.startswith("checkpoint")]
+    names = sorted(os.path.basename(x) for x in runs)
+    assert names == ["checkpoint.pt", "checkpoint.rank1.pt"], names
+    from gsc_amd.utils import checkpoint as ck
+    stamps = [ck.load_checkpoint(x)["meta"]["stamp"] for x in sorted(runs)]
+    assert stamps[0] == stamps[1] and stamps[0]["episode"] == 2 and stamps[0]["nonce"]
+    assert "test on" in r.stdout
 
 
 def test_checkpoint_format_1_rejected(tmp_path):

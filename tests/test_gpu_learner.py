@@ -64,7 +64,8 @@ def _per_param_err(flat_ref, flat_gpu, what="grad"):
     return out
 
 
-@pytest.mark.parametrize("case", ["composed", "two_topologies", "three_topologies", "deep", "odd_actions"])
+@pytest.mark.parametrize("case", ["composed", "two_topologies", "three_topologies", "deep", "odd_actions", "sigmoid",
+                                  "sigmoid_two_topologies"])
 def test_native_update_matches_fp32_reference(case):
     """Tolerance: per tensor max(3 %, 2.5x the error of the PyTorch bf16-autocast path on the same
     batch) -- deeper nets amplify bf16 rounding through ReLU gates, for either implementation.  The
@@ -81,7 +82,14 @@ def test_native_update_matches_fp32_reference(case):
     T = {"two_topologies": 2, "three_topologies": 3}.get(case, 1)
     P = 25 if case == "odd_actions" else 24         # A = 1,875: A % 8 != 0 (padded action rows)
     cfg = _cfg(actor=(128, 96), critic=(64, 32)) if case == "deep" else _cfg()
+    if case.startswith("sigmoid"):
+        # bounded actor: materialised [B, A] output with the sigmoid epilogue and its in-place backward gate
+        cfg["actor_output_activation"] = "sigmoid"
+        T = 2 if case == "sigmoid_two_topologies" else 1
     ref, gpu = _learners(cfg, T, P)
+    if case.startswith("sigmoid"):
+        nu = gpu.native_update(512)
+        assert nu.squash and not nu.compose and not nu.fuse_target
     _, auto = _learners(cfg, T, P)
     auto.native_ok = False                               # autograd + hipBLASLt bf16 path
     if case == "three_topologies":
@@ -165,11 +173,12 @@ def test_native_update_graphed_matches_eager():
     assert torch.equal(g1.target_actor_flat.flat, g2.target_actor_flat.flat)
 
 
-@pytest.mark.parametrize("T", [1, 2])
-def test_native_act_matches_fp32_module(T):
-    """Acting forward on the native kernels (embedder, folded mask block, hidden, masked output)
-    against the fp32 PyTorch actor on the same weights."""
+@pytest.mark.parametrize("T,act", [(1, "none"), (2, "none"), (2, "sigmoid")])
+def test_native_act_matches_fp32_module(T, act):
+    """Acting forward on the native kernels (embedder, folded mask block, hidden, masked output; the
+    sigmoid epilogue for a bounded actor) against the fp32 PyTorch actor on the same weights."""
     cfg = _cfg()
+    cfg["actor_output_activation"] = act
     ref, gpu = _learners(cfg, T)
     E = 300
     gpu.enable_native_act(E)

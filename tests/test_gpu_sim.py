@@ -70,3 +70,40 @@ def test_device_matches_host_large(case):
         assert torch.equal(oh.stats, od.stats.cpu()), f"step {k}"
         assert torch.equal(oh.obs, od.obs.cpu()), f"step {k}"
     dev.check_flags()
+
+
+def test_device_matches_host_syn200_256_envs():
+    """256 envs of 200-node topologies (one rank's share of a 2,048-env 8-GPU job): device == host over an
+    episode end (topology switch at the reset), with the heavy uniform schedule of scripts/sim_throughput.py
+    (every node forwards to every node: long paths, many pending link returns) and the cycle-counting
+    variant enabled for the second half (it must not touch memory outside its counters)."""
+    from gsc_amd.envs import threshold_normalize
+    cfg = yaml.safe_load(open(cfg_path("config", "agent", "agent_syn200.yaml")))
+    cfg["episode_steps"] = 4
+    E = 256
+    simcfg = cfg_path("config", "simulator", "sample_config.yaml")
+    nets = SYN200[:3]
+    host = load_batched_from_paths(nets, SVC3, simcfg, cfg, E, device="cpu", seed=7, topo_init=np.arange(E) % 3)
+    dev = load_batched_from_paths(nets, SVC3, simcfg, cfg, E, device="cuda", seed=7, topo_init=np.arange(E) % 3)
+    nxt = (np.arange(E) + 1) % 3
+    host.set_topologies(nxt)
+    dev.set_topologies(nxt)
+    assert torch.equal(host.reset().clone(), dev.reset().cpu())
+    P, n = host.n_pad, host.topologies[0].n
+    rng = np.random.default_rng(4)
+    a = np.zeros((P, host.C, host.F, P))
+    a[:n, :, :, :n] = rng.random((n, host.C, host.F, n))
+    uni = threshold_normalize(a.reshape(-1), P, 0.1, 2).astype(np.float32)
+    for k in range(7):
+        if k == 3:
+            dev.enable_profiling()
+        a = np.tile(uni, (E, 1)) if k % 2 == 0 else rng.random((E, host.action_dim), dtype=np.float32)
+        a = torch.from_numpy(a)
+        oh, od = host.step(a), dev.step(a.cuda())
+        torch.cuda.synchronize()
+        assert torch.equal(oh.stats, od.stats.cpu()), f"step {k}"
+        assert torch.equal(oh.obs, od.obs.cpu()), f"step {k}"
+        assert torch.equal(oh.reward, od.reward.cpu()), f"step {k}"
+    assert int(dev.prof[E * 4:].view(E, 64, 2)[:, :, 1].sum()) > 0
+    dev.check_flags()
+    host.check_flags()

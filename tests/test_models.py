@@ -78,6 +78,19 @@ def test_embedder_structure_and_pool():
     torch.testing.assert_close(got, torch.stack(outs), rtol=1e-9, atol=1e-9)
 
 
+def test_native_embedder_rejects_unsupported_width():
+    """GNN_features beyond every native kernel family fails up front with a clear error (not a kernel
+    check at the first forward); the PyTorch reference still covers it."""
+    topo = load_topology(ABILENE)
+    gs = GraphSet([topo], 24)
+    emb = GNNEmbedder(3, 80, 2, "mean", 2)
+    x = torch.rand(2, 24, 3)
+    tid = torch.zeros(2, dtype=torch.long)
+    with pytest.raises(ValueError, match="GNN_features=80"):
+        emb(x, tid, gs, use_native=True)
+    assert emb(x, tid, gs, use_native=False).shape == (2, 80)
+
+
 def test_mixed_topology_batch_is_per_graph():
     torch.manual_seed(2)
     topos = [load_topology(ABILENE), load_topology(TRIANGLE)]
