@@ -55,6 +55,8 @@ struct Operand {
   int dtype;     // DT_BF16 | DT_F32
   int vec;       // bf16, base 16-byte aligned, ld % 8 == 0: 16-byte loads of in-bounds chunks
   int vec32;     // fp32, base 16-byte aligned, ld % 4 == 0: two 16-byte loads per chunk (+ bf16 rounding)
+  const int* rows;  // optional: stored row r is physical row rows[r] (replay-ring rows of a sampled batch read
+                    // in place: the batch is never gathered into its own [B, A] copy)
 };
 
 struct Epilogue {
@@ -135,10 +137,11 @@ struct Stager {
       const int row = idx / CPR, ch = idx % CPR;
       const long gr = srow0 + row, gc = scol0 + ch * 8;
       const bool inb = gr < rows_total && gc + 8 <= cols_total;
+      const long pr = (o.rows && gr < rows_total) ? (long)o.rows[gr] : gr;  // physical row
       if (inb && o.vec) {
-        reg[i] = *reinterpret_cast<const s16x8*>(reinterpret_cast<const short*>(o.p) + gr * o.ld + gc);
+        reg[i] = *reinterpret_cast<const s16x8*>(reinterpret_cast<const short*>(o.p) + pr * o.ld + gc);
       } else if (inb && o.vec32) {
-        const float4* src = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(o.p) + gr * o.ld + gc);
+        const float4* src = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(o.p) + pr * o.ld + gc);
         const float4 x0 = src[0], x1 = src[1];
         reg[i] = s16x8{f2bf(x0.x), f2bf(x0.y), f2bf(x0.z), f2bf(x0.w), f2bf(x1.x), f2bf(x1.y), f2bf(x1.z),
                        f2bf(x1.w)};
@@ -149,7 +152,7 @@ struct Stager {
           const long c = gc + j;
           short x = 0;
           if (gr < rows_total) {
-            if (c < cols_total) x = load_elem(o, gr, c);
+            if (c < cols_total) x = load_elem(o, pr, c);
             else if (aug_n0 >= 0) {  // B_KN virtual columns: stored row = k (gr), column c
               const long t = c - aug_n0;
               if (t == 0) x = f2bf(1.f);
@@ -674,6 +677,7 @@ static Operand operand(uintptr_t p, long ld, int dtype) {
   o.dtype = dtype;
   o.vec = dtype == DT_BF16 && (p % 16 == 0) && (ld % 8 == 0);
   o.vec32 = dtype == DT_F32 && (p % 16 == 0) && (ld % 4 == 0);
+  o.rows = nullptr;
   return o;
 }
 
@@ -686,6 +690,8 @@ void gemm(int layout, int M, int N, int K, uintptr_t a, long lda, int adt, uintp
   g.M = M;
   g.N = N;
   g.K = K;
+  if (ep.contains("a_rows")) g.a.rows = ptr<const int>(ep["a_rows"].cast<uintptr_t>());
+  if (ep.contains("b_rows")) g.b.rows = ptr<const int>(ep["b_rows"].cast<uintptr_t>());
   g.aug_n0 = ep.contains("aug_n0") ? ep["aug_n0"].cast<int>() : -1;
   g.aug_t = ep.contains("aug_t") ? ep["aug_t"].cast<int>() : 0;
   g.aug_topo = ptr<const int>(ep.contains("aug_topo") ? ep["aug_topo"].cast<uintptr_t>() : 0);

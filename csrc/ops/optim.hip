@@ -175,7 +175,81 @@ void grad_guard(uintptr_t g, long n, uintptr_t flag, uintptr_t stream, uintptr_t
   check_launch();
 }
 
+// ---- sharded optimizer (data parallel, ZeRO-1: gsc_amd/parallel/zero.py) ------------------------------
+// local[0] = this rank's gradient shard holds a non-finite value (local[2]/[3]: monotonic event counters as
+// in grad_guard); the ranks then agree on local[0] (all-reduce MAX) before guard_apply
+__global__ void zflag_kernel(int* local) {
+  local[0] = local[2] != local[3];
+  local[3] = local[2];
+}
+void grad_guard_local(uintptr_t g, long n, uintptr_t local, uintptr_t stream) {
+  hipStream_t st = stream_of(stream);
+  long grid = (n + 1023) / 1024;
+  if (grid > 16384) grid = 16384;
+  hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)(grid > 0 ? grid : 1)), dim3(256), 0, st, ptr<const float>(g), n,
+                     ptr<int>(local));
+  hipLaunchKernelGGL(zflag_kernel, dim3(1), dim3(1), 0, st, ptr<int>(local));
+  check_launch();
+}
+// the agreed flag -> the optimizer's guard (flag, flagged-step count) and the device Adam step counter
+__global__ void guard_apply_kernel(const int* agreed, int* flag, long long* step) {
+  const int bad = agreed[0] != 0;
+  flag[0] = bad;
+  flag[1] += bad;
+  if (step && !bad) *step += 1;
+}
+void grad_guard_apply(uintptr_t agreed, uintptr_t flag, uintptr_t step, uintptr_t stream) {
+  hipLaunchKernelGGL(guard_apply_kernel, dim3(1), dim3(1), 0, stream_of(stream), ptr<const int>(agreed), ptr<int>(flag),
+                     ptr<long long>(step));
+  check_launch();
+}
+// after the all-gather of the updated parameters: target = tau p + (1 - tau) target and both bf16 shadows
+// over the whole buffer (skipped step: the target stays, the shadows are rewritten unchanged)
+__global__ __launch_bounds__(256) void polyak_shadow_kernel(const float* __restrict__ p, float* __restrict__ t, long n,
+                                                            float tau, __hip_bfloat16* p16, __hip_bfloat16* t16,
+                                                            const int* skip) {
+  const bool keep = skip && *skip;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long n4 = n >> 2;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 pv = reinterpret_cast<const float4*>(p)[i];
+    if (p16) store_bf16x4(p16, i, pv);
+    if (t) {
+      float4 tv = reinterpret_cast<float4*>(t)[i];
+      if (!keep) {
+        tv.x = tau * pv.x + (1.f - tau) * tv.x;
+        tv.y = tau * pv.y + (1.f - tau) * tv.y;
+        tv.z = tau * pv.z + (1.f - tau) * tv.z;
+        tv.w = tau * pv.w + (1.f - tau) * tv.w;
+        reinterpret_cast<float4*>(t)[i] = tv;
+      }
+      if (t16) store_bf16x4(t16, i, tv);
+    }
+  }
+  for (long i = (n4 << 2) + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (p16) p16[i] = __float2bfloat16(p[i]);
+    if (t) {
+      if (!keep) t[i] = tau * p[i] + (1.f - tau) * t[i];
+      if (t16) t16[i] = __float2bfloat16(t[i]);
+    }
+  }
+}
+void polyak_shadow(uintptr_t p, uintptr_t t, long n, float tau, uintptr_t p16, uintptr_t t16, uintptr_t skip,
+                   uintptr_t stream) {
+  GSC_CHECK((p & 15) == 0 && (t & 15) == 0 && (p16 & 7) == 0 && (t16 & 7) == 0, "polyak_shadow: aligned buffers");
+  long grid = (n / 4 + 511) / 512;
+  if (grid > 65536) grid = 65536;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(polyak_shadow_kernel, dim3((unsigned)grid), dim3(256), 0, stream_of(stream), ptr<const float>(p),
+                     t ? ptr<float>(t) : nullptr, n, tau, p16 ? ptr<__hip_bfloat16>(p16) : nullptr,
+                     t16 ? ptr<__hip_bfloat16>(t16) : nullptr, skip ? ptr<const int>(skip) : nullptr);
+  check_launch();
+}
+
 void register_optim(py::module_& m) {
+  m.def("grad_guard_local", &grad_guard_local, "local[0] = a non-finite value in this rank's gradient shard");
+  m.def("grad_guard_apply", &grad_guard_apply, "guard flag / count / Adam step from the ranks' agreed flag");
+  m.def("polyak_shadow", &polyak_shadow, "target Polyak update + bf16 shadows of params and target (full buffer)");
   m.def("grad_guard", &grad_guard, "flag[0] = any non-finite gradient; flag[1] counts flagged steps; step += !flag[0]",
         py::arg("g"), py::arg("n"), py::arg("flag"), py::arg("stream"), py::arg("step") = 0);
   m.def("adam_polyak", &adam_polyak, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("target"),

@@ -156,8 +156,11 @@ struct Dims {
 struct Layout {
   int hdr, node_cap, node_rem, inter_arr, max_usage, run_drop_node, mmpp_state, sf_load, sf_start, proc_traffic,
       requested, drop_locs, link_rem, link_passed, link_next, rel, flows, procs, events, flow_free, proc_free,
-      sf_present, placement, hot, sched, wrr, pmask, total;
+      sf_present, placement, wrr_ep, hot, sched, wrr, pmask, total;
 };
+
+// WRR counter rows ([N, C, S] rows of N counters) and the run-window epoch that tags them (see run_decide)
+__host__ __device__ constexpr int wrr_rows(const Dims& d) { return d.N * d.C * d.S; }
 
 // Topologies beyond one wave of destinations keep, per schedule row (src, c, sf), the bitset of its
 // positive destinations (4 x 64 bits, n <= 256): the device placement walk ORs rows instead of
@@ -193,6 +196,7 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   GSC_TAKE(proc_free, 2 * d.proc_cap);
   GSC_TAKE(sf_present, d.N * d.S);
   GSC_TAKE(placement, d.N * d.S);
+  GSC_TAKE(wrr_ep, 4 * (wrr_rows(d) + 1));  // per-row epoch + the current run-window epoch (last entry)
   L.hot = o;
   GSC_TAKE(sched, 8 * d.N * d.C * d.S * d.N);
   GSC_TAKE(wrr, 4 * d.N * d.C * d.S * d.N);
@@ -209,6 +213,9 @@ struct Env {
   double *node_cap, *node_rem, *inter_arr, *max_usage, *sf_load, *sf_start, *proc_traffic, *requested, *sched,
       *link_rem, *link_passed, *link_next;
   int32_t *run_drop_node, *mmpp_state, *drop_locs, *wrr;
+  int32_t* wrr_ep;     // [wrr_rows + 1]: run-window epoch of each WRR counter row, then the current epoch
+  const float* act;    // device kernels with HBM-resident schedule tables (BIG): this step's action block
+                       // ([n_pad, C, F, n_pad] floats), read in place of the (double) schedule table
   uint64_t* pmask;
   Release* rel;
   Flow* flows;
@@ -234,6 +241,8 @@ struct Env {
     drop_locs = (int32_t*)(base + L.drop_locs);
     sched = (double*)(cb + L.sched);
     wrr = (int32_t*)(cb + L.wrr);
+    wrr_ep = (int32_t*)(base + L.wrr_ep);
+    act = nullptr;
     pmask = (uint64_t*)(cb + L.pmask);
     link_rem = (double*)(base + L.link_rem);
     link_passed = (double*)(base + L.link_passed);
@@ -529,6 +538,10 @@ GSC_HD void lanes_sync(int ls) {
 
 // l0 / ls: this lane and the lane count sharing the work (device: wave_lane(), 64; host or a
 // single active lane: 0, 1)
+// BIG (device kernels whose [N, C, S, N] tables stay in HBM): the WRR counters are not zeroed here --
+// the run-window epoch advances and a decision zeroes a counter row the first time the window uses it
+// (200 nodes: 1.4 MB of counters per env and window otherwise, written by one wave)
+template <bool BIG = false>
 GSC_HD_CALL void reset_run_metrics(Env& S, const SimConst& K, int n, int l0, int ls) {
   Header* h = S.h;
   h->run_gen = h->run_processed = h->run_dropped = 0;
@@ -537,7 +550,13 @@ GSC_HD_CALL void reset_run_metrics(Env& S, const SimConst& K, int n, int l0, int
   for (int v = l0; v < N; v += ls) { S.run_drop_node[v] = 0; S.max_usage[v] = 0.0; }
   for (int i = l0; i < N * Sd; i += ls) S.proc_traffic[i] = 0.0;
   for (int i = l0; i < N * C * Sd; i += ls) S.requested[i] = 0.0;
-  for (int i = l0; i < N * C * Sd * N; i += ls) S.wrr[i] = 0;
+  if constexpr (BIG) {
+    const int ep = S.wrr_ep[wrr_rows(S.d)] + 1;  // every lane reads, then writes, the same value
+    lanes_sync(ls);
+    S.wrr_ep[wrr_rows(S.d)] = ep;
+  } else {
+    for (int i = l0; i < N * C * Sd * N; i += ls) S.wrr[i] = 0;
+  }
   lanes_sync(ls);
   (void)K; (void)n;
 }
@@ -656,7 +675,8 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
   const int sf = GSC_UNI(K.chain[sfc * kMaxF + GSC_UNI(f.pos)]);
   S.flows[fid].cur_sf = (int16_t)sf;
   S.requested[(node * C + sfc) * Sd + sf] += f.dr;
-  const int row = ((node * C + sfc) * Sd + sf) * N;
+  const int rid = (node * C + sfc) * Sd + sf;
+  const int row = rid * N;
   const double* p = S.sched + row;
   int32_t* cnt = S.wrr + row;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -666,34 +686,50 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
   double lbest = -1e300;
   int lidx = 0x7fffffff;
   if constexpr (BIG) {
-    if (n <= 256) {
-      int c4[4];
-      double p4[4];
+    // weights straight from this step's action block (float -> double is exact: the same values as the
+    // host path's double schedule table); counters of a row not yet used in this run window are stale
+    // (zero): the row is zeroed now and tagged with the window's epoch (reset_run_metrics<BIG>)
+    const float* pa = S.act + ((long)(node * K.C + sfc) * K.F + sf) * K.n_pad;
+    const int ep = S.wrr_ep[wrr_rows(S.d)];
+    const bool stale = GSC_UNI(S.wrr_ep[rid] != ep);
+    int c4[4];  // n <= 256 (SimContext checks N <= 256): four destinations per lane
+    double p4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = lane + 64 * j;
+      const bool in = d < n;
+      c4[j] = in ? cnt[d] : 0;
+      p4[j] = in ? (double)pa[d] : 0.0;
+    }
+    if (stale) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int d = lane + 64 * j;
-        const bool in = d < n;
-        c4[j] = in ? cnt[d] : 0;
-        p4[j] = in ? p[d] : 0.0;
-      }
-      const int total = wave_sum_i32(c4[0] + c4[1] + c4[2] + c4[3]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int d = lane + 64 * j;
-        const double ratio = total > 0 ? (double)c4[j] / (double)total : 0.0;
-        const double diff = p4[j] > 0 ? p4[j] - ratio : -1.0;
-        if (d < n && diff > lbest) { lbest = diff; lidx = d; }
-      }
-    } else {
-      int part = 0;
-      for (int d = lane; d < n; d += 64) part += cnt[d];
-      const int total = wave_sum_i32(part);
-      for (int d = lane; d < n; d += 64) {
-        const double ratio = total > 0 ? (double)cnt[d] / (double)total : 0.0;
-        const double diff = p[d] > 0 ? p[d] - ratio : -1.0;
-        if (diff > lbest) { lbest = diff; lidx = d; }
+        c4[j] = 0;
+        if (lane + 64 * j < n) cnt[lane + 64 * j] = 0;
       }
     }
+    const int total = wave_sum_i32(c4[0] + c4[1] + c4[2] + c4[3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = lane + 64 * j;
+      const double ratio = total > 0 ? (double)c4[j] / (double)total : 0.0;
+      const double diff = p4[j] > 0 ? p4[j] - ratio : -1.0;
+      if (d < n && diff > lbest) { lbest = diff; lidx = d; }
+    }
+    const double best_v = wave_max_f64(lbest);
+    const uint32_t cand = lbest == best_v ? (uint32_t)lidx : 0x7fffffffu;
+    const int best = GSC_UNI((int)dpp_red_u32(cand, 0x7fffffffu, [](uint32_t a, uint32_t b) { return a < b ? a : b; }));
+    // the chosen counter from the lane that loaded it (no re-read after the zeroing stores)
+    int cb = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (lane + 64 * j == best) cb = c4[j];
+    const int old = GSC_UNI(__builtin_amdgcn_readlane(cb, best & 63));
+    __builtin_amdgcn_wave_barrier();
+    cnt[best] = old + 1;
+    if (stale) S.wrr_ep[rid] = ep;
+    proc_return(S, pid, P, (int16_t)best);
+    return;
   } else {
     int part = 0;
     for (int d = lane; d < n; d += 64) part += cnt[d];
@@ -958,6 +994,7 @@ GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pi
 }
 
 // ResultWriter.begin_writing / write_network_state: the run-window clock.
+template <bool BIG = false>
 GSC_HD_CALL void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P) {
   switch (GSC_UNI(P.state)) {
     case W_BEGIN:
@@ -966,7 +1003,7 @@ GSC_HD_CALL void run_writer(Env& S, const SimConst& K, const TopoDev& T, int pid
       return;
     default:  // W_INIT
 #if defined(__HIP_DEVICE_COMPILE__)
-      reset_run_metrics(S, K, T.n, wave_lane(), 64);
+      reset_run_metrics<BIG>(S, K, T.n, wave_lane(), 64);
 #else
       reset_run_metrics(S, K, T.n, 0, 1);
 #endif
@@ -1048,7 +1085,7 @@ GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid, int f
     case P_REQUEST: run_request(S, K, pid, P, f); break;
     case P_FINISH: run_finish(S, K, pid, P, f); break;
     case P_ARRIVAL: run_arrival(S, K, T, pid, P); break;
-    case P_WRITER: run_writer(S, K, T, pid, P); break;
+    case P_WRITER: run_writer<BIG>(S, K, T, pid, P); break;
     case P_MMPP: run_mmpp(S, K, T, pid); break;
     case P_TRACE: run_trace(S, K, T, pid); break;
     default: S.h->flags |= FLAG_BAD_STATE; break;
@@ -1074,6 +1111,9 @@ GSC_HD void remove_event(Env& S, int idx) {
 // ------------------------------------------------------------------------------------------------
 // Episode init / controller apply / observation + reward epilogue
 // ------------------------------------------------------------------------------------------------
+// BIG: device kernels with HBM-resident [N, C, S, N] tables -- the schedule table is not used there
+// (decisions read the action block) and the WRR counters are reset lazily (reset_run_metrics<BIG>)
+template <bool BIG = false>
 GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo, uint32_t seed, int episode,
                           int l0 = 0, int ls = 1) {
   Header* h = S.h;
@@ -1097,7 +1137,8 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
   }
   for (int i = l0; i < N * Sd; i += ls) { S.sf_present[i] = 0; S.placement[i] = 0; S.sf_load[i] = 0; S.sf_start[i] = 0; }
   for (int i = l0; i < N * (Sd + 1); i += ls) S.drop_locs[i] = 0;
-  for (int i = l0; i < N * C * Sd * N; i += ls) S.sched[i] = 0.0;
+  if constexpr (!BIG)
+    for (int i = l0; i < N * C * Sd * N; i += ls) S.sched[i] = 0.0;
   for (int e = l0; e < S.d.E; e += ls) {
     S.link_rem[e] = e < T.E ? T.edge_cap[e] : 0.0;
     S.link_passed[e] = 0.0;
@@ -1108,7 +1149,7 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
   h->proc_top = S.d.proc_cap;
   h->proc_head = S.d.proc_cap > 0 ? 0 : -1;  // == proc_free[proc_cap - 1]
   for (int i = l0; i < S.d.proc_cap; i += ls) { S.proc_free[i] = (int16_t)(S.d.proc_cap - 1 - i); S.procs[i].type = P_FREE; }
-  reset_run_metrics(S, K, n, l0, ls);  // ends with lanes_sync
+  reset_run_metrics<BIG>(S, K, n, l0, ls);  // ends with lanes_sync
   // reference order: writer, (MMPP), (trace), arrivals; then one env.step()
   spawn(S, P_WRITER, W_BEGIN, -1, -1);
   if (K.use_states) {
@@ -1130,7 +1171,7 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
   const Event ev = S.events[idx];
   remove_event(S, idx);
   h->now = ev.t;
-  if (ev.proc >= 0) dispatch(S, K, T, ev.proc, ev.flow);
+  if (ev.proc >= 0) dispatch<BIG>(S, K, T, ev.proc, ev.flow);
 }
 
 // SimulatorWrapper.apply (placement derivation) + DurationController.get_next_state prologue.
@@ -1145,7 +1186,7 @@ GSC_HD_CALL void controller_prologue(Env& S, const SimConst& K, const TopoDev& T
     const int lane = wave_lane();
     for (int i = lane; i < N * Sd; i += 64) S.placement[i] = 0;
     lanes_sync(64);
-    const bool masks = BIG && n > 64 && pmask_rows(S.d) > 0;  // row bitsets written by load_action
+    const bool masks = BIG && n > 64 && pmask_rows(S.d) > 0;  // row bitsets written by sim_pmask_kernel
     for (int c = 0; c < K.C; ++c) {
       uint64_t f[4] = {0, 0, 0, 0};  // node bitset (n <= 256)
       for (int i = 0; i < T.n_ing; ++i) {
@@ -1188,9 +1229,10 @@ GSC_HD_CALL void controller_prologue(Env& S, const SimConst& K, const TopoDev& T
         for (int src = 0; src < n; ++src) {
           if (!((f[src >> 6] >> (src & 63)) & 1)) continue;
           const double* row = S.sched + ((src * C + c) * Sd + sf) * N;
+          const float* arow = BIG ? S.act + ((long)(src * K.C + c) * K.F + sf) * K.n_pad : nullptr;
           for (int d0 = 0; d0 < n; d0 += 64) {
             const int dst = d0 + lane;
-            const bool pos = dst < n && row[dst] > 0;
+            const bool pos = dst < n && (BIG ? arow[dst] > 0.f : row[dst] > 0);
             if (pos) S.placement[dst * Sd + sf] = 1;
             nf[d0 >> 6] |= (uint64_t)__ballot(pos);
           }
@@ -1390,49 +1432,9 @@ template <bool BIG = false>
 GSC_HD void load_action(Env& S, const SimConst& K, const TopoDev& T, const float* act, int lane, int nlanes) {
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n, P = K.n_pad;
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (BIG) {
-    if (n > 16 && nlanes == 64) {
-      const bool masks = pmask_rows(S.d) > 0;
-      // schedule rows with the destinations over the lanes (no index divisions), kG rows per pass with
-      // all their loads in flight before the first use (one HBM round trip per pass, not per row); each
-      // row's positive destinations' bitset from the same pass's ballots
-      constexpr int kG = 8;
-      const int rows = n * C * Sd;
-      int src = 0, c = 0, sf = 0;
-      for (int r0 = 0; r0 < rows; r0 += kG) {
-        float v[kG][4];
-        int ra[kG], rs[kG];
-#pragma unroll
-        for (int g = 0; g < kG; ++g) {
-          ra[g] = (src * K.C + c) * K.F + sf;  // action row / schedule row of row r0 + g
-          rs[g] = (src * C + c) * Sd + sf;
-          if (++sf == Sd) { sf = 0; if (++c == C) { c = 0; ++src; } }
-        }
-#pragma unroll
-        for (int g = 0; g < kG; ++g)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int dst = 64 * q + lane;
-            v[g][q] = (r0 + g < rows && dst < n) ? act[(long)ra[g] * P + dst] : 0.f;
-          }
-#pragma unroll
-        for (int g = 0; g < kG; ++g) {
-          if (r0 + g >= rows) break;
-          double* srow = S.sched + (long)rs[g] * N;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int dst = 64 * q + lane;
-            if (dst < n) srow[dst] = (double)v[g][q];
-            if (masks) {
-              const uint64_t b = (uint64_t)__ballot(v[g][q] > 0.f);
-              if (lane == q) S.pmask[4L * rs[g] + q] = b;
-            }
-          }
-        }
-      }
-      return;
-    }
-  }
+  // BIG (HBM-resident tables): nothing to copy -- decisions and the placement walk read the action block
+  // itself (Env::act) and the destination bitsets of large topologies come from sim_pmask_kernel
+  if constexpr (BIG) return;
 #endif
   const int total = n * C * Sd * n;
   for (int i = lane; i < total; i += nlanes) {

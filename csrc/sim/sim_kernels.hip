@@ -311,6 +311,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   // (measured: header in LDS instead = 2.83 vs 2.30 ms/step for 256 Abilene envs)
   Header h_reg = *h_mem;
   S.h = &h_reg;
+  if constexpr (BIG) S.act = a.actions + (long)env * a.action_stride;  // read in place of the schedule table
   const TopoDev T = a.topo_stage ? stage_topo(a.topos[S.h->topo], topo_lds, lane, a.stage_pedges)
                                  : a.topos[S.h->topo];
   load_action<BIG>(S, K, T, a.actions + (long)env * a.action_stride, lane, 64);
@@ -453,7 +454,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
     {  // every lane (wave-uniform header copies), init loops spread over the lanes
       const int topo = a.topo_next[env];
       if (a.topo_cur && lane == 0) a.topo_cur[env] = topo;
-      env_init(S, K, a.topos[topo], topo, a.seeds[env], S.h->episode + 1, lane, 64);
+      env_init<BIG>(S, K, a.topos[topo], topo, a.seeds[env], S.h->episode + 1, lane, 64);
     }
     __syncthreads();
     write_obs_wave(S, K, a.topos[a.topo_next[env]].n, a.obs + env * ostride, nullptr, lane);
@@ -516,6 +517,31 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
     a.prof_types[((long)env * 64 + 58) * 2 + 1] += 1;
     a.prof_types[((long)env * 64 + 59) * 2] += __builtin_amdgcn_s_memrealtime() - r_begin;
     a.prof_types[((long)env * 64 + 59) * 2 + 1] += 1;
+  }
+}
+
+// Positive-destination bitsets of every schedule row of this step's action block, for the placement walk of
+// topologies beyond 64 nodes (controller_prologue<BIG>): one wave per (env, row) over the whole device,
+// ahead of the step kernel (one HBM pass over the action block instead of a serial walk per env wave).
+__global__ __launch_bounds__(256) void sim_pmask_kernel(SimArgs a) {
+  const int env = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
+  char* g = a.states + (long)env * a.state_bytes;
+  const int n = a.topos[reinterpret_cast<const Header*>(g + a.L.hdr)->topo].n;  // topology of this step
+  const int C = a.D.C, Sd = a.D.S;
+  if (r >= n * C * Sd) return;
+  const int sf = r % Sd, c = (r / Sd) % C, src = r / (Sd * C);
+  if (sf >= a.K.F) return;  // not an action row (no chain position uses it)
+  const float* row = a.actions + (long)env * a.action_stride + ((long)(src * a.K.C + c) * a.K.F + sf) * a.K.n_pad;
+  uint64_t* pm = reinterpret_cast<uint64_t*>(g + a.L.pmask) + 4L * r;
+  float v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = 64 * q + lane < n ? row[64 * q + lane] : 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint64_t b = (uint64_t)__ballot(v[q] > 0.f);
+    if (lane == q) pm[q] = b;
   }
 }
 
@@ -689,6 +715,10 @@ class SimContext {
     if (device_) {
       const size_t lds = (size_t)lds_per_env();
       const hipStream_t st = stream_of(stream);
+      if (lds_mode_ != 1 && pmask_rows(D_) > 0) {  // HBM-resident tables (BIG kernels), > 64 nodes
+        hipLaunchKernelGGL(sim_pmask_kernel, dim3(E, (pmask_rows(D_) + 3) / 4), dim3(256), 0, st, a);
+        check_launch();
+      }
 #define GSC_LAUNCH_SIM(QS)                                                                                     \
   if (lds_mode_ == 1 && a.prof) hipLaunchKernelGGL((sim_step_kernel<QS, 1, true>), dim3(E), dim3(64), lds, st, a); \
   else if (lds_mode_ == 1) hipLaunchKernelGGL((sim_step_kernel<QS, 1>), dim3(E), dim3(64), lds, st, a);           \

@@ -42,7 +42,11 @@ _DIAG_NO_LEARN = os.environ.get("GSC_DIAG_NO_LEARN", "0") == "1"
 
 class DDPGLearner:
     def __init__(self, cfg: dict, obs_dim: int, action_dim: int, graphs: GraphSet, C: int, F_: int, device,
-                 dist_info: Optional[DistInfo] = None, amp_bf16: Optional[bool] = None, seed: int = 0):
+                 dist_info: Optional[DistInfo] = None, amp_bf16: Optional[bool] = None, seed: int = 0,
+                 zero: Optional[bool] = None):
+        """``zero``: data parallel with sharded optimizer state (reduce-scatter -> Adam on 1/W -> all-gather,
+        :mod:`gsc_amd.parallel.zero`); None = ``GSC_DP_ZERO`` (0/1), else on from 32 M parameters
+        (config-5 scale) -- the single flat all-reduce stays for small (latency-bound) networks."""
         self.cfg = cfg
         self.device = torch.device(device)
         self.graphs = graphs
@@ -52,10 +56,16 @@ class DDPGLearner:
         self.critic = QNetwork(cfg, obs_dim, action_dim).to(self.device)
         self.target_actor = copy.deepcopy(self.actor)
         self.target_critic = copy.deepcopy(self.critic)
-        self.actor_flat = FlatParams(self.actor)
-        self.critic_flat = FlatParams(self.critic)
-        self.target_actor_flat = FlatParams(self.target_actor)
-        self.target_critic_flat = FlatParams(self.target_critic)
+        if zero is None:
+            env = os.environ.get("GSC_DP_ZERO")
+            nparam = sum(p.numel() for p in self.actor.parameters()) + sum(p.numel() for p in self.critic.parameters())
+            zero = (env == "1") if env is not None else nparam >= 32_000_000
+        self.zero = bool(zero and self.dist.enabled)
+        ba = 8 * self.dist.world_size if self.zero else 0   # equal shards per bucket
+        self.actor_flat = FlatParams(self.actor, bucket_align=ba)
+        self.critic_flat = FlatParams(self.critic, bucket_align=ba)
+        self.target_actor_flat = FlatParams(self.target_actor, bucket_align=ba)
+        self.target_critic_flat = FlatParams(self.target_critic, bucket_align=ba)
         for m in (self.target_actor, self.target_critic):
             for p in m.parameters():
                 p.requires_grad_(False)
@@ -69,6 +79,14 @@ class DDPGLearner:
         self.gamma = float(cfg.get("gamma", 0.99))
         self.critic_opt = FusedAdamPolyak(self.critic_flat, lr=lr, target=self.target_critic_flat, tau=tau)
         self.actor_opt = FusedAdamPolyak(self.actor_flat, lr=lr, target=self.target_actor_flat, tau=tau)
+        if self.zero:
+            from gsc_amd.parallel.zero import ZeroShards, bucket_bounds
+            r, w = self.dist.rank, self.dist.world_size
+            # actor: [embedder | MLP] buckets (the MLP bucket is reduced while the embedder backward runs);
+            # critic: one bucket (all its gradients exist at once)
+            self.actor_opt.enable_zero(ZeroShards(bucket_bounds(self.actor_flat.flat.numel(), self.actor_flat.split),
+                                                  r, w))
+            self.critic_opt.enable_zero(ZeroShards(bucket_bounds(self.critic_flat.flat.numel(), 0), r, w))
         self.masks = graphs.action_masks(C, F_)
         self.amp = (self.device.type == "cuda") if amp_bf16 is None else bool(amp_bf16)
         if self.amp and self.device.type == "cuda":
@@ -207,6 +225,21 @@ class DDPGLearner:
         """``run``: five callables (critic grads | actor fwd | critic step + actor MLP grads | actor
         embedder bwd | actor step) with the gradient all-reduces issued between them."""
         r1, r2, r3, r3b, r4 = run
+        if self.zero:  # reduce-scatters instead of all-reduces (the optimizer steps all-gather the params)
+            r1()
+            hs = self.critic_opt.reduce_grads()
+            r2()
+            for h in hs:
+                h.wait()
+            r3()
+            two = len(self.actor_opt.zero.buckets) == 2
+            hs = self.actor_opt.reduce_grads(bucket=1) if (split and two) else []
+            r3b()
+            hs += self.actor_opt.reduce_grads(bucket=0) if (split and two) else self.actor_opt.reduce_grads()
+            for h in hs:
+                h.wait()
+            r4()
+            return
         r1()
         h_c = self._allreduce(self.critic_flat)
         r2()
@@ -277,6 +310,13 @@ class DDPGLearner:
         :meth:`topo32_buffer`."""
         inv_world = 1.0 / self.dist.world_size
         self._topo_ready = bool(topo_ready and pre is not None)
+        if self.zero:
+            # the sharded optimizer step issues collectives between its kernels: eager (an update at the
+            # scale that enables it runs for milliseconds; launch overhead is noise there)
+            if pre is not None:
+                pre()
+            self.update(b)
+            return
         if self._graphs is None:
             if self._graph_warm < warmup:
                 s = torch.cuda.Stream(self.device)
@@ -639,13 +679,28 @@ class BatchedTrainer:
         for _ in range(self.t.updates_per_step):
             if self.graphed:
                 if self._batch is None:
-                    self._batch = self.replay.empty_batch(self.batch_size)
-                    B, out = self.batch_size, self._batch
+                    B = self.batch_size
+                    fused = self.fused_action_gather()
+                    self._batch = self.replay.empty_batch(B, actions=not fused)
+                    out = self._batch
+                    if fused:  # the critic's action GEMMs read the sampled ring rows in place
+                        self.learner.native_update(B).act_rows = self.replay.indices(B)
                     sink = self._topo_sink = self.learner.topo32_buffer(B)
-                    self._sampler = lambda: self.replay.sample(B, out=out, topo32=sink)
+                    self._sampler = lambda: self.replay.sample(B, out=out, topo32=sink, actions=not fused)
                 self.learner.update_graphed(self._batch, pre=self._sampler, topo_ready=self._topo_sink is not None)
             else:
                 self.learner.update(self.replay.sample(self.batch_size))
+
+    def fused_action_gather(self) -> bool:
+        """Replayed actions read in place by the native learner's GEMMs (row-indexed operands) instead of
+        gathered into a [B, A] batch: on by default once that batch copy exceeds 256 MB (50/200-node
+        topologies: 1.2 / 18 GB at B = 25,600); GSC_FUSED_GATHER=0/1 forces it."""
+        if not (self.learner.native_ok and self.replay.actions.dtype == torch.bfloat16):
+            return False
+        env = os.environ.get("GSC_FUSED_GATHER")
+        if env is not None:
+            return env == "1"
+        return self.batch_size * self.replay.action_cols * 2 > (256 << 20)
 
     def metrics(self, reset: bool = True) -> dict:
         self.flush()

@@ -193,6 +193,9 @@ class NativeDDPGUpdate:
         self.gnn_partials = torch.empty(self.gnn_rows, ne, device=dev, dtype=F32)
         self.gnn_grad = mk(ne)
         self.topo32 = torch.zeros(B, dtype=torch.int32, device=dev)
+        # replayed actions read in place from the ring: ``b.actions`` is then the ring and these are the
+        # sampled rows (DeviceReplay.sample(actions=False)); None: ``b.actions`` is the gathered [B, A] batch
+        self.act_rows: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------------------------------------
     def _stream(self) -> int:
@@ -249,16 +252,18 @@ class NativeDDPGUpdate:
                         colmask.data_ptr() if colmask is not None else 0, self._stream())
         return dst[:, :A]
 
-    def _first(self, net: _Net, emb, rowtab, out16, extra=None, wa=None, extra_rowtab=None, acc_ready=False):
+    def _first(self, net: _Net, emb, rowtab, out16, extra=None, wa=None, extra_rowtab=None, acc_ready=False,
+               extra_rows=None):
         """h0 = relu(emb W_d^T + b + rowtab[topo] (+ extra wa^T + extra_rowtab[topo])) -> out16.
-        ``acc_ready``: ``hacc`` already holds the action projection (fused target path)."""
+        ``acc_ready``: ``hacc`` already holds the action projection (fused target path).  ``extra_rows``:
+        row r of ``extra`` is its physical row extra_rows[r] (replay ring read in place)."""
         h0 = net.width(0)
         acc = acc_ready
         if extra is not None:
             if extra_rowtab is not None:
                 gemm(extra, wa, "nt", out32=self.hacc[:, :h0], rowtab=extra_rowtab, topo=self.topo32)
             else:   # K = A: split-K when the [B, h0] output alone gives few workgroups (large A)
-                gemm(extra, wa, "nt", out32=self.hacc[:, :h0], splits=None, slabs=self.slabs)
+                gemm(extra, wa, "nt", out32=self.hacc[:, :h0], splits=None, slabs=self.slabs, a_rows=extra_rows)
             acc = True
         gemm(emb, net.w16(0)[:, :self.H], "nt", out16=out16, bias=net.b32(0), rowtab=rowtab, topo=self.topo32,
              relu=True, accumulate=acc, out32=self.hacc[:, :h0] if acc else None)
@@ -282,7 +287,7 @@ class NativeDDPGUpdate:
             dh = nxt
         return dh
 
-    def _first_bwd(self, net: _Net, emb, dh0, extra=None) -> None:
+    def _first_bwd(self, net: _Net, emb, dh0, extra=None, extra_rows=None) -> None:
         """Gradients of the first layer (dense, bias, mask block, optional action block) + d emb."""
         H, A, T = self.H, self.A, self.T
         h0 = net.width(0)
@@ -292,7 +297,7 @@ class NativeDDPGUpdate:
         self.nat.first_layer_grad(aug.data_ptr(), h0, H, T, A, self.masks.data_ptr(), self.masks.stride(0),
                                   gw.data_ptr(), gw.stride(0), net.gb(0).data_ptr(), self._stream())
         if extra is not None:
-            gemm(dh0, extra, "tn", out32=gw[:, H + A:], splits=self.splits, slabs=self.slabs)
+            gemm(dh0, extra, "tn", out32=gw[:, H + A:], splits=self.splits, slabs=self.slabs, b_rows=extra_rows)
         gemm(dh0, net.w16(0)[:, :H], "nn", out32=self.demb)
 
     def _critic_tail(self, net: _Net, acts, mode: int, dh_out: Optional[torch.Tensor], b) -> None:
@@ -353,14 +358,16 @@ class NativeDDPGUpdate:
         # critic on (s, a): loss + gradients
         self._gnn_fwd(c, b.obs, self.emb["c"], self.blob["c"], key="c")
         acts = b.actions[:, :A]   # replay rows are padded to 8 columns (16-byte aligned)
-        self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], extra=acts, wa=self._wa(c, "c"))
+        rows = self.act_rows      # the ring itself, addressed by the sampled rows (no [B, A] batch copy)
+        self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], extra=acts, wa=self._wa(c, "c"),
+                    extra_rows=rows)
         self._hidden_fwd(c, self.hid_c)
         C = c.width(c.nh - 1)
         dh = self.dh[0][:, :C]
         self._critic_tail(c, self.hid_c, 1, dh, b)
         self._head_reduce(c, C, 1)
         dh0 = self._hidden_bwd(c, self.hid_c, dh, grads=True)
-        self._first_bwd(c, self.emb["c"], dh0, extra=acts)
+        self._first_bwd(c, self.emb["c"], dh0, extra=acts, extra_rows=rows)
         self._gnn_bwd(c, b.obs, self.demb, self.blob["c"], key="c")
 
     def stage_actor_fwd(self, b) -> None:

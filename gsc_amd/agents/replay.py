@@ -107,21 +107,33 @@ class DeviceReplay:
         self.pos = new % self.capacity
 
     @torch.no_grad()
-    def sample(self, batch_size: int, out: Optional[Batch] = None, topo32: Optional[torch.Tensor] = None) -> Batch:
-        """Uniform sample (reference buffer.py:56-62); with ``out`` the rows are gathered into those
-        (static) buffers -- graph-capturable.  ``topo32`` (int32 [B]) also receives the sampled
-        topology ids (the native learner's kernels take int32)."""
-        if len(self) == 0:
-            raise RuntimeError("cannot sample from an empty replay buffer")
+    def indices(self, batch_size: int) -> torch.Tensor:
+        """The (static) int32 row-index buffer a sample of ``batch_size`` writes."""
         B = int(batch_size)
         idx = self._idx.get(B)
         if idx is None:
             idx = self._idx[B] = torch.empty(B, dtype=torch.int32, device=self.device)
+        return idx
+
+    def sample(self, batch_size: int, out: Optional[Batch] = None, topo32: Optional[torch.Tensor] = None,
+               actions: bool = True) -> Batch:
+        """Uniform sample (reference buffer.py:56-62); with ``out`` the rows are gathered into those
+        (static) buffers -- graph-capturable.  ``topo32`` (int32 [B]) also receives the sampled
+        topology ids (the native learner's kernels take int32).  ``actions=False``: the action column is
+        not gathered -- the native learner reads the sampled ring rows in place through
+        :meth:`indices` (row-indexed GEMM operands); ``out.actions`` is then the ring itself."""
+        if len(self) == 0:
+            raise RuntimeError("cannot sample from an empty replay buffer")
+        B = int(batch_size)
+        idx = self.indices(B)
         if out is None:
-            out = self.empty_batch(B)
+            out = self.empty_batch(B, actions=actions)
         nat, s, dev = self.nat, self._stream(), self.is_dev
         cols = []
         for src, dst in zip((self.obs, self.topo, self.actions, self.rewards, self.next_obs, self.dones), out):
+            if src is self.actions and not actions:
+                assert dst is self.actions
+                continue
             assert dst.is_contiguous() and dst.shape[0] == B and dst.dtype == src.dtype
             cols.append((src.data_ptr(), dst.data_ptr(), src[0].numel() * src.element_size(), 0))
         if topo32 is not None:
@@ -134,11 +146,12 @@ class DeviceReplay:
     def last_indices(self, batch_size: int) -> torch.Tensor:
         return self._idx[int(batch_size)]
 
-    def empty_batch(self, batch_size: int) -> Batch:
-        """Static batch buffers (for :meth:`sample` ``out=`` and HIP-graph replay)."""
+    def empty_batch(self, batch_size: int, actions: bool = True) -> Batch:
+        """Static batch buffers (for :meth:`sample` ``out=`` and HIP-graph replay); ``actions=False``: the
+        batch's action slot is the ring itself (rows addressed through :meth:`indices`)."""
         mk = lambda t: torch.empty((batch_size,) + tuple(t.shape[1:]), dtype=t.dtype, device=self.device)
-        return Batch(mk(self.obs), mk(self.topo), mk(self.actions), mk(self.rewards), mk(self.next_obs),
-                     mk(self.dones))
+        return Batch(mk(self.obs), mk(self.topo), mk(self.actions) if actions else self.actions, mk(self.rewards),
+                     mk(self.next_obs), mk(self.dones))
 
     def rng_state(self) -> torch.Tensor:
         return torch.cat([self.state.cpu(), torch.tensor([self.seed], dtype=torch.int64)])

@@ -73,24 +73,33 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: str = "nt", *, out16: Optiona
          dsig: Optional[torch.Tensor] = None, gmul: Optional[torch.Tensor] = None,
          clamp=None, accumulate: bool = False, splits: Optional[int] = 1, slabs: Optional[torch.Tensor] = None,
          aug_t: int = -1, aug_topo: Optional[torch.Tensor] = None, tile: Optional[int] = None,
-         bk: Optional[int] = None, stream: Optional[int] = None) -> None:
+         bk: Optional[int] = None, stream: Optional[int] = None, a_rows: Optional[torch.Tensor] = None,
+         b_rows: Optional[torch.Tensor] = None) -> None:
     """See module docstring.  ``splits=None`` picks a split-K count (needs ``slabs``).  ``aug_t >= 0`` appends ``1 + aug_t`` virtual columns to ``b`` (layouts
-    tn/nn): a ones column and the one-hot of ``aug_topo`` (the row topology of ``b``)."""
+    tn/nn): a ones column and the one-hot of ``aug_topo`` (the row topology of ``b``).  ``a_rows`` / ``b_rows``
+    (int32): the operand's stored row r is its physical row ``rows[r]`` (a sampled batch read in place from the
+    replay ring); the logical row count is ``rows.numel()``."""
     nat = load_native()
     lay = LAYOUTS[layout]
+    ar = a_rows.numel() if a_rows is not None else a.shape[0]   # logical stored rows
+    br = b_rows.numel() if b_rows is not None else b.shape[0]
     if lay == 0:
-        M, K = a.shape
-        N = b.shape[0]
+        M, K = ar, a.shape[1]
+        N = br
         assert b.shape[1] == K
     elif lay == 1:
-        K, M = a.shape
+        K, M = ar, a.shape[1]
         N = b.shape[1]
-        assert b.shape[0] == K
+        assert br == K
     else:
-        M, K = a.shape
+        M, K = ar, a.shape[1]
         N = b.shape[1]
-        assert b.shape[0] == K
+        assert br == K
     ep = {"alpha": float(alpha)}
+    for nm, r in (("a_rows", a_rows), ("b_rows", b_rows)):
+        if r is not None:
+            assert r.dtype == torch.int32 and r.is_contiguous() and r.device == a.device
+            ep[nm] = r.data_ptr()
     if aug_t >= 0:
         assert lay in (1, 2) and aug_topo is not None
         ep.update(aug_n0=N, aug_t=int(aug_t), aug_topo=aug_topo.data_ptr())

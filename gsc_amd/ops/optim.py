@@ -16,22 +16,33 @@ import torch.nn as nn
 
 
 class FlatParams:
-    def __init__(self, module: nn.Module, align: int = 4, matrix_align: int = 8):
+    def __init__(self, module: nn.Module, align: int = 4, matrix_align: int = 8, bucket_align: int = 0):
+        """``bucket_align`` > 0 (sharded optimizer, :mod:`gsc_amd.parallel.zero`): the block after the
+        embedder and the buffer end start on multiples of it, so both buckets split into equal shards."""
         self.module = module
         named = list(module.named_parameters())
         self.params: List[nn.Parameter] = [p for _, p in named]
         self.names = [n for n, _ in named]
         total = 0
         self.offsets = []
+        self.split = 0  # first element after the embedder block (0: no embedder / no bucket split)
+        seen_emb = False
         for name, p in named:
+            emb = name.startswith("embedder.")
+            if bucket_align and seen_emb and not emb and not self.split:
+                total = -(-total // bucket_align) * bucket_align
+                self.split = total
+            seen_emb |= emb
             # MLP weight matrices start on a 16-byte boundary of the bf16 shadow (16-byte staging loads
             # in the MFMA GEMMs); the GNN block stays packed (its kernels index it as one run)
-            if p.dim() == 2 and not name.startswith("embedder."):
+            if p.dim() == 2 and not emb:
                 total = -(-total // matrix_align) * matrix_align
             self.offsets.append(total)
             total += p.numel()
         self.numel = total
         dev = self.params[0].device
+        if bucket_align:
+            align = bucket_align
         pad = (-total) % align
         self.flat = torch.zeros(total + pad, device=dev, dtype=torch.float32)
         for p, o in zip(self.params, self.offsets):
@@ -116,6 +127,100 @@ class FusedAdamPolyak:
         # untouched (device-side decision, no host sync, works inside captured HIP graphs)
         self.guard = torch.zeros(4, dtype=torch.int32, device=flat.flat.device)
         self.guard_enabled = os.environ.get("GSC_GRAD_GUARD", "1") != "0"
+        self.zero = None  # ZeroShards: sharded optimizer state (enable_zero)
+
+    # -- sharded optimizer (ZeRO-1, gsc_amd/parallel/zero.py) -----------------------------------------
+    def enable_zero(self, shards) -> None:
+        """Keep Adam moments for this rank's shards only; :meth:`reduce_grads` fills ``gshard`` and
+        :meth:`step` updates the shard, all-gathers the parameters and refreshes targets + shadows."""
+        dev = self.fp.flat.device
+        self.zero = shards
+        n = shards.local_numel
+        self.m = torch.zeros(n, device=dev)
+        self.v = torch.zeros(n, device=dev)
+        self.gshard = torch.zeros(n, device=dev)
+        self.zflag = torch.zeros(4, dtype=torch.int32, device=dev)
+
+    def reduce_grads(self, bucket: Optional[int] = None, async_op: bool = True):
+        """Reduce-scatter the flat gradient's bucket(s) into ``gshard``; returns waitable handles."""
+        from gsc_amd.parallel.zero import reduce_scatter_bucket
+        z = self.zero
+        out = []
+        for b in ([bucket] if bucket is not None else range(len(z.buckets))):
+            lo, hi = z.buckets[b]
+            off = z.local_off[b]
+            h = reduce_scatter_bucket(self.fp.grad, lo, hi, self.gshard[off:off + z.chunk(b)], z.world, z.rank,
+                                      async_op=async_op)
+            if h is not None:
+                out.append(h)
+        return out
+
+    def _zero_state(self, t: torch.Tensor) -> torch.Tensor:
+        """Full-length copy of a sharded state tensor (all-gathered; collective)."""
+        from gsc_amd.parallel.zero import all_gather_bucket
+        z = self.zero
+        full = torch.zeros_like(self.fp.flat)
+        for b in range(len(z.buckets)):
+            lo, hi = z.shard(b)
+            full[lo:hi].copy_(t[z.local_off[b]:z.local_off[b] + z.chunk(b)])
+            all_gather_bucket(full, *z.buckets[b], z.world, z.rank)
+        return full
+
+    def _zero_load(self, t: torch.Tensor, full: torch.Tensor) -> None:
+        z = self.zero
+        for b in range(len(z.buckets)):
+            lo, hi = z.shard(b)
+            t[z.local_off[b]:z.local_off[b] + z.chunk(b)].copy_(full[lo:hi])
+
+    @torch.no_grad()
+    def _step_zero(self, grad_scale: float) -> None:
+        from gsc_amd.parallel.zero import agree_any, all_gather_bucket
+        z = self.zero
+        p, t = self.fp.flat, (self.target.flat if self.target is not None else None)
+        g = self.gshard
+        if p.is_cuda:
+            from gsc_amd.native import load
+            nat = load()
+            stream = torch.cuda.current_stream(p.device).cuda_stream
+            skip = 0
+            if self.guard_enabled:
+                nat.grad_guard_local(g.data_ptr(), g.numel(), self.zflag.data_ptr(), stream)
+                agree_any(self.zflag)      # one decision on every rank (the shards differ)
+                nat.grad_guard_apply(self.zflag.data_ptr(), self.guard.data_ptr(), self.step_t.data_ptr(), stream)
+                skip = self.guard.data_ptr()
+            else:
+                self.step_t.add_(1)
+            for b in range(len(z.buckets)):
+                lo, hi = z.shard(b)
+                off = z.local_off[b]
+                nat.adam_polyak(p[lo:].data_ptr(), g[off:].data_ptr(), self.m[off:].data_ptr(), self.v[off:].data_ptr(),
+                                0, hi - lo, self.lr, self.betas[0], self.betas[1], self.eps, 1, 0.0, float(grad_scale),
+                                self.wd, stream, step_ptr=self.step_t.data_ptr(), skip_ptr=skip)
+            for b in range(len(z.buckets)):
+                all_gather_bucket(p, *z.buckets[b], z.world, z.rank)
+            f16 = self.fp.flat16
+            t16 = getattr(self.target, "flat16", None) if t is not None else None
+            nat.polyak_shadow(p.data_ptr(), t.data_ptr() if t is not None else 0, p.numel(),
+                              self.tau if t is not None else 0.0, f16.data_ptr() if f16 is not None else 0,
+                              t16.data_ptr() if t16 is not None else 0, skip, stream)
+            return
+        bad = torch.tensor([0 if bool(torch.isfinite(g).all()) else 1], dtype=torch.int32)
+        if self.guard_enabled:
+            agree_any(bad)
+        if int(bad[0]):
+            self.guard[1] += 1
+            return
+        self._host_step += 1
+        self.step_t.add_(1)
+        for b in range(len(z.buckets)):
+            lo, hi = z.shard(b)
+            off, c = z.local_off[b], z.chunk(b)
+            adam_polyak_reference(p[lo:hi], g[off:off + c] * grad_scale, self.m[off:off + c], self.v[off:off + c],
+                                  None, self._host_step, self.lr, self.betas, self.eps, 0.0, self.wd)
+        for b in range(len(z.buckets)):
+            all_gather_bucket(p, *z.buckets[b], z.world, z.rank)
+        if t is not None:
+            t.copy_(self.tau * p + (1 - self.tau) * t)
 
     @property
     def skipped_steps(self) -> int:
@@ -126,17 +231,25 @@ class FusedAdamPolyak:
         return int(self.step_t.item()) if self.step_t.is_cuda else self._host_step
 
     def state_dict(self) -> dict:
-        return {"m": self.m, "v": self.v, "step": self.step_count, "lr": self.lr, "betas": self.betas,
-                "eps": self.eps}
+        """Full-length moments (sharded: all-gathered -- a collective, every rank calls it)."""
+        m, v = (self._zero_state(self.m), self._zero_state(self.v)) if self.zero is not None else (self.m, self.v)
+        return {"m": m, "v": v, "step": self.step_count, "lr": self.lr, "betas": self.betas, "eps": self.eps}
 
     def load_state_dict(self, sd: dict) -> None:
-        self.m.copy_(sd["m"])
-        self.v.copy_(sd["v"])
+        if self.zero is not None:
+            self._zero_load(self.m, sd["m"].to(self.m.device))
+            self._zero_load(self.v, sd["v"].to(self.v.device))
+        else:
+            self.m.copy_(sd["m"])
+            self.v.copy_(sd["v"])
         self._host_step = int(sd["step"])
         self.step_t.fill_(int(sd["step"]))
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0) -> None:
+        if self.zero is not None:
+            self._step_zero(grad_scale)
+            return
         p, g = self.fp.flat, self.fp.grad
         t = self.target.flat if self.target is not None else None
         if p.is_cuda:

@@ -15,6 +15,9 @@ Rank 0 prints one JSON line:
                         actor-MLP all-reduce overlapping the embedder backward)
   param_mismatch_frac   fraction of parameters differing by > 1e-4 from that single process after 3 updates
   trainer_replicas_bitwise  same check after 6 batched-trainer steps (per-rank envs, shared learner)
+  zero_replicas_bitwise / zero_param_mismatch_frac  the sharded optimizer (ZeRO-1: reduce-scatter, Adam on
+                        1/W, all-gather; gsc_amd/parallel/zero.py) on the native GPU kernels: replicas and
+                        agreement with the single process after the same 3 updates
 """
 import json
 import os
@@ -103,6 +106,21 @@ def main():
         d = torch.cat([(a - b).abs().view(-1) for a, b in zip(flats(L), flats(ref))])
         res["param_mismatch_frac"] = float((d > 1e-4).float().mean())
         res["param_max_abs_diff"] = float(d.max())
+    # (c) sharded optimizer state (ZeRO-1) on the native kernels, same batches
+    Z = DDPGLearner(cfg, 3, 1728, gs, 1, 3, dev, info, seed=3 if r == 0 else 100 + r, zero=True)
+    for k, b in enumerate(full):
+        for d, s in zip(static, b):
+            d.copy_(s[r * Bp:(r + 1) * Bp])
+        Z.update_graphed(static, warmup=1)
+    torch.cuda.synchronize()
+    res["zero"] = bool(Z.zero)
+    res["zero_moment_frac"] = Z.actor_opt.m.numel() / Z.actor_flat.flat.numel()
+    res["zero_replicas_bitwise"] = bitwise_same(flats(Z), W)
+    if r == 0:
+        d = torch.cat([(getattr(Z, net).state_dict()[k] - v).abs().view(-1)
+                       for net in ("actor", "critic", "target_actor", "target_critic")
+                       for k, v in getattr(ref, net).state_dict().items()])
+        res["zero_param_mismatch_frac"] = float((d > 1e-4).float().mean())
     # (b) batched trainer: per-rank envs, replicated learner, HIP-graph updates
     sim = load_batched_from_paths([net], "configs/service_functions/abc.yaml",
                                   "configs/config/simulator/sample_config.yaml", cfg, 32, device=dev, seed=1000 + r)

@@ -35,12 +35,13 @@ def _cfg():
     return cfg
 
 
-def _learner(dist_info=None, seed=3):
+def _learner(dist_info=None, seed=3, zero=None):
     from gsc_amd.agents import DDPGLearner
     from gsc_amd.coordsim.reader import load_topology
     from gsc_amd.models import GraphSet
     gs = GraphSet([load_topology(ABILENE)], 24, "cpu")
-    return DDPGLearner(_cfg(), 3, 24 * 1 * 3 * 24, gs, 1, 3, "cpu", dist_info, amp_bf16=False, seed=seed), gs
+    return DDPGLearner(_cfg(), 3, 24 * 1 * 3 * 24, gs, 1, 3, "cpu", dist_info, amp_bf16=False, seed=seed,
+                       zero=zero), gs
 
 
 def _batches(n_updates):
@@ -112,6 +113,51 @@ def _trainer_worker(rank, port, out_dir):
                 "succ": torch.tensor(m["succ"]), "updates": torch.tensor(tr.learner.updates)},
                os.path.join(out_dir, f"t{rank}.pt"))
     shutdown()
+
+
+def _zero_worker(rank, port, out_dir, n_updates):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from gsc_amd.agents import Batch
+    from gsc_amd.parallel.dist import init_distributed, shutdown
+    info = init_distributed("cpu")
+    learner, _ = _learner(info, seed=3 if rank == 0 else 99, zero=True)
+    assert learner.zero and learner.actor_opt.zero is not None
+    assert learner.actor_opt.m.numel() * WORLD == learner.actor_flat.flat.numel()   # moments of 1/W only
+    for b in _batches(n_updates):
+        sl = slice(rank * B_PER_RANK, (rank + 1) * B_PER_RANK)
+        learner.update(Batch(*(t[sl] for t in b)))
+    opt = learner.actor_opt.state_dict()                       # collective: full-length moments
+    out = {f"{net}.{n}": p.detach().clone() for net in ("actor", "critic", "target_actor")
+           for n, p in getattr(learner, net).named_parameters()}
+    out["actor_m"] = opt["m"][:learner.actor_flat.numel].clone()
+    out["flat"] = learner.actor_flat.flat.clone()
+    torch.save(out, os.path.join(out_dir, f"z{rank}.pt"))
+    shutdown()
+
+
+def test_dp_sharded_optimizer_matches_single_process():
+    """ZeRO-1 (reduce-scatter -> Adam on the rank's 1/W shard -> all-gather; :mod:`gsc_amd.parallel.zero`):
+    replicas stay bit-identical across ranks and equal the single-process update on the concatenated
+    batch (fp32 tolerance); each rank holds Adam moments for 1/W of the parameters."""
+    n_updates = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_zero_worker, args=(_free_port(), d, n_updates), nprocs=WORLD, join=True,
+                           start_method="spawn")
+        r = [torch.load(os.path.join(d, f"z{i}.pt"), weights_only=True) for i in range(WORLD)]
+    assert torch.equal(r[0]["flat"], r[1]["flat"])
+    for k in r[0]:
+        assert torch.equal(r[0][k], r[1][k]), f"{k} differs across ranks"
+    ref, _ = _learner(None, seed=3)
+    for b in _batches(n_updates):
+        ref.update(b)
+    for net in ("actor", "critic", "target_actor"):
+        for n, p in getattr(ref, net).named_parameters():
+            torch.testing.assert_close(r[0][f"{net}.{n}"], p.detach(), rtol=1e-5, atol=1e-6)
+    from gsc_amd.ops.optim import FlatParams  # noqa: F401
+    torch.testing.assert_close(r[0]["actor_m"].norm(), ref.actor_opt.m[:ref.actor_flat.numel].norm(), rtol=1e-5,
+                               atol=1e-7)
 
 
 def test_dp_batched_trainer_replicas_identical():

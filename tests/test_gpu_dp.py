@@ -36,3 +36,6 @@ def test_two_ranks_one_gpu_graphed_dp():
     assert res["grad_vs_single"] < 1e-3 and res["grad_vs_single_graphed"] < 1e-3, res
     assert res["param_mismatch_frac"] < 1e-3, res
     assert res["trainer_graphed"] and res["trainer_updates"] >= 4 and res["envs_differ"]
+    # sharded optimizer (ZeRO-1) on the native kernels
+    assert res["zero"] and res["zero_replicas_bitwise"] and res["zero_moment_frac"] == 0.5
+    assert res["zero_param_mismatch_frac"] < 1e-3, res

@@ -214,3 +214,31 @@ def test_native_act_follows_graphed_updates():
         want = gpu.actor(obs.obs, obs.topo, gpu.graphs, gpu.masks).float()
     err = ((got - want).norm() / want.norm()).item()
     assert err < 0.02, err
+
+
+def test_native_update_reads_replay_rows_in_place():
+    """The critic's action GEMMs reading the sampled replay-ring rows in place (row-indexed operands,
+    DeviceReplay.sample(actions=False)) compute exactly the update of the gathered [B, A] batch."""
+    from gsc_amd.agents.replay import DeviceReplay
+    cfg = _cfg()
+    _, g1 = _learners(cfg, 2)
+    _, g2 = _learners(cfg, 2)
+    A = 24 * 3 * 24
+    rb = DeviceReplay(2000, 24, 3, A, "cuda", action_dtype=torch.bfloat16, seed=3, action_row_align=8)
+    src = _batch(1000, 2, "cpu", seed=9)
+    for k in range(2):
+        sl = slice(500 * k, 500 * (k + 1))
+        rb.add(src.obs[sl].cuda(), src.topo[sl].cuda(), src.actions[sl].cuda(), src.rewards[sl].cuda(),
+               src.next_obs[sl].cuda(), src.dones[sl].cuda())
+    B = 512
+    for _ in range(2):
+        b1 = rb.sample(B)                                        # gathered actions
+        rb.state[2] -= 1                                         # same Philox draw again
+        b2 = rb.sample(B, actions=False)                         # actions = the ring
+        assert b2.actions is rb.actions
+        g1.update(b1)
+        g2.native_update(B).act_rows = rb.indices(B)
+        g2.update(b2)
+    torch.cuda.synchronize()
+    for nm in ("critic_flat", "actor_flat", "target_critic_flat"):
+        assert torch.equal(getattr(g1, nm).flat, getattr(g2, nm).flat), nm

@@ -112,3 +112,32 @@ def test_gemm_large_random_vs_fp32():
     torch.cuda.synchronize()
     err = (out - ref).abs().max().item()
     assert err < 0.05 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("layout", ["nt", "tn"])
+def test_gemm_row_indexed_operand(layout):
+    """Row-indexed operands (replay-ring rows read in place): exactly the GEMM of the gathered rows --
+    nt with A rows indexed (the critic's action projection, split-K) and tn with B rows indexed (its
+    weight gradient, K = batch)."""
+    g = torch.Generator().manual_seed(7)
+    cap, A, B, c1 = 300, 1000, 130, 64
+    ring = _ints(cap, 1008, g=g).cuda().bfloat16()        # rows padded to 8 columns
+    rows = torch.randint(0, cap, (B,), generator=g).int().cuda()
+    gathered = ring[rows.long()][:, :A].contiguous()
+    slabs = torch.empty(1 << 22, device="cuda")
+    if layout == "nt":
+        w = _ints(c1, A, g=g).cuda().bfloat16()
+        want = torch.empty(B, c1, device="cuda")
+        got = torch.empty(B, c1, device="cuda")
+        gemm(gathered, w, "nt", out32=want, splits=4, slabs=slabs)
+        gemm(ring[:, :A], w, "nt", out32=got, splits=4, slabs=slabs, a_rows=rows)
+        assert torch.equal(got, want)
+        torch.testing.assert_close(got, gathered.float() @ w.float().t())
+    else:
+        dh = _ints(B, c1, g=g).cuda().bfloat16()
+        want = torch.empty(c1, A, device="cuda")
+        got = torch.empty(c1, A, device="cuda")
+        gemm(dh, gathered, "tn", out32=want)
+        gemm(dh, ring[:, :A], "tn", out32=got, b_rows=rows)
+        assert torch.equal(got, want)
+        torch.testing.assert_close(got, dh.float().t() @ gathered.float())
