@@ -76,10 +76,42 @@ __global__ __launch_bounds__(256) void explore_postprocess_lanes_kernel(const fl
   if (on) out[base + i] = (float)w;
 }
 
+// Sum over the wave, broadcast: DPP row shifts + row broadcasts (VALU latency) instead of six LDS-routed
+// shuffles; a fixed order, so every lane and every launch gets the same bits
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+#define GSC_DPP_ADDD(ctrl, rm)                                                           \
+  {                                                                                      \
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), ctrl, rm, 0xF, false); \
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), ctrl, rm, 0xF, false); \
+    v += __hiloint2double(hi, lo);                                                       \
+  }
+  GSC_DPP_ADDD(0x111, 0xF) GSC_DPP_ADDD(0x112, 0xF) GSC_DPP_ADDD(0x114, 0xF) GSC_DPP_ADDD(0x118, 0xF)
+  GSC_DPP_ADDD(0x142, 0xA) GSC_DPP_ADDD(0x143, 0xC)
+#undef GSC_DPP_ADDD
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63), __builtin_amdgcn_readlane(__double2loint(v), 63));
+}
+
+// Noisy (or warm-up uniform) weights i0, i0 + 1 of a slice from ONE Philox draw (the pair's two uniforms,
+// both Box-Muller outputs) -- explore_weight's values for both members of the pair.
+__device__ __forceinline__ void explore_pair(const float* __restrict__ mu, const float* __restrict__ mrow, long base,
+                                            int i0, int warmup, float rand_mu, float rand_sigma, uint32_t seed,
+                                            uint32_t step, float& w0, float& w1) {
+  const Philox4 r = philox4x32_10(seed, step, (uint64_t)(base + i0));
+  const float u0 = (float)(r.v[0] >> 8) * (1.0f / 16777216.0f);
+  const float u1 = (float)(r.v[1] >> 8) * (1.0f / 16777216.0f);
+  if (warmup) {
+    w0 = u0 * mrow[i0];
+    w1 = u1 * mrow[i0 + 1];
+    return;
+  }
+  const float rad = sqrtf(-2.0f * __logf(1.0f - u0));
+  float sn, cs;
+  __sincosf(6.283185307179586f * u1, &sn, &cs);
+  const float s0 = 2.0f * mu[base + i0] - 1.0f + rand_mu + rand_sigma * (rad * cs);
+  const float s1 = 2.0f * mu[base + i0 + 1] - 1.0f + rand_mu + rand_sigma * (rad * sn);
+  const float a0 = 0.5f * (s0 + 1.0f), a1 = 0.5f * (s1 + 1.0f);
+  w0 = a0 < 0.f ? 0.f : (a0 > 1.f ? 1.f : a0);
+  w1 = a1 < 0.f ? 0.f : (a1 > 1.f ? 1.f : a1);
 }
 
 // 32 < n_pad <= 256: one slice per wave, K <= 4 consecutive weights per lane (lane l holds weights
@@ -100,10 +132,22 @@ __global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const flo
   const long base = slice * P;
   const float* mrow = topo ? mask + topo[slice / R] * (long)A + (slice % R) * P : mask + base;
   double w[K];
+  if constexpr (K % 2 == 0) {  // K even: lanes own whole pairs (one Philox draw per pair)
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int i = K * lane + k;
-    w[k] = i < P ? (double)explore_weight(mu, mrow, base, i, warmup, rand_mu, rand_sigma, seed, step) : 0.0;
+    for (int k = 0; k < K; k += 2) {
+      const int i = K * lane + k;
+      float a = 0.f, b = 0.f;
+      if (i + 1 < P) explore_pair(mu, mrow, base, i, warmup, rand_mu, rand_sigma, seed, step, a, b);
+      else if (i < P) a = explore_weight(mu, mrow, base, i, warmup, rand_mu, rand_sigma, seed, step);  // odd P
+      w[k] = a;
+      w[k + 1] = b;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = K * lane + k;
+      w[k] = i < P ? (double)explore_weight(mu, mrow, base, i, warmup, rand_mu, rand_sigma, seed, step) : 0.0;
+    }
   }
   const double acc = 1.4901161193847656e-08;  // sqrt(float64 eps)
   const double uni = round10(1.0 / P);
@@ -164,7 +208,7 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t
     };
     if (P <= 64) go(explore_postprocess_wave_kernel<1>);
     else if (P <= 128) go(explore_postprocess_wave_kernel<2>);
-    else if (P <= 192) go(explore_postprocess_wave_kernel<3>);
+    else if (P <= 192 && P % 2 == 1) go(explore_postprocess_wave_kernel<3>);
     else go(explore_postprocess_wave_kernel<4>);
   }
   check_launch();

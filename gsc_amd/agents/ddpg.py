@@ -45,8 +45,10 @@ class DDPGLearner:
                  dist_info: Optional[DistInfo] = None, amp_bf16: Optional[bool] = None, seed: int = 0,
                  zero: Optional[bool] = None):
         """``zero``: data parallel with sharded optimizer state (reduce-scatter -> Adam on 1/W -> all-gather,
-        :mod:`gsc_amd.parallel.zero`); None = ``GSC_DP_ZERO`` (0/1), else on from 32 M parameters
-        (config-5 scale) -- the single flat all-reduce stays for small (latency-bound) networks."""
+        :mod:`gsc_amd.parallel.zero`); None = ``GSC_DP_ZERO=1``.  Off by default: the all-reduce path hides its
+        collectives behind the actor forward / embedder backward, while the sharded step exposes the
+        parameter all-gathers (docs/ARCHITECTURE.md, "Data parallelism": it trades ~2.7 ms of exposed
+        all-gather for ~0.8 ms of optimizer time and 1/W of the moments at config-5 scale, 8 ranks)."""
         self.cfg = cfg
         self.device = torch.device(device)
         self.graphs = graphs
@@ -57,9 +59,7 @@ class DDPGLearner:
         self.target_actor = copy.deepcopy(self.actor)
         self.target_critic = copy.deepcopy(self.critic)
         if zero is None:
-            env = os.environ.get("GSC_DP_ZERO")
-            nparam = sum(p.numel() for p in self.actor.parameters()) + sum(p.numel() for p in self.critic.parameters())
-            zero = (env == "1") if env is not None else nparam >= 32_000_000
+            zero = os.environ.get("GSC_DP_ZERO", "0") == "1"
         self.zero = bool(zero and self.dist.enabled)
         ba = 8 * self.dist.world_size if self.zero else 0   # equal shards per bucket
         self.actor_flat = FlatParams(self.actor, bucket_align=ba)

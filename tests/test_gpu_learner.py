@@ -40,14 +40,17 @@ def _batch(B, T, device, seed=11, P=24):
     return Batch(*(t.to(device) for t in b[:2]), b.actions.to(device).bfloat16(), *(t.to(device) for t in b[3:]))
 
 
-def _learners(cfg, T, P=24):
+def _learners(cfg, T, P=24, nets=None, C=1):
     from gsc_amd.agents import DDPGLearner
     from gsc_amd.coordsim.reader import load_topology
     from gsc_amd.models import GraphSet
-    topos = [load_topology(ABILENE)] * T if T < 3 else [load_topology(p) for p in THREE]
-    A = P * 3 * P
-    ref = DDPGLearner(cfg, 3, A, GraphSet(topos, P, "cpu"), 1, 3, "cpu", amp_bf16=False, seed=3)
-    gpu = DDPGLearner(cfg, 3, A, GraphSet(topos, P, "cuda"), 1, 3, "cuda", seed=3)
+    if nets is not None:
+        topos = [load_topology(p) for p in nets]
+    else:
+        topos = [load_topology(ABILENE)] * T if T < 3 else [load_topology(p) for p in THREE]
+    A = P * C * 3 * P
+    ref = DDPGLearner(cfg, 3, A, GraphSet(topos, P, "cpu"), C, 3, "cpu", amp_bf16=False, seed=3)
+    gpu = DDPGLearner(cfg, 3, A, GraphSet(topos, P, "cuda"), C, 3, "cuda", seed=3)
     assert gpu.native_ok
     assert torch.equal(ref.actor_flat.flat, gpu.actor_flat.flat.cpu())
     return ref, gpu
@@ -242,3 +245,44 @@ def test_native_update_reads_replay_rows_in_place():
     torch.cuda.synchronize()
     for nm in ("critic_flat", "actor_flat", "target_critic_flat"):
         assert torch.equal(getattr(g1, nm).flat, getattr(g2, nm).flat), nm
+
+
+SYN200 = [cfg_path("networks", "synthetic", f"syn200-in16-cap1-3-s{i}.graphml") for i in range(3)]
+
+
+def test_native_update_matches_fp32_reference_200_nodes():
+    """Config-5 shapes: n_pad 200, 3 SFCs x 3 SFs (A = 360,000), three 200-node topologies (different
+    action masks), batch 256: the layer-wise GNN kernels, the composed multi-topology actor loss
+    (T c1 = 192 <= B), split-K action projections and the fused TD-target projection, against the fp32
+    CPU autograd learner (first-update gradients per tensor, losses)."""
+    cfg = yaml.safe_load(open(cfg_path("config", "agent", "agent_syn200.yaml")))
+    P, C, T, B = 200, 3, 3, 256
+    ref, gpu = _learners(cfg, T, P, nets=SYN200, C=C)
+    _, auto = _learners(cfg, T, P, nets=SYN200, C=C)
+    auto.native_ok = False
+    for l in (ref, gpu, auto):
+        l.critic_opt.lr = 0.0  # frozen critic (see the three_topologies case)
+    nu = gpu.native_update(B)
+    assert nu.compose and nu.fuse_target and nu.layerwise
+    from gsc_amd.agents import Batch
+    g = torch.Generator().manual_seed(5)
+    topo = torch.arange(B) % T
+    n = torch.tensor([gs_n for gs_n in ref.graphs.n_nodes.tolist()])[topo]
+    obs = torch.rand(B, P, 3, generator=g) * (torch.arange(P)[None, :, None] < n[:, None, None])
+    nxt = torch.rand(B, P, 3, generator=g) * (torch.arange(P)[None, :, None] < n[:, None, None])
+    act = torch.rand(B, P * C * 3 * P, generator=g) * ref.masks[topo]
+    bc = Batch(obs, topo, act, torch.rand(B, generator=g) - 0.5, nxt, (torch.rand(B, generator=g) < 0.2).float())
+    bg = Batch(*(t.cuda() for t in bc[:2]), bc.actions.cuda().bfloat16(), *(t.cuda() for t in bc[3:]))
+    ref.update(bc)
+    gpu.update(bg)
+    auto.update(bg)
+    torch.cuda.synchronize()
+    for nm in ("critic_flat", "actor_flat"):
+        fr, fg, fa = getattr(ref, nm), getattr(gpu, nm), getattr(auto, nm)
+        e_nat, e_auto = _per_param_err(fr, fg), _per_param_err(fr, fa)
+        print("syn200", nm, {k: (round(e_nat[k], 4), round(e_auto[k], 4)) for k in e_nat})
+        bad = {k: (e, e_auto[k]) for k, e in e_nat.items() if e > max(0.04, 2.5 * e_auto[k])}
+        assert not bad, bad
+    for key in ("qf1_loss", "actor_loss", "qf1_values"):
+        r, gv, au = float(ref.last[key]), float(gpu.last[key]), float(auto.last[key])
+        assert abs(r - gv) <= max(0.03 * abs(r) + 1e-3, 2.5 * abs(r - au)), (key, r, gv, au)

@@ -160,7 +160,7 @@ def test_adam_polyak_matches_reference():
     torch.testing.assert_close(tgt, t2, rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("P,n", [(24, 11), (50, 50), (64, 37), (200, 200), (200, 131)])
+@pytest.mark.parametrize("P,n", [(24, 11), (50, 50), (64, 37), (200, 200), (200, 131), (199, 150), (225, 200)])
 def test_explore_postprocess_device(P, n):
     """Lane-parallel kernels: two slices per wave (n_pad <= 32), one slice per wave with 1-4 weights per
     lane (n_pad <= 256, the 50- and 200-node configs)."""
@@ -182,6 +182,20 @@ def test_explore_postprocess_device(P, n):
     out = explore_postprocess(mu, mask, P, False, 0.0, 0.0, seed=5, step=7)
     ref = normalize_slices_reference((0.5 * (2 * mu - 1 + 1)).clamp(0, 1).view(E, -1, P).cpu().double(), 0.1, 2)
     torch.testing.assert_close(out.cpu(), ref.float().view(E, A), rtol=1e-6, atol=1e-6)
+
+
+def test_explore_noise_independent_of_slice_shape():
+    """The raw noisy weights (no threshold / normalisation passes) depend only on (seed, step, flat index):
+    the pair path (n_pad 200: one Philox draw per weight pair, 4 weights per lane) and the one-weight-per-lane
+    path (n_pad 40) give identical bits for the same flat action block."""
+    torch.manual_seed(3)
+    E, A = 4, 200 * 3 * 200
+    mu = torch.rand(E, A, device=DEV)
+    mask = torch.ones(E, A, device=DEV)
+    for warm in (True, False):
+        a = explore_postprocess(mu, mask, 200, warm, 0.0, 0.3, seed=9, step=4, threshold=0.0, passes=0)
+        b = explore_postprocess(mu, mask, 40, warm, 0.0, 0.3, seed=9, step=4, threshold=0.0, passes=0)
+        assert torch.equal(a, b)
 
 
 def test_splitk_linear_matches_linear():
