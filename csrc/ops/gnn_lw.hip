@@ -18,12 +18,83 @@
 #include <pybind11/pybind11.h>
 
 #include "../common.h"
+#include "gnn_mf.h"
 
 namespace py = pybind11;
 
 namespace gsc {
 
 constexpr float kLwSlope = 0.2f;
+
+// ---- MFMA node linears for the lane-per-node kernels (n_pad <= 256) ----------------------------------
+// A graph's node rows as a bf16 [row][k] image (row stride kMfRS = 40: conflict-free 16-byte fragment
+// reads), then one 32-row tile per wave and pass: X = rows W^T (+ b) on v_mfma_f32_32x32x16_bf16 with the
+// H x H weights as fragments (K <= 32: two k-steps) -- instead of H^2 broadcast-LDS FMAs per lane.
+// The image reuses a [P][HV] fp32 LDS region of the kernel: it needs ceil32(P) * 80 bytes.
+__host__ __device__ constexpr bool lw_mfma_fits(int P, int HV) {
+  return P <= 256 && HV >= 16 && ((P + 31) / 32) * 32 * kMfRS * 2 <= P * HV * 4;
+}
+// row i of the image from a lane's fp32 row (channels >= H and rows >= n are zero)
+template <int HV>
+__device__ __forceinline__ void lw_put_bf16_row(__bf16* img, int i, const float (&v)[HV], int H) {
+  bf16x8 c[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * q + j;
+      c[q][j] = (__bf16)((k < HV && k < H) ? v[k < HV ? k : 0] : 0.f);
+    }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) *reinterpret_cast<bf16x8*>(img + i * kMfRS + 8 * q) = c[q];
+}
+// out[b*P + row][c] = sum_k img[row][k] Wa[c][k] (+ Wb-term) + bias for every row < P (lane column c < H).
+// TRANS: the weights enter transposed (dX W: out[row][k] = sum_c img[row][c] W[c][k]).  imgb / wb optional
+// (the second product accumulates into the same tile: dX_l W_l + dX_r W_r).
+template <bool TRANS>
+__device__ __forceinline__ void lw_mfma_rows(const __bf16* imga, const float* __restrict__ wa, const float* __restrict__ ba,
+                                             float* __restrict__ outa, const __bf16* imgb, const float* __restrict__ wb,
+                                             const float* __restrict__ bb, float* __restrict__ outb, int P, int H, long row0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, waves = blockDim.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  bf16x8 fa[2], fb[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    fa[ks] = mf_wfrag(wa, H, H, r, 16 * ks + 8 * hh, TRANS);
+    fb[ks] = wb ? mf_wfrag(wb, H, H, r, 16 * ks + 8 * hh, TRANS) : fa[ks];
+  }
+  const float bca = (ba && r < H) ? ba[r] : 0.f, bcb = (bb && r < H) ? bb[r] : 0.f;
+  for (int t = wave; 32 * t < P; t += waves) {
+    f32x16 xa, xb;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      xa[i] = bca;
+      xb[i] = bcb;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(imga + (32 * t + r) * kMfRS + 16 * ks + 8 * hh);
+      if (outb) {  // two outputs from one input image (x_l', x_r')
+        xa = mf_mma(a, fa[ks], xa);
+        xb = mf_mma(a, fb[ks], xb);
+      } else {     // one output from two input images (dX_l W_l + dX_r W_r)
+        const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(imgb + (32 * t + r) * kMfRS + 16 * ks + 8 * hh);
+        xa = mf_mma(a, fa[ks], xa);
+        xa = mf_mma(a2, fb[ks], xa);
+      }
+    }
+    if (r < H) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = 32 * t + mf_row(i, hh);
+        if (row < P) {
+          outa[(row0 + row) * H + r] = xa[i];
+          if (outb) outb[(row0 + row) * H + r] = xb[i];
+        }
+      }
+    }
+  }
+}
 constexpr int LW_U = 4;  // messages per group in the per-node loops (loads in flight together)
 
 __device__ __forceinline__ void lw_stage_rows(const float* __restrict__ src, long r0, int nr, int w, float* dst);
@@ -301,7 +372,7 @@ __device__ __forceinline__ void lw_store_row(float* dst, const float (&v)[HV], i
 // graph's x_l rows sit in LDS with a padded row stride HV (16-byte reads), the raw scores in an LDS
 // slot per message (each message has one target), and the next conv's node linears read W
 // broadcast from LDS.  Same arithmetic as lw_attn_fwd_kernel.
-template <int HV>
+template <int HV, bool MF = false>
 __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const float* __restrict__ xl,
                                                                const float* __restrict__ xr,
                                                                const float* __restrict__ att,
@@ -316,7 +387,7 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
   const int b = blockIdx.x, t = g.topo[b];
   float* s_xl = lw_g;
   float* s_w = s_xl + P * HV;
-  float* s_sc = s_w + (nx.wl ? 2 * H * HV : 0);
+  float* s_sc = s_w + (nx.wl && !MF ? 2 * H * HV : 0);  // MF: no staged W (fragments from L2)
   float* s_deg = s_sc + M;
   int32_t* iptr = reinterpret_cast<int32_t*>(s_deg + P);
   int32_t* src = iptr + P + 1;
@@ -325,7 +396,7 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
     const int r = k / HV, c = k - r * HV;
     s_xl[k] = c < H ? xl[base + (long)r * H + c] : 0.f;
   }
-  if (nx.wl) {
+  if (nx.wl && !MF) {
     for (int k = threadIdx.x; k < H * HV; k += 256) {
       const int r = k / HV, c = k - r * HV;
       s_w[k] = c < H ? nx.wl[r * H + c] : 0.f;
@@ -346,9 +417,9 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
   }
   const int n = g.nnodes[t];
   float* al = alpha + (long)b * M;
-  float ys[HV];
+  float ys[HV], ykeep[HV];
 #pragma unroll
-  for (int c = 0; c < HV; ++c) ys[c] = 0.f;
+  for (int c = 0; c < HV; ++c) ys[c] = ykeep[c] = 0.f;
   for (int i = threadIdx.x; i < P; i += 256) {
     const long node = (long)b * P + i;
     float y[HV];
@@ -403,7 +474,10 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
       for (int c = 0; c < HV; ++c) y[c] = 0.f;
     }
     lw_store_row<HV>(h_out + node * H, y, H);
-    if (nx.wl) {  // x_l'[co] = b_l'[co] + W_l'[co] . y  (W rows broadcast from LDS)
+    if constexpr (MF) {  // P <= 256: this thread's only node -- its row feeds the MFMA epilogue below
+#pragma unroll
+      for (int c = 0; c < HV; ++c) ykeep[c] = y[c];
+    } else if (nx.wl) {  // x_l'[co] = b_l'[co] + W_l'[co] . y  (W rows broadcast from LDS)
       float ol[HV], orr[HV];
 #pragma unroll
       for (int co = 0; co < HV; ++co) {
@@ -425,6 +499,15 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
       }
       lw_store_row<HV>(nx.xl + node * H, ol, H);
       lw_store_row<HV>(nx.xr + node * H, orr, H);
+    }
+  }
+  if constexpr (MF) {
+    if (nx.wl) {  // the next conv's node linears on the matrix cores
+      __syncthreads();  // every lane is done with the x_l rows: the bf16 image reuses their LDS
+      __bf16* s_y = reinterpret_cast<__bf16*>(s_xl);
+      if ((int)threadIdx.x < ((P + 31) & ~31)) lw_put_bf16_row<HV>(s_y, threadIdx.x, ykeep, H);
+      __syncthreads();
+      lw_mfma_rows<false>(s_y, nx.wl, nx.bl, nx.xl, nullptr, nx.wr, nx.br, nx.xr, P, H, (long)b * P);
     }
   }
   if (emb) {
@@ -760,7 +843,7 @@ __device__ __forceinline__ void lw_load_row(float (&v)[HV], const float* src, in
 // source-sorted order) of alpha_q g_i + de_q att * LeakyReLU'(x_l[j] + x_r[i]), recomputed from
 // LDS, and with wl the input gradient d x_l W_l + d x_r W_r (W rows broadcast from LDS).  Same
 // arithmetic as lw_attn_bwd_kernel + lw_src_gather_kernel.
-template <int HV>
+template <int HV, bool MF = false>
 __global__ __launch_bounds__(256) void lw_lane_attn_bwd_kernel(LwGraph g, float* __restrict__ dh,
                                                                const float* __restrict__ h_out,
                                                                const float* __restrict__ xl,
@@ -778,7 +861,7 @@ __global__ __launch_bounds__(256) void lw_lane_attn_bwd_kernel(LwGraph g, float*
   float* s_rows = lw_g;
   float* s_g = s_rows + P * HV;
   float* s_w = s_g + P * HV;
-  float* al = s_w + (wl ? 2 * H * HV : 0);
+  float* al = s_w + (wl && !MF ? 2 * H * HV : 0);  // MF: no staged W (fragments from L2)
   float* s_de = al + M;
   float* s_deg = s_de + M;
   int32_t* iptr = reinterpret_cast<int32_t*>(s_deg + P);
@@ -792,7 +875,7 @@ __global__ __launch_bounds__(256) void lw_lane_attn_bwd_kernel(LwGraph g, float*
     s_rows[k] = c < H ? xl[base + (long)r * H + c] : 0.f;
     s_g[k] = 0.f;
   }
-  if (wl) {
+  if (wl && !MF) {
     for (int k = threadIdx.x; k < H * HV; k += 256) {
       const int r = k / HV, c = k - r * HV;
       s_w[k] = c < H ? wl[r * H + c] : 0.f;
@@ -892,6 +975,9 @@ __global__ __launch_bounds__(256) void lw_lane_attn_bwd_kernel(LwGraph g, float*
     s_rows[k] = c < H ? xr[base + (long)r * H + c] : 0.f;
   }
   __syncthreads();
+  float skeep[HV], rkeep[HV];  // MF: this thread's (only) source row of d x_l / d x_r for the MFMA epilogue
+#pragma unroll
+  for (int c = 0; c < HV; ++c) skeep[c] = rkeep[c] = 0.f;
   for (int j = threadIdx.x; j < P; j += 256) {
     const long node = (long)b * P + j;
     float s[HV];
@@ -921,7 +1007,13 @@ __global__ __launch_bounds__(256) void lw_lane_attn_bwd_kernel(LwGraph g, float*
       }
     }
     lw_store_row<HV>(dxl + node * H, s, H);
-    if (wl) {
+    if constexpr (MF) {
+      if (wl) {
+        lw_load_row<HV>(rkeep, dxr + node * H, H);  // written by this lane in phase 1 (same node)
+#pragma unroll
+        for (int c = 0; c < HV; ++c) skeep[c] = s[c];
+      }
+    } else if (wl) {
       float r[HV], d[HV];
       lw_load_row<HV>(r, dxr + node * H, H);  // written by this lane in phase 1 (same node)
 #pragma unroll
@@ -942,6 +1034,19 @@ __global__ __launch_bounds__(256) void lw_lane_attn_bwd_kernel(LwGraph g, float*
         }
       }
       lw_store_row<HV>(dh_in + node * H, d, H);
+    }
+  }
+  if constexpr (MF) {
+    if (wl) {  // input gradient d x_l W_l + d x_r W_r on the matrix cores
+      __syncthreads();  // phase 2 is done with the x_r / g rows: the bf16 images reuse their LDS
+      __bf16* img_l = reinterpret_cast<__bf16*>(s_rows);
+      __bf16* img_r = reinterpret_cast<__bf16*>(s_g);
+      if ((int)threadIdx.x < ((P + 31) & ~31)) {
+        lw_put_bf16_row<HV>(img_l, threadIdx.x, skeep, H);
+        lw_put_bf16_row<HV>(img_r, threadIdx.x, rkeep, H);
+      }
+      __syncthreads();
+      lw_mfma_rows<true>(img_l, wl, nullptr, dh_in, img_r, wr, nullptr, nullptr, P, H, (long)b * P);
     }
   }
 }
@@ -1081,6 +1186,75 @@ __global__ __launch_bounds__(256) void lw_conv_grads_kernel(const float* __restr
   }
 }
 
+// MFMA variant (H, Fi <= 32): the same outputs and partial layout.  Per stage of LW_RB rows, wave w owns rows
+// [16w, 16w + 16) and accumulates dW_l = dxl^T h and dW_r = dxr^T h on the matrix cores (A = the 16 rows'
+// d x column for channel c = lane, B = their h column for input k = lane; bf16 operands, fp32 accumulation);
+// the four vector sums (db_l, db_r, d att, d bias) stay fp32 on the VALU.  The waves' tiles are added in a
+// fixed order at the end (deterministic).
+__global__ __launch_bounds__(256) void lw_conv_grads_mfma_kernel(const float* __restrict__ dxl, const float* __restrict__ dxr,
+                                                                 const float* __restrict__ datt, const float* __restrict__ dy,
+                                                                 const float* __restrict__ hin, long R, int H, int Fi,
+                                                                 long chunk, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lw_rows[];  // [dxl | dxr | datt | dy][LW_RB][H], h [LW_RB][Fi]
+  const int C = 2 * H * Fi + 4 * H, HF = H * Fi, S = LW_RB * H;
+  float* s_h = lw_rows + 4 * S;
+  const long r0 = (long)blockIdx.x * chunk;
+  const long r1 = r0 + chunk < R ? r0 + chunk : R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c = lane & 31, hh = lane >> 5;
+  f32x16 gl, gr;
+  mf_zero(gl);
+  mf_zero(gr);
+  float vsum = 0.f;  // thread t < 4H: vector output t (db_l, db_r, d att, d bias)
+  const int vb = tid / H, vc = tid - vb * H;  // block of [dxl | dxr | datt | dy] and channel
+  for (long rb = r0; rb < r1; rb += LW_RB) {
+    const int nr = (int)(r1 - rb < LW_RB ? r1 - rb : LW_RB);
+    lw_stage_rows(dxl, rb, nr, H, lw_rows);
+    lw_stage_rows(dxr, rb, nr, H, lw_rows + S);
+    lw_stage_rows(datt, rb, nr, H, lw_rows + 2 * S);
+    lw_stage_rows(dy, rb, nr, H, lw_rows + 3 * S);
+    lw_stage_rows(hin, rb, nr, Fi, s_h);
+    __syncthreads();
+    if (tid < 4 * H) {
+      const float* pa = lw_rows + vb * S + vc;
+      for (int row = 0; row < nr; ++row) vsum += pa[row * H];
+    }
+    if (16 * wave < nr) {
+      bf16x8 al, ar, bh;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int row = 16 * wave + 8 * hh + j;
+        const bool in = row < nr;
+        al[j] = (__bf16)((in && c < H) ? lw_rows[row * H + c] : 0.f);
+        ar[j] = (__bf16)((in && c < H) ? lw_rows[S + row * H + c] : 0.f);
+        bh[j] = (__bf16)((in && c < Fi) ? s_h[row * Fi + c] : 0.f);
+      }
+      gl = mf_mma(al, bh, gl);
+      gr = mf_mma(ar, bh, gr);
+    }
+    __syncthreads();
+  }
+  // wave tiles -> LDS [wave][l|r][32][32], summed over the waves in a fixed order
+  float* red = lw_rows;  // 4 x 2 x 1024 floats (the stage buffers are free)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = mf_row(i, hh);  // dW row = channel of the A operand (row of the 32x32 tile)
+    red[(wave * 2 + 0) * 1024 + row * 32 + c] = gl[i];
+    red[(wave * 2 + 1) * 1024 + row * 32 + c] = gr[i];
+  }
+  __syncthreads();
+  for (int o = tid; o < 2 * HF; o += 256) {
+    const int side = o >= HF, oo = o - side * HF, ch = oo / Fi, k = oo - ch * Fi;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v += red[(w * 2 + side) * 1024 + ch * 32 + k];
+    part[(long)blockIdx.x * C + (side ? HF + H + oo : oo)] = v;  // [dW_l | db_l | dW_r | db_r | att | bias]
+  }
+  if (tid < 4 * H) {
+    const int off = vb == 0 ? HF : vb == 1 ? 2 * HF + H : 2 * HF + 2 * H + (vb - 2) * H;
+    part[(long)blockIdx.x * C + off + vc] = vsum;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------
 static LwGraph lw_graph(py::dict t, uintptr_t topo, int B, int P, int H) {
   LwGraph g{};
@@ -1127,11 +1301,16 @@ void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
   }
   if (H <= 32) {  // lane per node
     const int hv = H <= 8 ? 8 : H <= 16 ? 16 : H <= 24 ? 24 : 32;
-    const size_t lds = sizeof(float) * ((size_t)P * hv + (nx.wl ? 2 * H * hv : 0) + 2 * g.M + 2 * P + 1);
+    // MFMA node linears (no staged W) when the graph's rows fit the bf16 image (GSC_LW_MFMA=0: VALU)
+    static const bool mf_env = getenv("GSC_LW_MFMA") == nullptr || atoi(getenv("GSC_LW_MFMA")) != 0;
+    const bool mf = mf_env && nx.wl && lw_mfma_fits(P, hv);
+    const size_t lds = sizeof(float) * ((size_t)P * hv + (nx.wl && !mf ? 2 * H * hv : 0) + 2 * g.M + 2 * P + 1);
     if (lds <= 64 * 1024) {
-      auto kl = hv == 8 ? lw_lane_attn_fwd_kernel<8>
-                : hv == 16 ? lw_lane_attn_fwd_kernel<16> : hv == 24 ? lw_lane_attn_fwd_kernel<24>
-                                                           : lw_lane_attn_fwd_kernel<32>;
+      auto kl = mf ? (hv == 16 ? lw_lane_attn_fwd_kernel<16, true> : hv == 24 ? lw_lane_attn_fwd_kernel<24, true>
+                                                                    : lw_lane_attn_fwd_kernel<32, true>)
+                   : hv == 8 ? lw_lane_attn_fwd_kernel<8>
+                   : hv == 16 ? lw_lane_attn_fwd_kernel<16> : hv == 24 ? lw_lane_attn_fwd_kernel<24>
+                                                              : lw_lane_attn_fwd_kernel<32>;
       hipLaunchKernelGGL(kl, dim3(B), dim3(256), lds, stream_of(stream), g, ptr<const float>(xl), ptr<const float>(xr),
                          ptr<const float>(att), ptr<const float>(bias), relu, ptr<float>(h_out), ptr<float>(alpha), nx,
                          ptr<float>(emb));
@@ -1207,11 +1386,15 @@ void lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, ui
   GSC_CHECK(!wl || (wr && dh_in), "lw_attn_bwd_gather: the input gradient needs wl, wr, dh_in");
   if (H <= 32) {  // lane per node
     const int hv = H <= 8 ? 8 : H <= 16 ? 16 : H <= 24 ? 24 : 32;
-    const size_t ll = sizeof(float) * (2 * (size_t)P * hv + (wl ? 2 * H * hv : 0) + 5 * g.M + P + 2 * (P + 1));
+    static const bool mf_env = getenv("GSC_LW_MFMA") == nullptr || atoi(getenv("GSC_LW_MFMA")) != 0;
+    const bool mf = mf_env && wl && lw_mfma_fits(P, hv);
+    const size_t ll = sizeof(float) * (2 * (size_t)P * hv + (wl && !mf ? 2 * H * hv : 0) + 5 * g.M + P + 2 * (P + 1));
     if (ll <= 80 * 1024) {  // >= 2 workgroups per CU
-      auto kl = hv == 8 ? lw_lane_attn_bwd_kernel<8>
-                : hv == 16 ? lw_lane_attn_bwd_kernel<16> : hv == 24 ? lw_lane_attn_bwd_kernel<24>
-                                                           : lw_lane_attn_bwd_kernel<32>;
+      auto kl = mf ? (hv == 16 ? lw_lane_attn_bwd_kernel<16, true> : hv == 24 ? lw_lane_attn_bwd_kernel<24, true>
+                                                                    : lw_lane_attn_bwd_kernel<32, true>)
+                   : hv == 8 ? lw_lane_attn_bwd_kernel<8>
+                   : hv == 16 ? lw_lane_attn_bwd_kernel<16> : hv == 24 ? lw_lane_attn_bwd_kernel<24>
+                                                              : lw_lane_attn_bwd_kernel<32>;
       hipLaunchKernelGGL(kl, dim3(B), dim3(256), ll, stream_of(stream), g, ptr<float>(dh), ptr<const float>(h_out),
                          ptr<const float>(xl), ptr<const float>(xr), ptr<const float>(alpha), ptr<const float>(att),
                          ptr<float>(dxr), ptr<float>(datt), ptr<float>(dxl), ptr<const float>(wl),
@@ -1272,6 +1455,18 @@ void lw_conv_grads(uintptr_t dxl, uintptr_t dxr, uintptr_t datt, uintptr_t dy, u
   const int no = (C + 255) / 256;
   const size_t lds = sizeof(float) * LW_RB * (4 * H + Fi);  // 4 S is a multiple of 4 floats: s_h stays aligned
   const hipStream_t s = stream_of(stream);
+  static const bool mf_env = getenv("GSC_LW_MFMA") == nullptr || atoi(getenv("GSC_LW_MFMA")) != 0;
+  if (mf_env && H <= 32 && Fi <= 32 && 4 * H <= 256) {  // dW on the matrix cores
+    const size_t lds_mf = std::max(lds, sizeof(float) * 8 * 1024);  // the final wave-tile reduction
+    hipLaunchKernelGGL(lw_conv_grads_mfma_kernel, dim3(K), dim3(256), lds_mf, s, ptr<const float>(dxl),
+                       ptr<const float>(dxr), ptr<const float>(datt), ptr<const float>(dy), ptr<const float>(hin), R, H,
+                       Fi, chunk, ptr<float>(part));
+    check_launch();
+    hipLaunchKernelGGL(lw_colsum_p2_kernel, dim3(C), dim3(256), 0, s, ptr<const float>(part), K, C, ptr<float>(out),
+                       accumulate);
+    check_launch();
+    return;
+  }
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(K), dim3(256), lds, s, ptr<const float>(dxl), ptr<const float>(dxr),
                        ptr<const float>(datt), ptr<const float>(dy), ptr<const float>(hin), R, H, Fi, chunk,
