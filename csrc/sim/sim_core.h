@@ -156,7 +156,7 @@ struct Dims {
 struct Layout {
   int hdr, node_cap, node_rem, inter_arr, max_usage, run_drop_node, mmpp_state, sf_load, sf_start, proc_traffic,
       requested, drop_locs, link_rem, link_passed, link_next, rel, flows, procs, events, flow_free, proc_free,
-      sf_present, placement, wrr_ep, hot, sched, wrr, pmask, total;
+      sf_present, placement, hot, sched, wrr, pmask, total;
 };
 
 // WRR counter rows ([N, C, S] rows of N counters) and the run-window epoch that tags them (see run_decide)
@@ -168,6 +168,9 @@ __host__ __device__ constexpr int wrr_rows(const Dims& d) { return d.N * d.C * d
 __host__ __device__ constexpr int pmask_rows(const Dims& d) { return d.N > 64 ? d.N * d.C * d.S : 0; }
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
+__host__ __device__ constexpr int wrr_ep_offset(const Layout& L, const Dims& d) {
+  return L.hot - align16(4 * (wrr_rows(d) + 1));
+}
 
 __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   Layout L{};
@@ -196,7 +199,9 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   GSC_TAKE(proc_free, 2 * d.proc_cap);
   GSC_TAKE(sf_present, d.N * d.S);
   GSC_TAKE(placement, d.N * d.S);
-  GSC_TAKE(wrr_ep, 4 * (wrr_rows(d) + 1));  // per-row epoch + the current run-window epoch (last entry)
+  // the last run of the hot prefix: per-row WRR epoch + the current run-window epoch (wrr_ep_offset; not a
+  // Layout field -- the kernel-argument layout of the LDS-resident kernels stays as it was)
+  o += align16(4 * (wrr_rows(d) + 1));
   L.hot = o;
   GSC_TAKE(sched, 8 * d.N * d.C * d.S * d.N);
   GSC_TAKE(wrr, 4 * d.N * d.C * d.S * d.N);
@@ -241,7 +246,7 @@ struct Env {
     drop_locs = (int32_t*)(base + L.drop_locs);
     sched = (double*)(cb + L.sched);
     wrr = (int32_t*)(cb + L.wrr);
-    wrr_ep = (int32_t*)(base + L.wrr_ep);
+    wrr_ep = (int32_t*)(base + wrr_ep_offset(L, dims));
     act = nullptr;
     pmask = (uint64_t*)(cb + L.pmask);
     link_rem = (double*)(base + L.link_rem);

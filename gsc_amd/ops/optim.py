@@ -232,11 +232,12 @@ class FusedAdamPolyak:
 
     def state_dict(self) -> dict:
         """Full-length moments (sharded: all-gathered -- a collective, every rank calls it)."""
-        m, v = (self._zero_state(self.m), self._zero_state(self.v)) if self.zero is not None else (self.m, self.v)
+        z = getattr(self, "zero", None) is not None
+        m, v = (self._zero_state(self.m), self._zero_state(self.v)) if z else (self.m, self.v)
         return {"m": m, "v": v, "step": self.step_count, "lr": self.lr, "betas": self.betas, "eps": self.eps}
 
     def load_state_dict(self, sd: dict) -> None:
-        if self.zero is not None:
+        if getattr(self, "zero", None) is not None:
             self._zero_load(self.m, sd["m"].to(self.m.device))
             self._zero_load(self.v, sd["v"].to(self.v.device))
         else:
@@ -247,7 +248,7 @@ class FusedAdamPolyak:
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0) -> None:
-        if self.zero is not None:
+        if getattr(self, "zero", None) is not None:
             self._step_zero(grad_scale)
             return
         p, g = self.fp.flat, self.fp.grad

@@ -157,8 +157,14 @@ def _default_caps(topos: Sequence[Topology], cfg: dict, trace: Optional[dict] = 
     # configs are 30-60 events, so 128 leaves 2x headroom (overflow is flagged, never silent)
     # pending link returns: one per hop a flow took within its duration -- long paths (200 nodes:
     # 12 hops) hold several per flow
+    # pending events: the register queue holds 64 per set (csrc/sim/sim_kernels.hip RegQueue); measured peaks
+    # are 0.25-0.4 x the flow capacity (28 of 72 on sample_config, 72 of 288 at 200 nodes).  One set (64) for
+    # sample_config measured slower than two, 2.25 vs 2.16 ms/step on the bench's 64 CUs (the step kernel's
+    # code layout, not its instruction count, decides there), so 128 stays the floor
+    ev = 128 if max_ing <= 8 else 256
+    ev = int(os.environ.get("GSC_SIM_EVENT_CAP", ev))
     return dict(flow_cap=flows, proc_cap=int(min(32000, 2 * flows + 32 + cfg["F"] * hold)),
-                event_cap=128 if max_ing <= 8 else 256,
+                event_cap=ev,
                 rel_cap=int(min(16384, 2 * flows * max(1.0, hops / 4) + hops * hold)))
 
 
