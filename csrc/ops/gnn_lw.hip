@@ -527,6 +527,202 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
   }
 }
 
+template <int HV>
+__device__ __forceinline__ void lw_load_row(float (&v)[HV], const float* src, int H);
+
+// Staged lane-per-node forward (P <= 256, 16 <= H <= 32): one workgroup per graph, lane i = target node i.
+// Latency-oriented: every global load of a graph is issued before the first LDS store (the x_l block as
+// 16-B vectors, the lane's own x_r row, the topology rows: one HBM round trip per graph instead of one per
+// staging-loop trip), only the gathered x_l rows live in LDS (row stride HV + 4 = 16 B x odd: the random
+// row gathers spread over all bank quads), so ~32 KB per graph keeps 5 graphs in flight per CU.  The score
+// a . LeakyReLU(z) runs as (1+s)/2 (a . z) + (1-s)/2 (a . |z|) -- two independent FMA chains with the |z|
+// source modifier instead of a compare / select per channel.  Outputs leave through LDS with coalesced
+// stores; the next conv's node linears run on the matrix cores (lw_mfma_rows).
+template <int HV>
+__global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kernel(LwGraph g, const float* __restrict__ xl,
+                                                                const float* __restrict__ xr,
+                                                                const float* __restrict__ att,
+                                                                const float* __restrict__ bias, int relu,
+                                                                float* __restrict__ h_out, float* __restrict__ alpha,
+                                                                LwNext nx, float* __restrict__ emb) {
+  // LDS: x_l rows [P][RS] (then the output rows, then their bf16 image), scores [M] (then alpha), deg [P],
+  //      in_ptr [P+1], in_src [M]
+  constexpr int RS = HV + 4;
+  constexpr int kV = 8;  // 16-B vectors per thread of the x_l block (P H <= 256 x 32)
+  __shared__ float red[4][HV];
+  extern __shared__ __attribute__((aligned(16))) float lw_g[];
+  const int H = g.H, P = g.P, M = g.M;
+  const int b = blockIdx.x, t = g.topo[b];
+  float* s_xl = lw_g;
+  float* s_sc = s_xl + P * RS;
+  float* s_deg = s_sc + M;
+  int32_t* iptr = reinterpret_cast<int32_t*>(s_deg + P);
+  int32_t* src = iptr + P + 1;
+  const long base = (long)b * P * H;
+  const int NE = P * H, i = threadIdx.x;
+  const int n = g.nnodes[t];
+  const bool vec = (NE & 3) == 0 && ((reinterpret_cast<uintptr_t>(xl + base) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(h_out + base) & 15) == 0);
+  // ---- all loads in flight together
+  float4 v4[kV];
+  if (vec) {
+    const float4* x4 = reinterpret_cast<const float4*>(xl + base);
+#pragma unroll
+    for (int u = 0; u < kV; ++u) {
+      const int j = i + 256 * u;
+      if (j < NE / 4) v4[u] = x4[j];
+    }
+  }
+  float xri[HV];
+  if (i < n) lw_load_row<HV>(xri, xr + base + (long)i * H, H);
+  int ip = 0;
+  float dg = 1.f;
+  if (i <= P) ip = g.in_ptr[(long)t * (P + 1) + i];
+  if (i < P) dg = g.deg[(long)t * P + i];
+  int sv[kV];
+#pragma unroll
+  for (int u = 0; u < kV; ++u) {
+    const int j = i + 256 * u;
+    if (j < M) sv[u] = g.in_src[(long)t * M + j];
+  }
+  // ---- LDS images
+  if (vec) {
+#pragma unroll
+    for (int u = 0; u < kV; ++u) {
+      const int j = i + 256 * u;
+      if (j < NE / 4) {
+        int r = (4 * j) / H, c = 4 * j - r * H;
+        const float f[4] = {v4[u].x, v4[u].y, v4[u].z, v4[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s_xl[r * RS + c] = f[e];
+          if (++c == H) { c = 0; ++r; }
+        }
+      }
+    }
+  } else {
+    for (int k = i; k < NE; k += 256) {
+      const int r = k / H, c = k - r * H;
+      s_xl[r * RS + c] = xl[base + k];
+    }
+  }
+  for (int k = i; k < P * (HV - H); k += 256) {  // padded channels are read by the gathers: zero, not stale
+    const int r = k / (HV - H), c = H + k - r * (HV - H);
+    s_xl[r * RS + c] = 0.f;
+  }
+  if (i <= P) iptr[i] = ip;
+  if (i < P) s_deg[i] = dg;
+  if (P == 256 && i == 0) iptr[256] = g.in_ptr[(long)t * (P + 1) + 256];
+#pragma unroll
+  for (int u = 0; u < kV; ++u) {
+    const int j = i + 256 * u;
+    if (j < M) src[j] = sv[u];
+  }
+  for (int k = i + 256 * kV; k < M; k += 256) src[k] = g.in_src[(long)t * M + k];
+  __syncthreads();
+  // ---- lane = target node: scores, online softmax, aggregation
+  float y[HV];
+#pragma unroll
+  for (int c = 0; c < HV; ++c) y[c] = 0.f;
+  if (i < n) {
+    float a_[HV], acc[HV];  // a_: uniform (scalar registers)
+#pragma unroll
+    for (int c = 0; c < HV; ++c) {
+      a_[c] = c < H ? att[c] : 0.f;
+      acc[c] = 0.f;
+    }
+    const int q0 = iptr[i], q1 = iptr[i + 1];
+    float mx = -__builtin_inff(), den = 0.f;
+    for (int q = q0; q < q1; ++q) {
+      const float4* row = reinterpret_cast<const float4*>(s_xl + src[q] * RS);
+      float xj[HV];
+#pragma unroll
+      for (int v = 0; v < HV / 4; ++v) {
+        const float4 f = row[v];
+        xj[4 * v] = f.x;
+        xj[4 * v + 1] = f.y;
+        xj[4 * v + 2] = f.z;
+        xj[4 * v + 3] = f.w;
+      }
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int c = 0; c < HV; ++c) {
+        const float z = xj[c] + xri[c];
+        s0 = fmaf(a_[c], z, s0);
+        s1 = fmaf(a_[c], fabsf(z), s1);
+      }
+      const float sc = 0.5f * (1.f + kLwSlope) * s0 + 0.5f * (1.f - kLwSlope) * s1;
+      s_sc[q] = sc;
+      if (sc > mx) {
+        const float r = __expf(mx - sc);  // 0 for the first message
+        den *= r;
+#pragma unroll
+        for (int c = 0; c < HV; ++c) acc[c] *= r;
+        mx = sc;
+      }
+      const float e = __expf(sc - mx);
+      den += e;
+#pragma unroll
+      for (int c = 0; c < HV; ++c) acc[c] = fmaf(e, xj[c], acc[c]);
+    }
+    const float inv = 1.f / (den + 1e-16f);
+    for (int q = q0; q < q1; ++q) s_sc[q] = __expf(s_sc[q] - mx) * inv;  // alpha, in place
+    const float scl = inv / s_deg[i];
+#pragma unroll
+    for (int c = 0; c < HV; ++c) {
+      float v = acc[c] * scl + (c < H ? bias[c] : 0.f);
+      if (relu) v = v > 0.f ? v : 0.f;
+      y[c] = c < H ? v : 0.f;
+    }
+  }
+  __syncthreads();  // every lane is done gathering x_l rows: the output rows take their place
+  if (i < P) {
+    float4* ro = reinterpret_cast<float4*>(s_xl + i * RS);
+#pragma unroll
+    for (int v = 0; v < HV / 4; ++v) ro[v] = make_float4(y[4 * v], y[4 * v + 1], y[4 * v + 2], y[4 * v + 3]);
+  }
+  __syncthreads();
+  if (vec) {  // coalesced 16-B stores of the [P][H] block
+    float4* o4 = reinterpret_cast<float4*>(h_out + base);
+    for (int j = i; j < NE / 4; j += 256) {
+      int r = (4 * j) / H, c = 4 * j - r * H;
+      float f[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        f[e] = s_xl[r * RS + c];
+        if (++c == H) { c = 0; ++r; }
+      }
+      o4[j] = make_float4(f[0], f[1], f[2], f[3]);
+    }
+  } else {
+    for (int k = i; k < NE; k += 256) {
+      const int r = k / H, c = k - r * H;
+      h_out[base + k] = s_xl[r * RS + c];
+    }
+  }
+  const int m = iptr[n];
+  for (int q = i; q < m; q += 256) alpha[(long)b * M + q] = s_sc[q];
+  if (emb) {  // mean pool: lane partial sums reduced in a fixed shuffle / wave order
+    const int lane = i & 63, w = i >> 6;
+#pragma unroll
+    for (int c = 0; c < HV; ++c) {
+      float v = i < n ? y[c] : 0.f;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) red[w][c] = v;
+    }
+    __syncthreads();
+    if (i < H) emb[(long)b * H + i] = ((red[0][i] + red[1][i]) + (red[2][i] + red[3][i])) / (float)n;
+  }
+  if (nx.wl) {  // the next conv's node linears on the matrix cores (after the pool: y dies in the bf16 image)
+    __syncthreads();
+    __bf16* s_y = reinterpret_cast<__bf16*>(s_xl);
+    if (i < ((P + 31) & ~31)) lw_put_bf16_row<HV>(s_y, i, y, H);
+    __syncthreads();
+    lw_mfma_rows<false>(s_y, nx.wl, nx.bl, nx.xl, nullptr, nx.wr, nx.br, nx.xr, P, H, (long)b * P);
+  }
+}
+
 // emb[b,:] = mean over the graph's real nodes of h[b,:,:]
 template <int NL>
 __global__ __launch_bounds__(256) void lw_pool_kernel(LwGraph g, const float* __restrict__ h, float* __restrict__ emb) {
@@ -1051,6 +1247,261 @@ __global__ __launch_bounds__(256) void lw_lane_attn_bwd_kernel(LwGraph g, float*
   }
 }
 
+// [P][H] block <-> LDS rows [P][LD] (channels >= H untouched), 16-B global vectors (caller checks alignment)
+template <int LD, int KV>
+__device__ __forceinline__ void lw_block_load(float4 (&v)[KV], const float* src, int NE) {
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+#pragma unroll
+  for (int u = 0; u < KV; ++u) {
+    const int j = threadIdx.x + 256 * u;
+    if (j < NE / 4) v[u] = s4[j];
+  }
+}
+template <int LD, int KV>
+__device__ __forceinline__ void lw_block_to_lds(const float4 (&v)[KV], float* rows, int NE, int H) {
+#pragma unroll
+  for (int u = 0; u < KV; ++u) {
+    const int j = threadIdx.x + 256 * u;
+    if (j < NE / 4) {
+      int r = (4 * j) / H, c = 4 * j - r * H;
+      const float f[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        rows[r * LD + c] = f[e];
+        if (++c == H) { c = 0; ++r; }
+      }
+    }
+  }
+}
+template <int LD>
+__device__ __forceinline__ void lw_lds_to_block(float* dst, const float* rows, int NE, int H) {
+  float4* d4 = reinterpret_cast<float4*>(dst);
+  for (int j = threadIdx.x; j < NE / 4; j += 256) {
+    int r = (4 * j) / H, c = 4 * j - r * H;
+    float f[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      f[e] = rows[r * LD + c];
+      if (++c == H) { c = 0; ++r; }
+    }
+    d4[j] = make_float4(f[0], f[1], f[2], f[3]);
+  }
+}
+template <int HV>
+__device__ __forceinline__ void lw_put_row(float* rows, int i, const float (&v)[HV]) {
+  float4* o = reinterpret_cast<float4*>(rows + i * HV);
+#pragma unroll
+  for (int k = 0; k < HV / 4; ++k) o[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+}
+template <int HV>
+__device__ __forceinline__ void lw_get_row(float (&v)[HV], const float* rows, int i) {
+  const float4* o = reinterpret_cast<const float4*>(rows + i * HV);
+#pragma unroll
+  for (int k = 0; k < HV / 4; ++k) {
+    const float4 f = o[k];
+    v[4 * k] = f.x;
+    v[4 * k + 1] = f.y;
+    v[4 * k + 2] = f.z;
+    v[4 * k + 3] = f.w;
+  }
+}
+
+// Staged lane-per-node backward (P <= 256, 16 <= H <= 32, 16-B aligned [P][H] blocks): the arithmetic of
+// lw_lane_attn_bwd_kernel, laid out for latency and occupancy.  Every global load of a graph is issued
+// before the first LDS store (x_l, dh, h_out blocks as 16-B vectors, alpha, the topology rows, the lane's
+// own x_r / x_l rows); two [P][HV] row images (x_l then x_r; g) plus byte / short message indices keep a
+// 200-node graph at ~53 KB (3 graphs per CU); the gated dY goes back to dh from the staging registers;
+// phase 1 (lane = target node) and phase 2 (lane = source node) read only LDS; x_r replaces x_l in LDS
+// between them (L2-hot reload).  d x_l / d x_r / d att leave through LDS with coalesced 16-B stores, and
+// the input gradient d x_l W_l + d x_r W_r runs on the matrix cores (lw_mfma_rows).
+template <int HV>
+__global__ __launch_bounds__(256, HV <= 24 ? 3 : 2) void lw_stage_attn_bwd_kernel(LwGraph g, float* __restrict__ dh,
+                                                                   const float* __restrict__ h_out,
+                                                                   const float* __restrict__ xl,
+                                                                   const float* __restrict__ xr,
+                                                                   const float* __restrict__ alpha,
+                                                                   const float* __restrict__ att, float* __restrict__ dxr,
+                                                                   float* __restrict__ datt, float* __restrict__ dxl,
+                                                                   const float* __restrict__ wl,
+                                                                   const float* __restrict__ wr, float* __restrict__ dh_in) {
+  // LDS: rows [P][HV] (x_l, then x_r, then outputs), g [P][HV], alpha, de [M] (fp32), deg [P], in_ptr / out_ptr
+  //      [P+1], out_q [M] (u16), in_src / target [M] (u8)
+  constexpr int KV = HV / 4;  // 16-B vectors per thread of a [P][H] block (P H <= 256 HV)
+  extern __shared__ __attribute__((aligned(16))) float lw_g[];
+  const int H = g.H, P = g.P, M = g.M;
+  const int b = blockIdx.x, t = g.topo[b];
+  float* s_rows = lw_g;
+  float* s_g = s_rows + P * HV;
+  float* al = s_g + P * HV;
+  float* s_de = al + M;
+  float* s_deg = s_de + M;
+  int32_t* iptr = reinterpret_cast<int32_t*>(s_deg + P);
+  int32_t* optr = iptr + P + 1;
+  uint16_t* oq = reinterpret_cast<uint16_t*>(optr + P + 1);
+  uint8_t* src = reinterpret_cast<uint8_t*>(oq + M);
+  uint8_t* tgt = src + M;
+  const long base = (long)b * P * H;
+  const int NE = P * H, i = threadIdx.x;
+  const int n = g.nnodes[t];
+  // ---- every load in flight together
+  float4 vx[KV], vd[KV], vh[KV];
+  lw_block_load<HV, KV>(vx, xl + base, NE);
+  lw_block_load<HV, KV>(vd, dh + base, NE);
+  if (h_out) lw_block_load<HV, KV>(vh, h_out + base, NE);
+  float xri[HV];
+  if (i < n) lw_load_row<HV>(xri, xr + base + (long)i * H, H);
+  int ip = 0, op = 0;
+  float dg = 1.f;
+  if (i <= P) {
+    ip = g.in_ptr[(long)t * (P + 1) + i];
+    op = g.out_ptr[(long)t * (P + 1) + i];
+  }
+  if (i < P) dg = g.deg[(long)t * P + i];
+  for (int k = i; k < M; k += 256) {
+    al[k] = alpha[(long)b * M + k];
+    src[k] = (uint8_t)g.in_src[(long)t * M + k];
+    oq[k] = (uint16_t)g.out_q[(long)t * M + k];
+  }
+  // ---- LDS images; dY = dh (ReLU-gated by the conv output, padded nodes 0) back to dh
+  lw_block_to_lds<HV, KV>(vx, s_rows, NE, H);
+#pragma unroll
+  for (int u = 0; u < KV; ++u) {
+    const int j = i + 256 * u;
+    if (j < NE / 4) {
+      float f[4] = {vd[u].x, vd[u].y, vd[u].z, vd[u].w};
+      if (h_out) {
+        const float o[4] = {vh[u].x, vh[u].y, vh[u].z, vh[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f[e] = o[e] > 0.f ? f[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if ((4 * j + e) / H >= n) f[e] = 0.f;
+      vd[u] = make_float4(f[0], f[1], f[2], f[3]);
+      reinterpret_cast<float4*>(dh + base)[j] = vd[u];
+    }
+  }
+  lw_block_to_lds<HV, KV>(vd, s_g, NE, H);
+  for (int k = i; k < P * (HV - H); k += 256) {  // padded channels: read by the row loads, must be finite
+    const int r = k / (HV - H), c = H + k - r * (HV - H);
+    s_rows[r * HV + c] = 0.f;
+    s_g[r * HV + c] = 0.f;
+  }
+  if (i <= P) {
+    iptr[i] = ip;
+    optr[i] = op;
+  }
+  if (i < P) s_deg[i] = dg;
+  if (P == 256 && i == 0) {
+    iptr[256] = g.in_ptr[(long)t * (P + 1) + 256];
+    optr[256] = g.out_ptr[(long)t * (P + 1) + 256];
+  }
+  __syncthreads();
+  float a_[HV];
+#pragma unroll
+  for (int c = 0; c < HV; ++c) a_[c] = c < H ? att[c] : 0.f;
+  // ---- phase 1: lane = target node
+  float d1[HV], d2[HV];  // d x_r, d att
+#pragma unroll
+  for (int c = 0; c < HV; ++c) {
+    d1[c] = 0.f;
+    d2[c] = 0.f;
+  }
+  if (i < n) {
+    float gc[HV];
+    lw_get_row<HV>(gc, s_g, i);
+    const float inv_deg = 1.f / s_deg[i];
+#pragma unroll
+    for (int c = 0; c < HV; ++c) gc[c] *= inv_deg;
+    lw_put_row<HV>(s_g, i, gc);  // own row: phase 2 reads the scaled rows after the barrier
+    const int q0 = iptr[i], q1 = iptr[i + 1];
+    float sad = 0.f;
+    for (int q = q0; q < q1; ++q) {
+      const float4* row = reinterpret_cast<const float4*>(s_rows + src[q] * HV);
+      float da = 0.f;
+#pragma unroll
+      for (int v = 0; v < HV / 4; ++v) {
+        const float4 f = row[v];
+        da += gc[4 * v] * f.x + gc[4 * v + 1] * f.y + gc[4 * v + 2] * f.z + gc[4 * v + 3] * f.w;
+      }
+      sad += al[q] * da;
+    }
+    for (int q = q0; q < q1; ++q) {
+      float xj[HV];
+      lw_get_row<HV>(xj, s_rows, src[q]);
+      float da = 0.f;
+#pragma unroll
+      for (int c = 0; c < HV; ++c) da += gc[c] * xj[c];
+      const float de = al[q] * (da - sad);
+      s_de[q] = de;
+      tgt[q] = (uint8_t)i;
+#pragma unroll
+      for (int c = 0; c < HV; ++c) {
+        const float z = xj[c] + xri[c];
+        d2[c] += de * leaky(z);
+        d1[c] += de * a_[c] * (z > 0.f ? 1.f : kLwSlope);
+      }
+    }
+  }
+  float xlj[HV];  // the lane's own x_l row for phase 2, before x_r replaces the image
+  if (i < n) lw_get_row<HV>(xlj, s_rows, i);
+  __syncthreads();  // phase 1 is done with the x_l rows; scaled g, de and targets complete
+  {
+    float4 vr[KV];  // x_r block (L2-hot: the lanes' own-row reads above)
+    lw_block_load<HV, KV>(vr, xr + base, NE);
+    lw_block_to_lds<HV, KV>(vr, s_rows, NE, H);
+  }
+  __syncthreads();
+  // ---- phase 2: lane = source node
+  float s[HV];  // d x_l
+#pragma unroll
+  for (int c = 0; c < HV; ++c) s[c] = 0.f;
+  if (i < n) {
+    const int p0 = optr[i], p1 = optr[i + 1];
+    for (int p = p0; p < p1; ++p) {
+      const int q = oq[p];
+      const int ti = tgt[q];
+      const float aq = al[q], de = s_de[q];
+      const float4* xr4 = reinterpret_cast<const float4*>(s_rows + ti * HV);
+      const float4* g4 = reinterpret_cast<const float4*>(s_g + ti * HV);
+#pragma unroll
+      for (int v = 0; v < HV / 4; ++v) {
+        const float4 fr = xr4[v], fg = g4[v];
+        const float zr[4] = {fr.x, fr.y, fr.z, fr.w}, gg[4] = {fg.x, fg.y, fg.z, fg.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 4 * v + e;
+          const float z = xlj[c] + zr[e];
+          s[c] += aq * gg[e] + de * a_[c] * (z > 0.f ? 1.f : kLwSlope);
+        }
+      }
+    }
+  }
+  __syncthreads();  // every lane is done gathering x_r / g rows
+  if (i < P) {      // rows >= n carry zeros
+    lw_put_row<HV>(s_rows, i, s);
+    lw_put_row<HV>(s_g, i, d1);
+  }
+  __syncthreads();
+  lw_lds_to_block<HV>(dxl + base, s_rows, NE, H);
+  lw_lds_to_block<HV>(dxr + base, s_g, NE, H);
+  __syncthreads();
+  if (i < P) lw_put_row<HV>(s_rows, i, d2);
+  __syncthreads();
+  lw_lds_to_block<HV>(datt + base, s_rows, NE, H);
+  if (wl) {  // input gradient d x_l W_l + d x_r W_r on the matrix cores (bf16 images over the row images)
+    __syncthreads();
+    __bf16* img_l = reinterpret_cast<__bf16*>(s_rows);
+    __bf16* img_r = reinterpret_cast<__bf16*>(s_g);
+    if (i < ((P + 31) & ~31)) {
+      lw_put_bf16_row<HV>(img_l, i, s, H);
+      lw_put_bf16_row<HV>(img_r, i, d1, H);
+    }
+    __syncthreads();
+    lw_mfma_rows<true>(img_l, wl, nullptr, dh_in, img_r, wr, nullptr, nullptr, P, H, (long)b * P);
+  }
+}
+
 // Deterministic column sums of x [R, C] (row stride ldx, C <= 256): phase 1 -- block k sums rows
 // [k*chunk, (k+1)*chunk): lane t < L = (256 / C) C owns column t % C and rows t / C + j (L / C), so a
 // wave reads whole rows (coalesced); the lanes of a column are added in a fixed order.  Phase 2 --
@@ -1304,6 +1755,20 @@ void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
     // MFMA node linears (no staged W) when the graph's rows fit the bf16 image (GSC_LW_MFMA=0: VALU)
     static const bool mf_env = getenv("GSC_LW_MFMA") == nullptr || atoi(getenv("GSC_LW_MFMA")) != 0;
     const bool mf = mf_env && nx.wl && lw_mfma_fits(P, hv);
+    // staged variant: both row blocks in LDS, coalesced output / alpha stores, MFMA linears
+    const size_t lds_st = sizeof(float) * ((size_t)P * (hv + 4) + 2 * g.M + 2 * P + 1);
+    if (mf_env && P <= 256 && hv >= 16 && (!nx.wl || lw_mfma_fits(P, hv + 4)) && lds_st <= 80 * 1024) {
+      auto ks = hv == 16 ? lw_stage_attn_fwd_kernel<16> : hv == 24 ? lw_stage_attn_fwd_kernel<24>
+                                                                  : lw_stage_attn_fwd_kernel<32>;
+      if (lds_st > 65536)  // two workgroups still share a CU's 160 KB
+        GSC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(ks),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_st));
+      hipLaunchKernelGGL(ks, dim3(B), dim3(256), lds_st, stream_of(stream), g, ptr<const float>(xl),
+                         ptr<const float>(xr), ptr<const float>(att), ptr<const float>(bias), relu, ptr<float>(h_out),
+                         ptr<float>(alpha), nx, ptr<float>(emb));
+      check_launch();
+      return;
+    }
     const size_t lds = sizeof(float) * ((size_t)P * hv + (nx.wl && !mf ? 2 * H * hv : 0) + 2 * g.M + 2 * P + 1);
     if (lds <= 64 * 1024) {
       auto kl = mf ? (hv == 16 ? lw_lane_attn_fwd_kernel<16, true> : hv == 24 ? lw_lane_attn_fwd_kernel<24, true>
@@ -1388,6 +1853,25 @@ void lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, ui
     const int hv = H <= 8 ? 8 : H <= 16 ? 16 : H <= 24 ? 24 : 32;
     static const bool mf_env = getenv("GSC_LW_MFMA") == nullptr || atoi(getenv("GSC_LW_MFMA")) != 0;
     const bool mf = mf_env && wl && lw_mfma_fits(P, hv);
+    // staged: two row images + fp32 alpha / de + u16 / u8 message indices; 16-B aligned [P][H] blocks
+    const size_t lst = sizeof(float) * (2 * (size_t)P * hv + 2 * g.M + P + 2 * (P + 1)) + 4 * (size_t)g.M;
+    auto al16 = [](uintptr_t p) { return (p & 15) == 0; };
+    const bool blocks16 = ((long)P * H) % 4 == 0 && al16(dh) && al16(xl) && al16(xr) && (!h_out || al16(h_out)) &&
+                          al16(dxr) && al16(datt) && al16(dxl);
+    if (mf_env && P <= 256 && hv >= 16 && g.M < 65536 && blocks16 && (!wl || lw_mfma_fits(P, hv)) &&
+        lst <= 80 * 1024) {
+      auto ks = hv == 16 ? lw_stage_attn_bwd_kernel<16> : hv == 24 ? lw_stage_attn_bwd_kernel<24>
+                                                                  : lw_stage_attn_bwd_kernel<32>;
+      if (lst > 65536)
+        GSC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(ks),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lst));
+      hipLaunchKernelGGL(ks, dim3(B), dim3(256), lst, stream_of(stream), g, ptr<float>(dh), ptr<const float>(h_out),
+                         ptr<const float>(xl), ptr<const float>(xr), ptr<const float>(alpha), ptr<const float>(att),
+                         ptr<float>(dxr), ptr<float>(datt), ptr<float>(dxl), ptr<const float>(wl),
+                         ptr<const float>(wr), ptr<float>(dh_in));
+      check_launch();
+      return;
+    }
     const size_t ll = sizeof(float) * (2 * (size_t)P * hv + (wl && !mf ? 2 * H * hv : 0) + 5 * g.M + P + 2 * (P + 1));
     if (ll <= 80 * 1024) {  // >= 2 workgroups per CU
       auto kl = mf ? (hv == 16 ? lw_lane_attn_bwd_kernel<16, true> : hv == 24 ? lw_lane_attn_bwd_kernel<24, true>

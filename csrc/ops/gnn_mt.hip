@@ -573,7 +573,11 @@ static MtLayout mt_layout(const ClArgs& a, int kind, int HPF) {
   MtLayout m{};
   m.NT = (a.NM + 31) / 32;
   m.NV = 32 * m.NT;
-  m.NVS = m.NV + 16;  // 16-B aligned rows; own-tile rows of E^T (32 x NVS) hold the two dX row images
+  // 16-B aligned rows; own-tile rows of E^T (32 x NVS) hold the two dX row images (NVS >= 80).  The row
+  // stride in 16-B units must be odd: the MFMA operand reads (ds_read_b128, lane r = row r) then hit 16
+  // distinct bank quads per lane group (NV 64: 88, not 80 -- 80 B-quads mod 64 banks repeat every 8 rows)
+  m.NVS = m.NV + 16;
+  if (((m.NVS / 8) & 1) == 0) m.NVS += 8;
   m.MS = a.MP + 8;
   m.hTrows0 = (a.Fin + 3) & ~3;
   m.hTrows = HPF;
@@ -591,7 +595,9 @@ static MtLayout mt_layout(const ClArgs& a, int kind, int HPF) {
     o += (bytes + 15) & ~15;
     return at;
   };
-  const int fb = m.NV * mf_xs(HPF) * 4, M4b = ((a.M + 3) & ~3) * 4;
+  // fp32 row images (x_l, x_r, dy) are read and written per message / per real node only: NM rows, not
+  // NV (keeps the backward at two workgroups per CU with the wider NVS)
+  const int fb = a.NM * mf_xs(HPF) * 4, M4b = ((a.M + 3) & ~3) * 4;
   m.xl = take(fb);
   m.xr = take(fb);
   m.E = take(m.NV * m.NVS * 2);

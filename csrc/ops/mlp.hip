@@ -115,8 +115,21 @@ __device__ __forceinline__ short load_elem(const Operand& o, long r, long c) {
 // four rows of every ds_read_b64_tr_b16 block fall on disjoint bank ranges.
 __host__ __device__ constexpr int tr_stride(int C) { return ((C / 32) % 2 == 1) ? C : C + 32; }
 
+// K-contiguous images are [R][BK] with no row padding; the 16-byte chunk c of row r sits at chunk slot
+// c ^ ((r / RP) & (BK / 8 - 1)), RP = 128 / BK rows per 64 banks.  Fragment reads (ds_read_b128, lane r =
+// row r, all lanes the same chunk) then hit 16 distinct bank quads per lane group -- the 16 rows of a group
+// are distinct mod 16 and (r mod RP, r / RP) spreads them over the 64 banks -- and the staging stores
+// (ds_write_b128, 8 consecutive lanes = 32 contiguous dwords of one or two rows) cover the 32 store banks
+// once.  A padded [R][BK + 8] image (the previous layout) serves the reads conflict-free but puts the
+// second row of every store group on the first row's banks (2-way on every staging store).
+template <int BK>
+__device__ __forceinline__ int rowimg_off(int row, int ch) {
+  constexpr int RP = 128 / BK, CPR = BK / 8;
+  return row * BK + 8 * (ch ^ ((row / RP) & (CPR - 1)));
+}
+
 // Stage one operand tile into LDS.
-//   ROWIMG: image [R][BK + 8] of a K-contiguous operand (rows r0.., k0..)
+//   ROWIMG: image [R][BK] (swizzled chunks, rowimg_off) of a K-contiguous operand (rows r0.., k0..)
 //   !ROWIMG: image [BK][tr_stride(R)] of an M/N-contiguous operand (stored [k][c])
 template <int R, int BK, bool ROWIMG>
 struct Stager {
@@ -168,13 +181,13 @@ struct Stager {
 
   __device__ __forceinline__ void store(short* img, int tid) const {
     constexpr int CPR = ROWIMG ? BK / 8 : R / 8;
-    constexpr int LD = ROWIMG ? BK + 8 : tr_stride(R);
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int idx = tid + 256 * i;
       if (CH % 256 != 0 && idx >= CH) break;
       const int row = idx / CPR, ch = idx % CPR;
-      *reinterpret_cast<s16x8*>(img + row * LD + ch * 8) = reg[i];
+      const int off = ROWIMG ? rowimg_off<BK>(row, ch) : row * tr_stride(R) + ch * 8;
+      *reinterpret_cast<s16x8*>(img + off) = reg[i];
     }
   }
 };
@@ -185,7 +198,7 @@ template <int R, int BK, bool ROWIMG>
 __device__ __forceinline__ s16x8 frag(const short* img, int c0, int s, int lane) {
   if constexpr (ROWIMG) {
     const int r = lane & 31, h = lane >> 5;
-    return *reinterpret_cast<const s16x8*>(img + (c0 + r) * (BK + 8) + 16 * s + 8 * h);
+    return *reinterpret_cast<const s16x8*>(img + rowimg_off<BK>(c0 + r, 2 * s + h));
   } else {
     constexpr int LD = tr_stride(R);
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
@@ -201,9 +214,13 @@ __device__ __forceinline__ s16x8 frag(const short* img, int c0, int s, int lane)
 template <int RM, int RN, int WM, int WN, int BK, bool A_COL, bool B_KN>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   constexpr int BM = 32 * RM * WM, BN = 32 * RN * WN;
-  constexpr int A_ELEMS = A_COL ? BK * tr_stride(BM) : BM * (BK + 8);
-  constexpr int B_ELEMS = B_KN ? BK * tr_stride(BN) : BN * (BK + 8);
-  __shared__ __attribute__((aligned(16))) short smem[2 * (A_ELEMS + B_ELEMS)];
+  constexpr int A_ELEMS = A_COL ? BK * tr_stride(BM) : BM * BK;
+  constexpr int B_ELEMS = B_KN ? BK * tr_stride(BN) : BN * BK;
+  // bf16 epilogue staging: per-wave [32 RM][32 RN] sub-tiles, unpadded (the 16-byte row-chunk reads of the
+  // write-out then cover 64 distinct banks per lane group; a +8 pad put row 3 on row 0's banks)
+  constexpr int LDT = 32 * RN;
+  constexpr int OPS = 2 * (A_ELEMS + B_ELEMS), STG = 4 * (32 * RM) * LDT;
+  __shared__ __attribute__((aligned(16))) short smem[OPS > STG ? OPS : STG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const long m0 = (long)blockIdx.x * BM, n0 = (long)blockIdx.y * BN;
@@ -267,8 +284,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   const int col_l = lane & 31, hh = lane >> 5;
   const bool per_row_topo = (e.rowtab || e.colmask) && !e.single_topo;
   // bf16 output through LDS (per-wave sub-tile, padded rows) when the output rows are 16-byte aligned
-  constexpr int LDT = 32 * RN + 8;
-  static_assert(4 * (32 * RM) * LDT <= 2 * (A_ELEMS + B_ELEMS), "epilogue staging tile exceeds the LDS buffers");
   const bool stage16 = !split && e.c16 && e.vec16;
   short* stile = smem + wave * (32 * RM) * LDT;
   if (stage16) __syncthreads();  // every wave is done reading the operand tiles
