@@ -45,13 +45,14 @@ PRESETS = {
                   model="GSC GATv2-DDPG, 50-node synthetic topology, 3 SFCs, trace traffic (A = 22,500)"),
     # BASELINE config 5 ("scheduler-driven network changes during training"): the network scheduler
     # switches every env to the next topology at every episode end (period 1) and episodes are 20 steps,
-    # so any timed window of more than 20 steps contains a switch (counted in the JSON line).  Learner
-    # batch 16 per env-step: the [B, A] actor output / action gradient at A = 360,000 (three
-    # topologies: not re-associated) bounds it (2.9 GB per bf16 buffer at B = 4,096)
+    # so any timed window of more than 20 steps contains a switch (counted in the JSON line).  256 envs and
+    # the common learner ratio (100 replayed samples per env-step: B = 25,600); the [B, A] action blocks
+    # are never materialised (replay rows read in place by the critic GEMM, composed actor loss, fused
+    # TD-target projection), so A = 360,000 costs HBM bandwidth, not capacity
     "syn200": dict(network=[f"configs/networks/synthetic/syn200-in16-cap1-3-s{i}.graphml" for i in range(3)],
                    service="configs/service_functions/abc-3sfc.yaml",
                    sim_config="configs/config/simulator/sample_config.yaml",
-                   agent_config="configs/config/agent/agent_syn200.yaml", envs=128, batch=2048, period=1,
+                   agent_config="configs/config/agent/agent_syn200.yaml", envs=256, batch=None, period=1,
                    episode_steps=20,
                    model="GSC GATv2-DDPG, 200-node synthetic topologies switched every episode (20 steps), 3 SFCs "
                          "(A = 360,000)"),

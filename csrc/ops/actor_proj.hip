@@ -9,8 +9,11 @@
 // is W and Wa once per XCD instead of writing and re-reading M x A bf16 (1.5 GB at M = 2048,
 // A = 360,000: the materialised path took ~4 ms of the syn200 update).
 //
-// Workgroup = 8 waves over BM = 128 batch rows (4 x 2 waves of 32 x 32 for both products); its H
-// rows stay resident in LDS (K <= 256); it walks a contiguous range of action tiles with the W / Wa
+// Workgroup = 8 waves over BM = 128 batch rows (4 x 2 waves of 32 x 32 for both products); each wave
+// keeps the A fragments of its 32 H rows in registers for the whole walk (K <= 256: 16 fragments), so
+// the first product reads only the W fragment from LDS (two 16-B LDS reads per MFMA with H in LDS put
+// the kernel at the LDS read rate, 256 B/clk/CU, not the MFMA rate); it walks a contiguous range of
+// action tiles with the W / Wa
 // rows of the next PD tiles in flight in a register ring (the stream is latency-bound otherwise:
 // one tile of MFMA work is ~0.5 us, an HBM round trip under load longer).  Grid = row blocks x
 // S splits of the tiles; id = rb S + s with S a multiple of 8, so every row block of split s runs on
@@ -35,7 +38,7 @@ constexpr int BN = 64;   // action columns per tile
 constexpr int NJ = 64;   // critic units (J <= NJ)
 constexpr int NT = 512;  // threads
 constexpr int LDP = BN + 8;
-constexpr int PD = 4;    // tiles in flight (register ring)
+constexpr int PD = 3;    // tiles in flight (register ring; 4 spilled once the H fragments moved to registers)
 
 struct Args {
   const short* h;   // [M][ldh] bf16
@@ -71,55 +74,55 @@ __device__ __forceinline__ s16x8 load_chunk(const short* p, long ld, long r, lon
   return *reinterpret_cast<const s16x8*>(p + r * ld + c0);
 }
 
+constexpr int LDM = BN + 4;  // fp32 row stride of the staged mask rows (T rows: distinct banks)
+
+// LDS bytes of the kernel: W double buffer [2][BN][K + 8] bf16, Wa double buffer [2][NJ][LDP] bf16, bias /
+// mask double buffer [2][(1 + 4) LDM] fp32; the end-of-kernel partial exchange reuses the W buffers
+template <int K>
+constexpr size_t aproj_lds() {
+  return sizeof(short) * (2 * BN * (K + 8) + 2 * NJ * LDP) + sizeof(float) * 2 * 5 * LDM;
+}
+
+// The first product is computed transposed, P^T[n][m] = W[n] . H[m] (A = W rows from LDS, B = the wave's
+// resident H fragments): a lane then owns one batch row m (one topology: one mask row) and 16 action
+// columns n in registers, and those registers ARE the A operand of the second product once the k order
+// of each 16-wide step is permuted to the accumulator's row order (lane half hh holds n = 4 hh + 0..3 and
+// 8 + 4 hh + 0..3; the Wa fragment is read in the same order with two 8-byte LDS reads).  P never goes
+// through LDS: no P stores, no P barrier, and the epilogue is (acc + bias) * mask, clamp, bf16 per element.
+// Each wave (wm, wn) accumulates Z[32 wm + .][0 .. 64) over its 32 columns of every tile; the two wn
+// partials are added in a fixed order at the end (deterministic).
 template <int K>
 __global__ __launch_bounds__(NT) void actor_proj_kernel(Args a) {
   constexpr int LDK = K + 8;
   constexpr int KC = K / 8;                  // 16-byte chunks per row
   constexpr int WCH = BN * KC / NT;          // W tile chunks per thread
   static_assert(BN * KC % NT == 0 && BM * KC % NT == 0, "tile / thread mismatch");
-  __shared__ __attribute__((aligned(16))) short s_h[BM * LDK];
-  __shared__ __attribute__((aligned(16))) short s_w[BN * LDK];
-  __shared__ __attribute__((aligned(16))) short s_p[BM * LDP];
-  __shared__ __attribute__((aligned(16))) short s_wa[2][NJ * LDP];
+  extern __shared__ __attribute__((aligned(16))) short ap_lds[];
+  short* const s_w0 = ap_lds;                                       // [2][BN][LDK]
+  short* const s_wa0 = s_w0 + 2 * BN * LDK;                         // [2][NJ][LDP]
+  float* const s_v0 = reinterpret_cast<float*>(s_wa0 + 2 * NJ * LDP);  // [2][bias | mask t = 0..3][LDM]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  const int hh = lane >> 5, col = lane & 31;
   const int rb = blockIdx.x / a.S, split = blockIdx.x - rb * a.S;
   const long m0 = (long)rb * BM;
   const int t0 = split * a.per_split;
   const int t1 = min(a.tiles, t0 + a.per_split);
 
-  // resident H rows
-  for (int i = tid; i < BM * KC; i += NT) {
-    const int r = i / KC, c = i - r * KC;
-    *reinterpret_cast<s16x8*>(s_h + r * LDK + 8 * c) = load_chunk(a.h, a.ldh, m0 + r, a.M, 8 * c, K);
-  }
-  // topology of this lane's 16 accumulator rows (fixed for the workgroup)
-  const int hh = lane >> 5, col = lane & 31;
-  // packed 2 bits per row, formed before the tile loop (so no wait on these loads inside it)
-  unsigned tpb = 0;
+  // the lane's batch row (B column of the first product, A row of the second) and its topology
+  const long mrow = m0 + 32 * wm + col;
+  const int tp = a.topo[mrow < a.M ? mrow : a.M - 1] & 3;
+  // resident B fragments of the wave's 32 H rows (column m = col, k = 16 s + 8 hh)
+  s16x8 hf[K / 16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const long m = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * hh;
-    tpb |= (unsigned)(a.topo[m < a.M ? m : a.M - 1] & 3) << (2 * r);
-  }
+  for (int s = 0; s < K / 16; ++s) hf[s] = load_chunk(a.h, a.ldh, mrow, a.M, 16 * s + 8 * hh, K);
 
-  // register ring of PD tile stages (W / Wa rows, bias, mask column): tile ti + PD is requested right
-  // after tile ti's P is built and stored to LDS PD - 1 tiles later, so the loads have PD - 1 tiles
-  // of MFMA work to arrive
+  // register ring of PD tile stages: W / Wa chunks; threads < BN also the column's bias and masks
   s16x8 wreg[PD][WCH], areg[PD];
-  float bst[PD], mst[PD][4];
-  bool lst[PD];  // the stage's column is live (applied where the values are used: no wait at the load)
-  // stage d <- tile tt (tt >= t1: a padding tile of the last group, its mask is zero)
+  float vst[PD][5];
   auto load_stage = [&](int d, int tt) {
     const long n0 = (long)(tt < a.tiles ? tt : a.tiles - 1) * BN;
-    const long n = n0 + 32 * wn + col;
-    const long nc = n < a.A ? n : a.A - 1;
-    const bool live = tt < t1 && n < a.A;
-    lst[d] = live;
-    bst[d] = a.bias[nc];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) mst[d][t] = a.mask[(long)(t < a.T ? t : a.T - 1) * a.ldm + nc];
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
       const int idx = tid + NT * i, r = idx / KC, c = idx - r * KC;
@@ -127,77 +130,114 @@ __global__ __launch_bounds__(NT) void actor_proj_kernel(Args a) {
     }
     const int r = tid >> 3, c = tid & 7;  // NJ x 8 chunks = 512
     areg[d] = load_chunk(a.wa, a.ldwa, r, a.J, n0 + 8 * c, a.A8);
+    const long n = n0 + (tid & (BN - 1));
+    const long nc = n < a.A ? n : a.A - 1;
+    vst[d][0] = a.bias[nc];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) vst[d][1 + t] = a.mask[(long)(t < a.T ? t : a.T - 1) * a.ldm + nc];
   };
-  auto store_stage = [&](int d, int buf) {
+  // a padding tile of the last group or a column beyond A gets mask 0 at the store (no wait at the load)
+  auto store_stage = [&](int d, int buf, int tt) {
+    short* sw = s_w0 + buf * BN * LDK;
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
       const int idx = tid + NT * i, r = idx / KC, c = idx - r * KC;
-      *reinterpret_cast<s16x8*>(s_w + r * LDK + 8 * c) = wreg[d][i];
+      *reinterpret_cast<s16x8*>(sw + r * LDK + 8 * c) = wreg[d][i];
     }
     const int r = tid >> 3, c = tid & 7;
-    *reinterpret_cast<s16x8*>(&s_wa[buf][r * LDP + 8 * c]) = areg[d];
-  };
-
-  f32x16 acc2;
+    *reinterpret_cast<s16x8*>(s_wa0 + buf * NJ * LDP + r * LDP + 8 * c) = areg[d];
+    if (tid < BN) {
+      const long n = (long)tt * BN + tid;
+      const bool live = tt < t1 && n < a.A;
+      float* v = s_v0 + buf * 5 * LDM;
+      v[tid] = vst[d][0];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
+      for (int t = 0; t < 4; ++t) v[(1 + t) * LDM + tid] = live ? vst[d][1 + t] : 0.f;
+    }
+  };
+  f32x16 acc2[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc2[j][r] = 0.f;
 
 #pragma unroll
   for (int d = 0; d < PD; ++d) load_stage(d, t0 + d);
-  store_stage(0, 0);
+  store_stage(0, 0, t0);
   __syncthreads();
-  // groups of PD tiles (the last group padded with zero-mask tiles: no branches around loads)
   for (int tb = t0; tb < t1; tb += PD) {
 #pragma unroll
     for (int d = 0; d < PD; ++d) {
       const int ti = tb + d;
-      {
-        const int cur = (ti - t0) & 1;
-        // P tile = epilogue(H W^T) for columns ti * 64 ..
-        f32x16 acc1;
+      const int buf = (ti - t0) & 1;
+      const short* sw = s_w0 + buf * BN * LDK;
+      const short* swa = s_wa0 + buf * NJ * LDP;
+      const float* sv = s_v0 + buf * 5 * LDM;
+      // P^T tile: rows n = 32 wn + (i & 3) + 8 (i >> 2) + 4 hh, column m = col
+      f32x16 acc1;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc1[r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc1[r] = 0.f;
 #pragma unroll
-        for (int s = 0; s < K / 16; ++s) {
-          const s16x8 fa = *reinterpret_cast<const s16x8*>(s_h + (32 * wm + col) * LDK + 16 * s + 8 * hh);
-          const s16x8 fb = *reinterpret_cast<const s16x8*>(s_w + (32 * wn + col) * LDK + 16 * s + 8 * hh);
-          acc1 = mma(fa, fb, acc1);
-        }
-        const float bn = bst[d];
-        const float mz0 = lst[d] ? mst[d][0] : 0.f, mz1 = lst[d] ? mst[d][1] : 0.f;
-        const float mz2 = lst[d] ? mst[d][2] : 0.f, mz3 = lst[d] ? mst[d][3] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          // two-level select on the topology bits (v_cndmask, no branches); topologies < T only
-          const bool b0 = (tpb >> (2 * r)) & 1, b1 = (tpb >> (2 * r)) & 2;
-          const float mlo = b0 ? mz1 : mz0, mhi = b0 ? mz3 : mz2;
-          const float m = b1 ? mhi : mlo;
-          float v = (acc1[r] + bn) * m;
-          v = fminf(fmaxf(v, a.lo), a.hi);
-          s_p[row * LDP + 32 * wn + col] = f2bf(v);
-        }
-        __syncthreads();  // P complete; every wave is done reading s_w
-        store_stage((d + 1) % PD, cur ^ 1);
-        load_stage(d, ti + PD);
-        // Z += P Wa^T over the tile's 64 columns
-#pragma unroll
-        for (int s = 0; s < BN / 16; ++s) {
-          const s16x8 fa = *reinterpret_cast<const s16x8*>(s_p + (32 * wm + col) * LDP + 16 * s + 8 * hh);
-          const s16x8 fb = *reinterpret_cast<const s16x8*>(&s_wa[cur][(32 * wn + col) * LDP + 16 * s + 8 * hh]);
-          acc2 = mma(fa, fb, acc2);
-        }
-        __syncthreads();  // done with P / Wa[cur]; the next tile's W / Wa are visible
+      for (int s = 0; s < K / 16; ++s) {
+        const s16x8 fw = *reinterpret_cast<const s16x8*>(sw + (32 * wn + col) * LDK + 16 * s + 8 * hh);
+        acc1 = mma(fw, hf[s], acc1);
       }
+      // epilogue in registers: (acc + bias[n]) * mask[tp][n], clamp, bf16 -> the second product's A operand
+      s16x8 pa[2];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int nb = 32 * wn + 8 * q + 4 * hh;
+        const float4 bv = *reinterpret_cast<const float4*>(sv + nb);
+        const float4 mv = *reinterpret_cast<const float4*>(sv + (1 + tp) * LDM + nb);
+        const float bb[4] = {bv.x, bv.y, bv.z, bv.w}, mm[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = (acc1[4 * q + e] + bb[e]) * mm[e];
+          v = fminf(fmaxf(v, a.lo), a.hi);
+          pa[q >> 1][4 * (q & 1) + e] = f2bf(v);
+        }
+      }
+      // Z[m][j] += sum_n P[m][n] Wa[j][n] over the wave's 32 columns (k order = the accumulator's row order)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          const short* wr = swa + (32 * jb + col) * LDP + 32 * wn + 16 * s2 + 4 * hh;
+          typedef __attribute__((ext_vector_type(4))) short s16x4;
+          const s16x4 lo4 = *reinterpret_cast<const s16x4*>(wr);
+          const s16x4 hi4 = *reinterpret_cast<const s16x4*>(wr + 8);
+          const s16x8 fb = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+          acc2[jb] = mma(pa[s2], fb, acc2[jb]);
+        }
+      }
+      // tile ti + 1 into the other buffers (last read by tile ti - 1, before the previous barrier)
+      store_stage((d + 1) % PD, buf ^ 1, ti + 1);
+      load_stage(d, ti + PD);
+      __syncthreads();
     }
   }
-  // partial Z of this split
-  float* out = a.slabs + (long)split * a.M * a.J;
-  const int j = 32 * wn + col;
+  // the two wn halves of every Z row block: wn = 1 parks its partial in LDS, wn = 0 adds it (fixed order)
+  float* xch = reinterpret_cast<float*>(ap_lds) + wm * 32 * 64;  // [4][32 m][64 j] over the W buffers
+  if (wn == 1) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const long m = m0 + 32 * wm + (r & 3) + 8 * (r >> 2) + 4 * hh;
-    if (m < a.M && j < a.J) out[m * a.J + j] = acc2[r];
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xch[((r & 3) + 8 * (r >> 2) + 4 * hh) * 64 + 32 * jb + col] = acc2[jb][r];
+  }
+  __syncthreads();
+  if (wn == 0) {
+    float* out = a.slabs + (long)split * a.M * a.J;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      const int j = 32 * jb + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mr = (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const long m = m0 + 32 * wm + mr;
+        const float v = acc2[jb][r] + xch[mr * 64 + j];
+        if (m < a.M && j < a.J) out[m * a.J + j] = v;
+      }
+    }
   }
 }
 
@@ -252,9 +292,18 @@ int actor_proj(uintptr_t h, long ldh, uintptr_t w, long ldw, uintptr_t bias, uin
   a.hi = hi;
   const hipStream_t s = stream_of(stream);
   const dim3 grid((unsigned)(rbs * S));
-  if (K == 256) hipLaunchKernelGGL(actor_proj_kernel<256>, grid, dim3(NT), 0, s, a);
-  else if (K == 128) hipLaunchKernelGGL(actor_proj_kernel<128>, grid, dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL(actor_proj_kernel<64>, grid, dim3(NT), 0, s, a);
+  static bool attr[3] = {false, false, false};  // > 64 KB of dynamic LDS: opted in once per width
+  auto go = [&](auto kern, size_t lds, int slot) {
+    if (!attr[slot]) {
+      GSC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)lds));
+      attr[slot] = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(NT), lds, s, a);
+  };
+  if (K == 256) go(actor_proj_kernel<256>, aproj_lds<256>(), 0);
+  else if (K == 128) go(actor_proj_kernel<128>, aproj_lds<128>(), 1);
+  else go(actor_proj_kernel<64>, aproj_lds<64>(), 2);
   check_launch();
   splitk_reduce_fwd(slabs, (long)M * J, S, M, J, J, z, ldz, 1.f, 0, stream);
   return S;

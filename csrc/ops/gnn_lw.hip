@@ -562,7 +562,7 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
   const int NE = P * H, i = threadIdx.x;
   const int n = g.nnodes[t];
   const bool vec = (NE & 3) == 0 && ((reinterpret_cast<uintptr_t>(xl + base) & 15) == 0) &&
-                   ((reinterpret_cast<uintptr_t>(h_out + base) & 15) == 0);
+                   (!h_out || (reinterpret_cast<uintptr_t>(h_out + base) & 15) == 0);
   // ---- all loads in flight together
   float4 v4[kV];
   if (vec) {
@@ -676,13 +676,16 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
     }
   }
   __syncthreads();  // every lane is done gathering x_l rows: the output rows take their place
-  if (i < P) {
-    float4* ro = reinterpret_cast<float4*>(s_xl + i * RS);
+  if (h_out) {        // (null: a forward without a backward, or the last conv -- nobody reads the rows)
+    if (i < P) {
+      float4* ro = reinterpret_cast<float4*>(s_xl + i * RS);
 #pragma unroll
-    for (int v = 0; v < HV / 4; ++v) ro[v] = make_float4(y[4 * v], y[4 * v + 1], y[4 * v + 2], y[4 * v + 3]);
+      for (int v = 0; v < HV / 4; ++v) ro[v] = make_float4(y[4 * v], y[4 * v + 1], y[4 * v + 2], y[4 * v + 3]);
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (vec) {  // coalesced 16-B stores of the [P][H] block
+  if (!h_out) {
+  } else if (vec) {  // coalesced 16-B stores of the [P][H] block
     float4* o4 = reinterpret_cast<float4*>(h_out + base);
     for (int j = i; j < NE / 4; j += 256) {
       int r = (4 * j) / H, c = 4 * j - r * H;
@@ -700,8 +703,10 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
       h_out[base + k] = s_xl[r * RS + c];
     }
   }
-  const int m = iptr[n];
-  for (int q = i; q < m; q += 256) alpha[(long)b * M + q] = s_sc[q];
+  if (alpha) {
+    const int m = iptr[n];
+    for (int q = i; q < m; q += 256) alpha[(long)b * M + q] = s_sc[q];
+  }
   if (emb) {  // mean pool: lane partial sums reduced in a fixed shuffle / wave order
     const int lane = i & 63, w = i >> 6;
 #pragma unroll
@@ -1323,7 +1328,9 @@ __global__ __launch_bounds__(256, HV <= 24 ? 3 : 2) void lw_stage_attn_bwd_kerne
                                                                    const float* __restrict__ att, float* __restrict__ dxr,
                                                                    float* __restrict__ datt, float* __restrict__ dxl,
                                                                    const float* __restrict__ wl,
-                                                                   const float* __restrict__ wr, float* __restrict__ dh_in) {
+                                                                   const float* __restrict__ wr, float* __restrict__ dh_in,
+                                                                   float* __restrict__ vpart) {
+  // vpart (optional, [B][H]): the graph's d att row sum instead of the d att rows (lw_conv_grads_v)
   // LDS: rows [P][HV] (x_l, then x_r, then outputs), g [P][HV], alpha, de [M] (fp32), deg [P], in_ptr / out_ptr
   //      [P+1], out_q [M] (u16), in_src / target [M] (u8)
   constexpr int KV = HV / 4;  // 16-B vectors per thread of a [P][H] block (P H <= 256 HV)
@@ -1488,7 +1495,22 @@ __global__ __launch_bounds__(256, HV <= 24 ? 3 : 2) void lw_stage_attn_bwd_kerne
   __syncthreads();
   if (i < P) lw_put_row<HV>(s_rows, i, d2);
   __syncthreads();
-  lw_lds_to_block<HV>(datt + base, s_rows, NE, H);
+  if (vpart) {  // column sums of the d att rows in a fixed order (8 row groups, then the groups)
+    const int c = i & 31, gq = i >> 5;
+    float cs = 0.f;
+    if (c < H)
+      for (int r = gq; r < P; r += 8) cs += s_rows[r * HV + c];
+    s_g[i] = cs;  // the g image is free (copied out above)
+    __syncthreads();
+    if (i < H) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v += s_g[32 * q + i];
+      vpart[(long)b * H + i] = v;
+    }
+  } else {
+    lw_lds_to_block<HV>(datt + base, s_rows, NE, H);
+  }
   if (wl) {  // input gradient d x_l W_l + d x_r W_r on the matrix cores (bf16 images over the row images)
     __syncthreads();
     __bf16* img_l = reinterpret_cast<__bf16*>(s_rows);
@@ -1547,18 +1569,33 @@ __global__ __launch_bounds__(256) void lw_node_linear_kernel(const float* __rest
                                                              const float* __restrict__ wl, const float* __restrict__ bl,
                                                              const float* __restrict__ wr, const float* __restrict__ br,
                                                              float* __restrict__ xl, float* __restrict__ xr) {
-  const long total = R * H;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / H;
-    const int c = (int)(i - r * H);
-    float a = bl[c], b = br[c];
-    for (int k = 0; k < Fi; ++k) {
-      const float v = x[r * Fi + k];
-      a += wl[c * Fi + k] * v;
-      b += wr[c * Fi + k] * v;
+  // 8 rows x 32 channel lanes (4 x 64 for H > 32) per block step (no per-element 64-bit division); the
+  // lane's weight rows stay in registers (Fi <= 8); consecutive lanes write consecutive channels of a row
+  const int lpr = H <= 32 ? 32 : 64, rps = 256 / lpr;
+  const int c = threadIdx.x % lpr, rl = threadIdx.x / lpr;
+  const bool on = c < H;
+  const int cc = on ? c : 0;
+  float wlr[8], wrr[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    wlr[k] = k < Fi ? wl[cc * Fi + k] : 0.f;
+    wrr[k] = k < Fi ? wr[cc * Fi + k] : 0.f;
+  }
+  const float b0 = bl[cc], b1 = br[cc];
+  for (long r = (long)blockIdx.x * rps + rl; r < R; r += (long)gridDim.x * rps) {
+    float a = b0, b = b1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < Fi) {
+        const float v = x[r * Fi + k];
+        a = fmaf(wlr[k], v, a);
+        b = fmaf(wrr[k], v, b);
+      }
     }
-    xl[i] = a;
-    xr[i] = b;
+    if (on) {
+      xl[r * H + c] = a;
+      xr[r * H + c] = b;
+    }
   }
 }
 
@@ -1706,6 +1743,118 @@ __global__ __launch_bounds__(256) void lw_conv_grads_mfma_kernel(const float* __
   }
 }
 
+// Conv parameter gradients streamed from HBM (H <= 32, Fi <= 31): dW = dX^T h on the matrix cores with the
+// A / B fragments loaded straight from the row-major [R][H] / [R][Fi] blocks (lane c = channel, 8 rows per
+// lane half) and h extended by a ones column (k = Fi), so the same MFMA also yields the bias sums of d x_l /
+// d x_r; the d bias sum of dY on the VALU.  Each wave walks 16-row steps of its workgroup's contiguous row
+// range with the next step's loads in flight (no LDS staging round trip per step); the 4 waves' tiles are
+// combined in a fixed order into one partial row per workgroup [dW_l | db_l | dW_r | db_r | 0 | d bias]
+// (d att comes from the attention backward's per-graph sums).  Deterministic.
+__global__ __launch_bounds__(256) void lw_conv_grads_stream_kernel(const float* __restrict__ dxl,
+                                                                   const float* __restrict__ dxr,
+                                                                   const float* __restrict__ dy,
+                                                                   const float* __restrict__ hin, long R, int H, int Fi,
+                                                                   long rows_per_blk, float* __restrict__ part) {
+  __shared__ float red[4][2][32][33];
+  __shared__ float redb[4][32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, hh = lane >> 5;
+  const long r0 = (long)blockIdx.x * rows_per_blk;
+  const long r1 = r0 + rows_per_blk < R ? r0 + rows_per_blk : R;
+  f32x16 gl, gr;
+  mf_zero(gl);
+  mf_zero(gr);
+  float vb = 0.f;
+  const bool ch = c < H, hk = c < Fi, one = c == Fi;
+  // every load issued unconditionally at a clamped address into raw registers; the range masks are applied
+  // where the values are consumed (a branch around a load, or a select right after it, made the compiler
+  // wait for the outstanding loads there: one step in flight)
+  const int cc = ch ? c : H - 1, ck = hk ? c : Fi - 1;
+  auto load = [&](long rs, float (&l)[8], float (&q)[8], float (&h)[8], float (&y)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      long v = rs + 8 * hh + j;
+      v = v < r1 ? v : r1 - 1;
+      l[j] = dxl[v * H + cc];
+      q[j] = dxr[v * H + cc];
+      y[j] = dy[v * H + cc];
+      h[j] = hin[v * Fi + ck];
+    }
+  };
+  auto step = [&](long rs, const float (&l)[8], const float (&q)[8], const float (&h)[8], const float (&y)[8]) {
+    bf16x8 al, ar, bh;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool in = rs + 8 * hh + j < r1;
+      al[j] = (__bf16)((in && ch) ? l[j] : 0.f);
+      ar[j] = (__bf16)((in && ch) ? q[j] : 0.f);
+      bh[j] = (__bf16)(in ? (hk ? h[j] : (one ? 1.f : 0.f)) : 0.f);
+      vb += (in && ch) ? y[j] : 0.f;
+    }
+    gl = mf_mma(al, bh, gl);
+    gr = mf_mma(ar, bh, gr);
+  };
+  // two register sets in a ping-pong: one step computes while the next step's loads are in flight (loads past
+  // the range read the last row again and are masked off)
+  float l0[8], q0[8], h0[8], y0[8], l1[8], q1[8], h1[8], y1[8];
+  long rs = r0 + 16 * w;
+  load(rs, l0, q0, h0, y0);
+  for (; rs < r1; rs += 128) {
+    load(rs + 64, l1, q1, h1, y1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the conversions the scheduler would hoist
+    step(rs, l0, q0, h0, y0);
+    load(rs + 128, l0, q0, h0, y0);
+    __builtin_amdgcn_sched_barrier(0);
+    step(rs + 64, l1, q1, h1, y1);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = mf_row(i, hh);  // output channel (A row); column c = h column k
+    red[w][0][row][c] = gl[i];
+    red[w][1][row][c] = gr[i];
+  }
+  vb += __shfl_xor(vb, 32);
+  if (hh == 0) redb[w][c] = vb;
+  __syncthreads();
+  const int HF = H * Fi, C = 2 * HF + 4 * H;
+  for (int o = tid; o < C; o += 256) {
+    float v = 0.f;
+    if (o < 2 * HF + 2 * H) {
+      const int side = o >= HF + H, oo = o - side * (HF + H);
+      const int chn = oo < HF ? oo / Fi : oo - HF, k = oo < HF ? oo - (oo / Fi) * Fi : Fi;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) v += red[ww][side][chn][k];
+    } else if (o >= 2 * HF + 3 * H) {
+      const int chn = o - 2 * HF - 3 * H;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) v += redb[ww][chn];
+    }
+    part[(long)blockIdx.x * C + o] = v;
+  }
+}
+
+void lw_colsum(uintptr_t x, long R, int C, long ldx, uintptr_t part, uintptr_t out, int accumulate, uintptr_t stream);
+
+// part >= 1024 (2 H Fi + 4 H) floats, vpart [B][H] per-graph d att sums (lw_attn_bwd_gather), vscr >= 1024 H
+void lw_conv_grads_v(uintptr_t dxl, uintptr_t dxr, uintptr_t dy, uintptr_t hin, long R, int H, int Fi, uintptr_t part,
+                     long part_floats, uintptr_t out, int accumulate, uintptr_t vpart, int B, uintptr_t vscr,
+                     uintptr_t stream) {
+  GSC_CHECK(H <= 32 && Fi <= 31, "lw_conv_grads_v: H <= 32, Fi <= 31");
+  const int C = 2 * H * Fi + 4 * H;
+  long rpb = (R + 1023) / 1024;
+  rpb = (rpb + 63) / 64 * 64;
+  const int K = (int)((R + rpb - 1) / rpb);
+  GSC_CHECK((long)K * C <= part_floats, "lw_conv_grads_v: partials buffer too small");
+  const hipStream_t s = stream_of(stream);
+  hipLaunchKernelGGL(lw_conv_grads_stream_kernel, dim3(K), dim3(256), 0, s, ptr<const float>(dxl),
+                     ptr<const float>(dxr), ptr<const float>(dy), ptr<const float>(hin), R, H, Fi, rpb, ptr<float>(part));
+  check_launch();
+  hipLaunchKernelGGL(lw_colsum_p2_kernel, dim3(C), dim3(256), 0, s, ptr<const float>(part), K, C, ptr<float>(out),
+                     accumulate);
+  check_launch();
+  // d att: the per-graph sums on top (the partial rows carry zeros there)
+  lw_colsum(vpart, B, H, H, vscr, out + sizeof(float) * (2 * H * Fi + 2 * H), 1, stream);
+}
+
 // ---------------------------------------------------------------------------------------------------
 static LwGraph lw_graph(py::dict t, uintptr_t topo, int B, int P, int H) {
   LwGraph g{};
@@ -1735,9 +1884,11 @@ static dim3 node_grid(const LwGraph& g) {
 void lw_pool(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t h, uintptr_t emb, uintptr_t stream);
 
 // emb (last conv, optional): also the mean pool into emb [B][H] (fused on the lane-per-node path)
+// store: bit 0 = the output rows h_out, bit 1 = alpha are needed (a later backward); the staged kernel skips
+// the others, the other kernels always write both
 void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t xl, uintptr_t xr, uintptr_t att,
                  uintptr_t bias, int relu, uintptr_t h_out, uintptr_t alpha, uintptr_t stream, py::tuple next,
-                 uintptr_t emb) {
+                 uintptr_t emb, int store) {
   const LwGraph g = lw_graph(tables, topo, B, P, H);
   LwNext nx{};
   if (next.size() == 6) {
@@ -1764,8 +1915,9 @@ void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
         GSC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(ks),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_st));
       hipLaunchKernelGGL(ks, dim3(B), dim3(256), lds_st, stream_of(stream), g, ptr<const float>(xl),
-                         ptr<const float>(xr), ptr<const float>(att), ptr<const float>(bias), relu, ptr<float>(h_out),
-                         ptr<float>(alpha), nx, ptr<float>(emb));
+                         ptr<const float>(xr), ptr<const float>(att), ptr<const float>(bias), relu,
+                         (store & 1) ? ptr<float>(h_out) : nullptr, (store & 2) ? ptr<float>(alpha) : nullptr, nx,
+                         ptr<float>(emb));
       check_launch();
       return;
     }
@@ -1844,9 +1996,11 @@ void lw_src_gather(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr
 
 // attention backward + source gather (+ input gradient when wl): one per-graph launch when the
 // graph's x_l block fits the LDS budget, else the per-node kernels
-void lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t dh, uintptr_t h_out, uintptr_t xl,
+// vpart (optional, [B][H]): the staged kernel writes per-graph d att sums there instead of the d att rows;
+// returns whether it did (else the rows are in datt)
+bool lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t dh, uintptr_t h_out, uintptr_t xl,
                         uintptr_t xr, uintptr_t alpha, uintptr_t att, uintptr_t dxr, uintptr_t msg, uintptr_t datt,
-                        uintptr_t dxl, uintptr_t wl, uintptr_t wr, uintptr_t dh_in, uintptr_t stream) {
+                        uintptr_t dxl, uintptr_t wl, uintptr_t wr, uintptr_t dh_in, uintptr_t stream, uintptr_t vpart) {
   const LwGraph g = lw_graph(tables, topo, B, P, H);
   GSC_CHECK(!wl || (wr && dh_in), "lw_attn_bwd_gather: the input gradient needs wl, wr, dh_in");
   if (H <= 32) {  // lane per node
@@ -1868,9 +2022,9 @@ void lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, ui
       hipLaunchKernelGGL(ks, dim3(B), dim3(256), lst, stream_of(stream), g, ptr<float>(dh), ptr<const float>(h_out),
                          ptr<const float>(xl), ptr<const float>(xr), ptr<const float>(alpha), ptr<const float>(att),
                          ptr<float>(dxr), ptr<float>(datt), ptr<float>(dxl), ptr<const float>(wl),
-                         ptr<const float>(wr), ptr<float>(dh_in));
+                         ptr<const float>(wr), ptr<float>(dh_in), ptr<float>(vpart));
       check_launch();
-      return;
+      return vpart != 0;
     }
     const size_t ll = sizeof(float) * (2 * (size_t)P * hv + (wl && !mf ? 2 * H * hv : 0) + 5 * g.M + P + 2 * (P + 1));
     if (ll <= 80 * 1024) {  // >= 2 workgroups per CU
@@ -1884,7 +2038,7 @@ void lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, ui
                          ptr<float>(dxr), ptr<float>(datt), ptr<float>(dxl), ptr<const float>(wl),
                          ptr<const float>(wr), ptr<float>(dh_in));
       check_launch();
-      return;
+      return false;
     }
   }
   const size_t lds = sizeof(float) * ((size_t)P * H + (wl ? 2 * H * H : 0) + g.M + P + 2 * (P + 1) + 2 * g.M);
@@ -1895,10 +2049,11 @@ void lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, ui
                        ptr<float>(dxr), ptr<float>(msg), ptr<float>(datt), ptr<float>(dxl), ptr<const float>(wl),
                        ptr<const float>(wr), ptr<float>(dh_in));
     check_launch();
-    return;
+    return false;
   }
   lw_attn_bwd(tables, topo, B, P, H, dh, h_out, xl, xr, alpha, att, dxr, msg, datt, stream);
   lw_src_gather(tables, topo, B, P, H, msg, dxl, stream, dxr, wl, wr, dh_in);
+  return false;
 }
 
 void lw_relu_mask(uintptr_t dh, uintptr_t h, long n, uintptr_t stream) {
@@ -1921,8 +2076,9 @@ void lw_colsum(uintptr_t x, long R, int C, long ldx, uintptr_t part, uintptr_t o
 
 void lw_node_linear(uintptr_t x, long R, int Fi, int H, uintptr_t wl, uintptr_t bl, uintptr_t wr, uintptr_t br,
                     uintptr_t xl, uintptr_t xr, uintptr_t stream) {
-  long g = (R * H + 255) / 256;
-  if (g > 8192) g = 8192;
+  GSC_CHECK(Fi <= 8 && H <= 64, "lw_node_linear: Fi <= 8, H <= 64");
+  long g = (R + 3) / 4;
+  if (g > 16384) g = 16384;
   hipLaunchKernelGGL(lw_node_linear_kernel, dim3((unsigned)g), dim3(256), 0, stream_of(stream), ptr<const float>(x), R, Fi,
                      H, ptr<const float>(wl), ptr<const float>(bl), ptr<const float>(wr), ptr<const float>(br),
                      ptr<float>(xl), ptr<float>(xr));
@@ -1977,7 +2133,7 @@ void register_gnn_lw(py::module_& m) {
   m.def("lw_attn_fwd", &lw_attn_fwd, "layer-wise GATv2: attention + aggregation (+ReLU), alpha saved; optionally "
         "the next conv's node linears", py::arg("tables"), py::arg("topo"), py::arg("B"), py::arg("P"), py::arg("H"),
         py::arg("xl"), py::arg("xr"), py::arg("att"), py::arg("bias"), py::arg("relu"), py::arg("h_out"),
-        py::arg("alpha"), py::arg("stream"), py::arg("next") = py::tuple(), py::arg("emb") = 0);
+        py::arg("alpha"), py::arg("stream"), py::arg("next") = py::tuple(), py::arg("emb") = 0, py::arg("store") = 3);
   m.def("lw_pool", &lw_pool, "layer-wise GATv2: mean pool over real nodes");
   m.def("lw_pool_bwd", &lw_pool_bwd, "layer-wise GATv2: mean-pool backward");
   m.def("lw_attn_bwd", &lw_attn_bwd, "layer-wise GATv2: attention backward per target node");
@@ -1986,7 +2142,13 @@ void register_gnn_lw(py::module_& m) {
         py::arg("stream"), py::arg("dxr") = 0, py::arg("wl") = 0, py::arg("wr") = 0, py::arg("dh") = 0);
   m.def("lw_relu_mask", &lw_relu_mask, "dh *= (h > 0)");
   m.def("lw_attn_bwd_gather", &lw_attn_bwd_gather,
-        "layer-wise GATv2: attention backward + source gather (+ input gradient), per graph when it fits");
+        "layer-wise GATv2: attention backward + source gather (+ input gradient), per graph when it fits; "
+        "returns whether vpart holds the per-graph d att sums", py::arg("tables"), py::arg("topo"), py::arg("B"),
+        py::arg("P"), py::arg("H"), py::arg("dh"), py::arg("h_out"), py::arg("xl"), py::arg("xr"), py::arg("alpha"),
+        py::arg("att"), py::arg("dxr"), py::arg("msg"), py::arg("datt"), py::arg("dxl"), py::arg("wl"), py::arg("wr"),
+        py::arg("dh_in"), py::arg("stream"), py::arg("vpart") = 0);
+  m.def("lw_conv_grads_v", &lw_conv_grads_v, "layer-wise GATv2: conv parameter gradients, streamed (MFMA dW with "
+        "a ones column for the bias sums), d att from per-graph sums");
   m.def("lw_colsum", &lw_colsum, "deterministic column sums (two phases)");
 }
 

@@ -204,7 +204,7 @@ class NativeDDPGUpdate:
     def _gnn_fwd(self, net: _Net, x: torch.Tensor, out: torch.Tensor, save: Optional[torch.Tensor],
                  key: str = "-") -> None:
         if self.layerwise:
-            self.lwo[key].forward(net.fp.flat[:self.ne], x, self.topo32, out)
+            self.lwo[key].forward(net.fp.flat[:self.ne], x, self.topo32, out, save=key != "-")
             return
         self.nat.gnn_forward(self.tables, net.emb_ptr(), x.data_ptr(), self.topo32.data_ptr(), out.data_ptr(), self.B,
                              self.P, self.Fin, self.H, self.layer_of, self._stream(),
@@ -511,7 +511,7 @@ class NativeAct:
             self.topo32.copy_(topo)
             self._topo_ref, self._topo_ver = topo, topo._version
         if self.lw is not None:
-            self.lw.forward(n.fp.flat[:self.ne], obs, self.topo32, self.emb)
+            self.lw.forward(n.fp.flat[:self.ne], obs, self.topo32, self.emb, save=False)
         else:
             self.nat.gnn_forward(self.tables, n.emb_ptr(), obs.data_ptr(), self.topo32.data_ptr(), self.emb.data_ptr(),
                                  self.E, self.P, self.Fin, self.H, self.layer_of, s, 0)

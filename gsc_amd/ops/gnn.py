@@ -148,7 +148,7 @@ class _GnnEmbedLW(torch.autograd.Function):
         need = grad_mode and any(ctx.needs_input_grad[4:])
         lw = _lw(graphs, B, P, Fin, H, layer_of, x.device, fresh=need)
         emb = torch.empty(B, H, device=x.device, dtype=torch.float32)
-        lw.forward(flat, x, topo32, emb)
+        lw.forward(flat, x, topo32, emb, save=need)
         ctx.lw, ctx.flat, ctx.shapes = lw, flat, [p.shape for p in params]
         ctx.keep = (x, topo32)  # the saved forward references them
         return emb

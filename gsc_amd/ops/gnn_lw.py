@@ -18,6 +18,8 @@ from __future__ import annotations
 
 from typing import List
 
+import os
+
 import torch
 
 from gsc_amd.native import load as load_native
@@ -55,6 +57,7 @@ class LayerwiseGAT:
         self.msg = mk(self.B * M, H)
         self.part = mk(1024 * max(H, 32))
         self.part_conv = mk(1024 * (2 * H * max(H, Fin) + 4 * H))   # per-block partials of lw_conv_grads
+        self.vpart = mk(self.B, H)                                    # per-graph d att sums (staged backward)
         self.slabs = mk(max(4 << 20, 64 * H * max(H, Fin)))
         self.topo32 = None
 
@@ -82,8 +85,11 @@ class LayerwiseGAT:
         bias = flat[o:o + H]
         return Fi, Wl, bl, Wr, br, att, bias
 
-    def forward(self, flat: torch.Tensor, x: torch.Tensor, topo32: torch.Tensor, emb: torch.Tensor) -> None:
-        """flat: fp32 embedder parameters (module order); x [B, P, Fin] fp32; topo32 [B] int32; emb [B, H]."""
+    def forward(self, flat: torch.Tensor, x: torch.Tensor, topo32: torch.Tensor, emb: torch.Tensor,
+                save: bool = True) -> None:
+        """flat: fp32 embedder parameters (module order); x [B, P, Fin] fp32; topo32 [B] int32; emb [B, H].
+        save=False: no backward follows -- the staged kernels skip the per-conv output rows and alpha (the
+        last conv's rows are read only as a ReLU gate, i.e. by a single-conv embedder)."""
         B, P, H = self.B, self.P, self.H
         assert x.shape == (B, P, self.Fin) and x.is_contiguous() and x.dtype == torch.float32
         assert topo32.dtype == torch.int32 and topo32.numel() == B
@@ -106,7 +112,8 @@ class LayerwiseGAT:
                        self.xr[l + 1].data_ptr())
             nat.lw_attn_fwd(t, topo32.data_ptr(), B, P, H, self.xl[l].data_ptr(), self.xr[l].data_ptr(),
                             att.data_ptr(), bias.data_ptr(), int(self._relu(l)), self.hout[l].data_ptr(),
-                            self.alpha[l].data_ptr(), s, nxt, emb.data_ptr() if l + 1 == self.L else 0)
+                            self.alpha[l].data_ptr(), s, nxt, emb.data_ptr() if l + 1 == self.L else 0,
+                            store=(1 if save and (l + 1 < self.L or self._relu(l)) else 0) | (2 if save else 0))
             h = self.hout[l]   # the last conv also writes the mean pool into emb
 
     def backward(self, flat: torch.Tensor, demb: torch.Tensor, grad: torch.Tensor) -> None:
@@ -125,15 +132,24 @@ class LayerwiseGAT:
             seen.add(blk)
             hin = self.x.view(R, self.Fin) if l == 0 else self.hout[l - 1]
             # attention backward + d x_l gather; l > 0: also the input gradient dxl W_l + dxr W_r into nxt
-            nat.lw_attn_bwd_gather(t, tp, B, P, H, cur.data_ptr(), self.hout[l].data_ptr() if self._relu(l) else 0,
-                                   self.xl[l].data_ptr(), self.xr[l].data_ptr(), self.alpha[l].data_ptr(),
-                                   att.data_ptr(), self.dxr.data_ptr(), self.msg.data_ptr(), self.datt.data_ptr(),
-                                   self.dxl.data_ptr(), Wl.data_ptr() if l > 0 else 0, Wr.data_ptr() if l > 0 else 0,
-                                   nxt.data_ptr() if l > 0 else 0, s)
+            # per-graph d att sums instead of [R, H] d att rows when the streamed gradient kernel applies
+            stream_ok = H <= 32 and Fi <= 31 and os.environ.get("GSC_LW_STREAM_GRADS", "1") != "0"
+            vsum = nat.lw_attn_bwd_gather(t, tp, B, P, H, cur.data_ptr(),
+                                          self.hout[l].data_ptr() if self._relu(l) else 0,
+                                          self.xl[l].data_ptr(), self.xr[l].data_ptr(), self.alpha[l].data_ptr(),
+                                          att.data_ptr(), self.dxr.data_ptr(), self.msg.data_ptr(),
+                                          self.datt.data_ptr(), self.dxl.data_ptr(), Wl.data_ptr() if l > 0 else 0,
+                                          Wr.data_ptr() if l > 0 else 0, nxt.data_ptr() if l > 0 else 0, s,
+                                          vpart=self.vpart.data_ptr() if stream_ok else 0)
             # dW_l | db_l | dW_r | db_r | d att | d bias in one pass (the block's layout in the flat gradient)
             assert gWl.data_ptr() == grad.data_ptr() + 4 * _block_offset(blk, self.Fin, H)
-            nat.lw_conv_grads(self.dxl.data_ptr(), self.dxr.data_ptr(), self.datt.data_ptr(), cur.data_ptr(),
-                              hin.data_ptr(), R, H, Fi, self.part_conv.data_ptr(), self.part_conv.numel(),
-                              gWl.data_ptr(), int(acc), s)
+            if vsum:
+                nat.lw_conv_grads_v(self.dxl.data_ptr(), self.dxr.data_ptr(), cur.data_ptr(), hin.data_ptr(), R, H, Fi,
+                                    self.part_conv.data_ptr(), self.part_conv.numel(), gWl.data_ptr(), int(acc),
+                                    self.vpart.data_ptr(), B, self.part.data_ptr(), s)
+            else:
+                nat.lw_conv_grads(self.dxl.data_ptr(), self.dxr.data_ptr(), self.datt.data_ptr(), cur.data_ptr(),
+                                  hin.data_ptr(), R, H, Fi, self.part_conv.data_ptr(), self.part_conv.numel(),
+                                  gWl.data_ptr(), int(acc), s)
             if l > 0:
                 cur, nxt = nxt, cur
