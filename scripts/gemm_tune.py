@@ -2,9 +2,10 @@
 """Time the MFMA GEMM engine (csrc/ops/mlp.hip) at the DDPG learner's shapes for every output tile x
 K-stage depth, next to hipBLASLt (torch.mm) as a yardstick.
 
-    python scripts/gemm_tune.py [abilene|syn200]
+    python scripts/gemm_tune.py [abilene|syn200] [B]
 
-abilene: B = 25,600, A = 1,728 (sample agent); syn200: B = 2,048, A = 360,000, 3 topologies (config 5)."""
+abilene: B = 25,600, A = 1,728 (sample agent); syn200: A = 360,000, 3 topologies (config 5), B = 25,600 (the
+preset's 100 samples per env-step at 256 envs) unless given."""
 import os
 import sys
 
@@ -41,7 +42,7 @@ if PRESET == "abilene":
         ("dX  [B,64]x[64,256] -> bf16", "nn", (B, 64), (64, 256), {}),
     ]
 else:
-    B, A, T = 2048, 360000, 3
+    B, A, T = int(sys.argv[2]) if len(sys.argv) > 2 else 25600, 360000, 3
     cases = [
         ("target actor out [B,256]x[A,256]^T -> bf16 (masked, clamped)", "nt", (B, 256), (A, 256), {"mask": True}),
         ("critic act [B,A]x[64,A]^T -> f32 (split-K)", "nt", (B, A), (64, A), {"o32": True, "split": True}),
