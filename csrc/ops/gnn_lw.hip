@@ -125,6 +125,18 @@ __device__ __forceinline__ float leaky(float z) { return z > 0.f ? z : kLwSlope 
 // With nx.wl set, the epilogue also computes the next conv's node linears from the output row
 // (x_l' = h W_l'^T + b_l', x_r' likewise; the H x H weights staged transposed in LDS, the row
 // broadcast lane by lane), so the layer-to-layer GEMMs and the re-read of h_out disappear.
+// first conv from a narrow input (Fi <= 8): x_l / x_r computed in the attention kernel (no node-linear pass)
+struct LwFirst {
+  const float* x;  // [B*P][Fi] (null: x_l / x_r come from memory)
+  int Fi;
+  const float* wl;  // [H][Fi]
+  const float* bl;
+  const float* wr;
+  const float* br;
+  float* xl_out;    // [B*P][H] (null: not needed -- no backward)
+  float* xr_out;
+};
+
 struct LwNext {
   const float* wl;  // [H][H] (null: last conv)
   const float* bl;
@@ -538,13 +550,13 @@ __device__ __forceinline__ void lw_load_row(float (&v)[HV], const float* src, in
 // a . LeakyReLU(z) runs as (1+s)/2 (a . z) + (1-s)/2 (a . |z|) -- two independent FMA chains with the |z|
 // source modifier instead of a compare / select per channel.  Outputs leave through LDS with coalesced
 // stores; the next conv's node linears run on the matrix cores (lw_mfma_rows).
-template <int HV>
+template <int HV, bool FIRST = false>
 __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kernel(LwGraph g, const float* __restrict__ xl,
                                                                 const float* __restrict__ xr,
                                                                 const float* __restrict__ att,
                                                                 const float* __restrict__ bias, int relu,
                                                                 float* __restrict__ h_out, float* __restrict__ alpha,
-                                                                LwNext nx, float* __restrict__ emb) {
+                                                                LwNext nx, float* __restrict__ emb, LwFirst f0) {
   // LDS: x_l rows [P][RS] (then the output rows, then their bf16 image), scores [M] (then alpha), deg [P],
   //      in_ptr [P+1], in_src [M]
   constexpr int RS = HV + 4;
@@ -561,11 +573,16 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
   const long base = (long)b * P * H;
   const int NE = P * H, i = threadIdx.x;
   const int n = g.nnodes[t];
-  const bool vec = (NE & 3) == 0 && ((reinterpret_cast<uintptr_t>(xl + base) & 15) == 0) &&
-                   (!h_out || (reinterpret_cast<uintptr_t>(h_out + base) & 15) == 0);
+  constexpr bool first = FIRST;  // f0.x set: x_l / x_r from the narrow input (own instantiation: registers)
+  const bool vin = !first && (NE & 3) == 0 && ((reinterpret_cast<uintptr_t>(xl + base) & 15) == 0);
+  const bool vec = (NE & 3) == 0 && (!h_out || (reinterpret_cast<uintptr_t>(h_out + base) & 15) == 0);
   // ---- all loads in flight together
   float4 v4[kV];
-  if (vec) {
+  float xin[8];  // first conv: the lane's input row
+  if (first) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xin[k] = (i < P && k < f0.Fi) ? f0.x[((long)b * P + i) * f0.Fi + k] : 0.f;
+  } else if (vin) {
     const float4* x4 = reinterpret_cast<const float4*>(xl + base);
 #pragma unroll
     for (int u = 0; u < kV; ++u) {
@@ -574,7 +591,7 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
     }
   }
   float xri[HV];
-  if (i < n) lw_load_row<HV>(xri, xr + base + (long)i * H, H);
+  if (!first && i < n) lw_load_row<HV>(xri, xr + base + (long)i * H, H);
   int ip = 0;
   float dg = 1.f;
   if (i <= P) ip = g.in_ptr[(long)t * (P + 1) + i];
@@ -586,7 +603,36 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
     if (j < M) sv[u] = g.in_src[(long)t * M + j];
   }
   // ---- LDS images
-  if (vec) {
+  if (first) {  // x_l / x_r rows of node i from its input row (uniform weights: scalar loads)
+    if (i < P) {
+#pragma unroll
+      for (int v = 0; v < HV / 4; ++v) {  // four channels at a time: x_l straight to LDS, x_r kept
+        float xl4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 4 * v + e;
+          float al = 0.f, ar = 0.f;
+          if (c < H) {
+            al = f0.bl[c];
+            ar = f0.br[c];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (k < f0.Fi) {
+                al = fmaf(f0.wl[c * f0.Fi + k], xin[k], al);
+                ar = fmaf(f0.wr[c * f0.Fi + k], xin[k], ar);
+              }
+            if (f0.xl_out) {  // the backward reads them
+              f0.xl_out[base + (long)i * H + c] = al;
+              f0.xr_out[base + (long)i * H + c] = ar;
+            }
+          }
+          xl4[e] = al;
+          xri[c] = ar;
+        }
+        reinterpret_cast<float4*>(s_xl + i * RS)[v] = make_float4(xl4[0], xl4[1], xl4[2], xl4[3]);
+      }
+    }
+  } else if (vin) {
 #pragma unroll
     for (int u = 0; u < kV; ++u) {
       const int j = i + 256 * u;
@@ -606,7 +652,7 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
       s_xl[r * RS + c] = xl[base + k];
     }
   }
-  for (int k = i; k < P * (HV - H); k += 256) {  // padded channels are read by the gathers: zero, not stale
+  for (int k = first ? P * HV : i; k < P * (HV - H); k += 256) {  // padded channels are read: zero, not stale
     const int r = k / (HV - H), c = H + k - r * (HV - H);
     s_xl[r * RS + c] = 0.f;
   }
@@ -1886,10 +1932,38 @@ void lw_pool(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t h, 
 // emb (last conv, optional): also the mean pool into emb [B][H] (fused on the lane-per-node path)
 // store: bit 0 = the output rows h_out, bit 1 = alpha are needed (a later backward); the staged kernel skips
 // the others, the other kernels always write both
+// first = (x, Fi, wl, bl, wr, br, store_xlxr): the first conv from its narrow input x [B*P][Fi] (Fi <= 8); x_l /
+// x_r go to xl / xr only when store_xlxr (a backward follows) -- or always, through lw_node_linear, when the
+// staged kernel does not apply
+void lw_node_linear(uintptr_t x, long R, int Fi, int H, uintptr_t wl, uintptr_t bl, uintptr_t wr, uintptr_t br,
+                    uintptr_t xl, uintptr_t xr, uintptr_t stream);
 void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t xl, uintptr_t xr, uintptr_t att,
                  uintptr_t bias, int relu, uintptr_t h_out, uintptr_t alpha, uintptr_t stream, py::tuple next,
-                 uintptr_t emb, int store) {
+                 uintptr_t emb, int store, py::tuple first) {
   const LwGraph g = lw_graph(tables, topo, B, P, H);
+  LwFirst f0{};
+  if (first.size() == 7) {
+    f0.x = ptr<const float>(first[0].cast<uintptr_t>());
+    f0.Fi = first[1].cast<int>();
+    f0.wl = ptr<const float>(first[2].cast<uintptr_t>());
+    f0.bl = ptr<const float>(first[3].cast<uintptr_t>());
+    f0.wr = ptr<const float>(first[4].cast<uintptr_t>());
+    f0.br = ptr<const float>(first[5].cast<uintptr_t>());
+    if (first[6].cast<int>()) {
+      f0.xl_out = ptr<float>(xl);
+      f0.xr_out = ptr<float>(xr);
+    }
+    GSC_CHECK(f0.Fi >= 1 && f0.Fi <= 8, "lw_attn_fwd: the fused first conv takes Fi <= 8 input features");
+  } else {
+    GSC_CHECK(first.size() == 0, "lw_attn_fwd: first = (x, Fi, wl, bl, wr, br, store_xlxr) or ()");
+  }
+  // the non-staged kernels read x_l / x_r from memory
+  auto materialise_first = [&]() {
+    if (f0.x)
+      lw_node_linear(reinterpret_cast<uintptr_t>(f0.x), (long)B * P, f0.Fi, H, reinterpret_cast<uintptr_t>(f0.wl),
+                     reinterpret_cast<uintptr_t>(f0.bl), reinterpret_cast<uintptr_t>(f0.wr),
+                     reinterpret_cast<uintptr_t>(f0.br), xl, xr, stream);
+  };
   LwNext nx{};
   if (next.size() == 6) {
     nx.wl = ptr<const float>(next[0].cast<uintptr_t>());
@@ -1909,18 +1983,21 @@ void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
     // staged variant: both row blocks in LDS, coalesced output / alpha stores, MFMA linears
     const size_t lds_st = sizeof(float) * ((size_t)P * (hv + 4) + 2 * g.M + 2 * P + 1);
     if (mf_env && P <= 256 && hv >= 16 && (!nx.wl || lw_mfma_fits(P, hv + 4)) && lds_st <= 80 * 1024) {
-      auto ks = hv == 16 ? lw_stage_attn_fwd_kernel<16> : hv == 24 ? lw_stage_attn_fwd_kernel<24>
-                                                                  : lw_stage_attn_fwd_kernel<32>;
+      auto ks = f0.x ? (hv == 16 ? lw_stage_attn_fwd_kernel<16, true>
+                                 : hv == 24 ? lw_stage_attn_fwd_kernel<24, true> : lw_stage_attn_fwd_kernel<32, true>)
+                     : (hv == 16 ? lw_stage_attn_fwd_kernel<16> : hv == 24 ? lw_stage_attn_fwd_kernel<24>
+                                                                        : lw_stage_attn_fwd_kernel<32>);
       if (lds_st > 65536)  // two workgroups still share a CU's 160 KB
         GSC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(ks),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_st));
       hipLaunchKernelGGL(ks, dim3(B), dim3(256), lds_st, stream_of(stream), g, ptr<const float>(xl),
                          ptr<const float>(xr), ptr<const float>(att), ptr<const float>(bias), relu,
                          (store & 1) ? ptr<float>(h_out) : nullptr, (store & 2) ? ptr<float>(alpha) : nullptr, nx,
-                         ptr<float>(emb));
+                         ptr<float>(emb), f0);
       check_launch();
       return;
     }
+    materialise_first();
     const size_t lds = sizeof(float) * ((size_t)P * hv + (nx.wl && !mf ? 2 * H * hv : 0) + 2 * g.M + 2 * P + 1);
     if (lds <= 64 * 1024) {
       auto kl = mf ? (hv == 16 ? lw_lane_attn_fwd_kernel<16, true> : hv == 24 ? lw_lane_attn_fwd_kernel<24, true>
@@ -1935,6 +2012,7 @@ void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
       return;
     }
   }
+  if (H > 32) materialise_first();
   const size_t graph_lds = sizeof(float) * (2L * P * H + (nx.wl ? 2L * H * H : 0) + (P + 1) + g.M + P);
   if (graph_lds <= 64 * 1024) {  // per-graph blocks (>= 2 workgroups per CU)
     auto kg = lanes_per_node(g) == 32 ? lw_graph_attn_fwd_kernel<32> : lw_graph_attn_fwd_kernel<64>;
@@ -2133,7 +2211,8 @@ void register_gnn_lw(py::module_& m) {
   m.def("lw_attn_fwd", &lw_attn_fwd, "layer-wise GATv2: attention + aggregation (+ReLU), alpha saved; optionally "
         "the next conv's node linears", py::arg("tables"), py::arg("topo"), py::arg("B"), py::arg("P"), py::arg("H"),
         py::arg("xl"), py::arg("xr"), py::arg("att"), py::arg("bias"), py::arg("relu"), py::arg("h_out"),
-        py::arg("alpha"), py::arg("stream"), py::arg("next") = py::tuple(), py::arg("emb") = 0, py::arg("store") = 3);
+        py::arg("alpha"), py::arg("stream"), py::arg("next") = py::tuple(), py::arg("emb") = 0, py::arg("store") = 3,
+        py::arg("first") = py::tuple());
   m.def("lw_pool", &lw_pool, "layer-wise GATv2: mean pool over real nodes");
   m.def("lw_pool_bwd", &lw_pool_bwd, "layer-wise GATv2: mean-pool backward");
   m.def("lw_attn_bwd", &lw_attn_bwd, "layer-wise GATv2: attention backward per target node");

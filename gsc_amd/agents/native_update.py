@@ -166,6 +166,12 @@ class NativeDDPGUpdate:
         self.hx = mk(B, T * hl, dt=BF16) if T > 1 else None  # topology-expanded actor hidden / critic grads
         self.dh0x = mk(B, T * c1, dt=BF16) if T > 1 else None
         self.splits = None                                   # auto split-K for the batch reductions
+        # output tiles of the products that stream the [B, A] action block / the A-long weights at large A
+        # (scripts/gemm_tune.py syn200 at B = 25,600, profiles/gemm_tune_syn200.txt): the critic's action
+        # projection 4.87 -> 3.44 ms with 128-row tiles and 64-deep K stages, its weight gradient 4.36 -> 3.91 ms
+        # with 64-deep stages, Mc 245 -> 144 us with 64 x 128 tiles
+        self.big_tiles = ({"act": {"tile": 1, "bk": 64}, "dw": {"tile": 2, "bk": 64}, "mc": {"tile": 3}}
+                          if A >= 65536 and os.environ.get("GSC_LARGE_A_TILES", "1") != "0" else {})
         self.slabs = mk(16 << 20)                            # split-K slabs (64 MB; bounds the split count)
         self.head_blocks = max(64, min(256, -(-B // 64)))    # one block per CU (>= 16 rows per wave)
         cm = self.critic.width(self.critic.nh - 1)
@@ -263,7 +269,8 @@ class NativeDDPGUpdate:
             if extra_rowtab is not None:
                 gemm(extra, wa, "nt", out32=self.hacc[:, :h0], rowtab=extra_rowtab, topo=self.topo32)
             else:   # K = A: split-K when the [B, h0] output alone gives few workgroups (large A)
-                gemm(extra, wa, "nt", out32=self.hacc[:, :h0], splits=None, slabs=self.slabs, a_rows=extra_rows)
+                gemm(extra, wa, "nt", out32=self.hacc[:, :h0], splits=None, slabs=self.slabs, a_rows=extra_rows,
+                     **self.big_tiles.get("act", {}))
             acc = True
         gemm(emb, net.w16(0)[:, :self.H], "nt", out16=out16, bias=net.b32(0), rowtab=rowtab, topo=self.topo32,
              relu=True, accumulate=acc, out32=self.hacc[:, :h0] if acc else None)
@@ -297,7 +304,8 @@ class NativeDDPGUpdate:
         self.nat.first_layer_grad(aug.data_ptr(), h0, H, T, A, self.masks.data_ptr(), self.masks.stride(0),
                                   gw.data_ptr(), gw.stride(0), net.gb(0).data_ptr(), self._stream())
         if extra is not None:
-            gemm(dh0, extra, "tn", out32=gw[:, H + A:], splits=self.splits, slabs=self.slabs, b_rows=extra_rows)
+            gemm(dh0, extra, "tn", out32=gw[:, H + A:], splits=self.splits, slabs=self.slabs, b_rows=extra_rows,
+                 **self.big_tiles.get("dw", {}))
         gemm(dh0, net.w16(0)[:, :H], "nn", out32=self.demb)
 
     def _critic_tail(self, net: _Net, acts, mode: int, dh_out: Optional[torch.Tensor], b) -> None:
@@ -393,8 +401,9 @@ class NativeDDPGUpdate:
             for t in range(T):
                 self.nat.copy2d(w.data_ptr() + 2 * (H + A), w.stride(0), wam[t * c1].data_ptr(), wam.stride(0), c1, A,
                                 self.masks[t].data_ptr(), st)
-            ks = max(16, auto_splits(T * c1, hw, A, 2, self.slabs.numel()))
-            gemm(wam, a.w16(last), "nn", out32=self.mc32, slabs=self.slabs, splits=ks)   # Mc_t = W_a diag(m_t) W
+            ks = max(16, auto_splits(T * c1, hw, A, self.big_tiles.get("mc", {}).get("tile", 2), self.slabs.numel()))
+            gemm(wam, a.w16(last), "nn", out32=self.mc32, slabs=self.slabs, splits=ks,   # Mc_t = W_a diag(m_t) W
+                 **self.big_tiles.get("mc", {}))
             self.nat.cast2d(self.mc32.data_ptr(), hw, self.mc16.data_ptr(), hw, T * c1, hw, st)
             for t in range(T):                                        # [Mc_0 | .. ]: row j holds Mc_t[j] at t*hw
                 self.nat.cast2d(self.mc32[t * c1].data_ptr(), hw, self.mccat.data_ptr() + 2 * t * hw,

@@ -98,8 +98,11 @@ class LayerwiseGAT:
         h = x.view(B * P, self.Fin)
         for l, blk in enumerate(self.layer_of):
             Fi, Wl, bl, Wr, br, att, bias = self._params(flat, blk)
+            first = ()
             if l == 0:   # later convs' node linears come from the previous attention kernel
-                if Fi <= 8:
+                if Fi <= 8 and not save:   # computed inside the attention kernel, never stored
+                    first = (h.data_ptr(), Fi, Wl.data_ptr(), bl.data_ptr(), Wr.data_ptr(), br.data_ptr(), 0)
+                elif Fi <= 8:   # a backward reads x_l / x_r: one coalesced pass writes them
                     nat.lw_node_linear(h.data_ptr(), B * P, Fi, H, Wl.data_ptr(), bl.data_ptr(), Wr.data_ptr(),
                                        br.data_ptr(), self.xl[l].data_ptr(), self.xr[l].data_ptr(), s)
                 else:
@@ -113,7 +116,8 @@ class LayerwiseGAT:
             nat.lw_attn_fwd(t, topo32.data_ptr(), B, P, H, self.xl[l].data_ptr(), self.xr[l].data_ptr(),
                             att.data_ptr(), bias.data_ptr(), int(self._relu(l)), self.hout[l].data_ptr(),
                             self.alpha[l].data_ptr(), s, nxt, emb.data_ptr() if l + 1 == self.L else 0,
-                            store=(1 if save and (l + 1 < self.L or self._relu(l)) else 0) | (2 if save else 0))
+                            store=(1 if save and (l + 1 < self.L or self._relu(l)) else 0) | (2 if save else 0),
+                            first=first)
             h = self.hout[l]   # the last conv also writes the mean pool into emb
 
     def backward(self, flat: torch.Tensor, demb: torch.Tensor, grad: torch.Tensor) -> None:
