@@ -1,5 +1,6 @@
 #!/bin/bash
-# full GPU suite + smoke, then the three preset benches
+# full GPU suite + smoke, the three preset benches, then the Abilene timed-window trace (last: the profiled
+# process can segfault in the tool finalizer)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
@@ -13,3 +14,4 @@ for p in syn200 abilene syn50; do
   timeout -k 10 400 python $R/bench.py --preset $p --steps ${STEPS:-30} --warmup 5 > $OUT/bench_$p.json 2> $OUT/bench_$p.err || exit $?
   echo "$p: $(cut -c1-250 $OUT/bench_$p.json)" >> $OUT/r4c10.txt
 done
+PRESET=abilene STEPS=20 bash $R/scripts/gpurun/prof_preset.sh
