@@ -471,6 +471,7 @@ class BatchedTrainer:
         self._topo_sink = None
         self._handoff = True
         self.sim_stream = self.learn_stream = None
+        self.act_stream = None  # GSC_ACT_STREAM=1: the act path on an unmasked stream (every CU)
         self.sim_cus = 0
         if self.device.type == "cuda" and tcfg.overlap_sim:
             sim_cus = tcfg.sim_cus if tcfg.sim_cus >= 0 else self.auto_sim_cus(sim)
@@ -495,6 +496,11 @@ class BatchedTrainer:
                 else:
                     self.learn_stream = torch.cuda.ExternalStream(
                         nat.create_cu_masked_stream(list(range(k, n))), device=self.device)
+                # The act path (actor forward + exploration of step t+1) sits between two simulator
+                # steps, when the learner's CUs are idle too (update t done, update t+1 waits for it):
+                # GSC_ACT_STREAM=1 runs it on an unmasked stream instead of the simulator's CUs
+                if os.environ.get("GSC_ACT_STREAM", "0") == "1":
+                    self.act_stream = torch.cuda.Stream(self.device)
                 # persistent GNN grids sized to the CUs free while the simulator runs (one full round)
                 budget = int(os.environ.get("GSC_GNN_CU_BUDGET", str(n - k)))
                 nat.gnn_set_cu_budget(budget)
@@ -623,10 +629,18 @@ class BatchedTrainer:
             # buffers this step reuses).  The learner's replay insert of step t-1 and update t wait for the
             # act only (the update rewrites the actor weights), so they run concurrently with simulator(t).
             self.sim_stream.wait_stream(main)
+            if self.act_stream is not None:
+                self.act_stream.wait_stream(self.sim_stream)
+                with torch.cuda.stream(self.act_stream):
+                    act = self._act(obs, topo, warm, k)
+                    ev_act = self._event()
+                    ev_act.record(self.act_stream)
+                self.sim_stream.wait_event(ev_act)
             with torch.cuda.stream(self.sim_stream):
-                act = self._act(obs, topo, warm, k)
-                ev_act = self._event()
-                ev_act.record(self.sim_stream)
+                if self.act_stream is None:
+                    act = self._act(obs, topo, warm, k)
+                    ev_act = self._event()
+                    ev_act.record(self.sim_stream)
                 self._schedule_next()
                 out = self.sim.step(act, buffer_set=k, obs_out=obs_next)
                 ev_sim = self._event()
