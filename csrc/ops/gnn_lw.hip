@@ -621,10 +621,6 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
                 al = fmaf(f0.wl[c * f0.Fi + k], xin[k], al);
                 ar = fmaf(f0.wr[c * f0.Fi + k], xin[k], ar);
               }
-            if (f0.xl_out) {  // the backward reads them
-              f0.xl_out[base + (long)i * H + c] = al;
-              f0.xr_out[base + (long)i * H + c] = ar;
-            }
           }
           xl4[e] = al;
           xri[c] = ar;
@@ -666,6 +662,17 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
   }
   for (int k = i + 256 * kV; k < M; k += 256) src[k] = g.in_src[(long)t * M + k];
   __syncthreads();
+  if (first && f0.xl_out) {  // a backward reads x_l / x_r: coalesced stores (x_l from the LDS rows, x_r recomputed)
+    for (int e0 = i; e0 < NE; e0 += 256) {
+      const int r = e0 / H, c = e0 - r * H;
+      float ar = f0.br[c];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+        if (kk < f0.Fi) ar = fmaf(f0.wr[c * f0.Fi + kk], f0.x[((long)b * P + r) * f0.Fi + kk], ar);
+      f0.xl_out[base + e0] = s_xl[r * RS + c];
+      f0.xr_out[base + e0] = ar;
+    }
+  }
   // ---- lane = target node: scores, online softmax, aggregation
   float y[HV];
 #pragma unroll
@@ -1375,7 +1382,10 @@ __global__ __launch_bounds__(256, HV <= 24 ? 3 : 2) void lw_stage_attn_bwd_kerne
                                                                    float* __restrict__ datt, float* __restrict__ dxl,
                                                                    const float* __restrict__ wl,
                                                                    const float* __restrict__ wr, float* __restrict__ dh_in,
-                                                                   float* __restrict__ vpart) {
+                                                                   float* __restrict__ vpart,
+                                                                   const float* __restrict__ demb) {
+  // demb (optional, [B][H]): the last conv's incoming gradient is the mean-pool backward, formed here
+  // (demb / n on the real nodes) instead of read from dh (no separate pool-backward pass)
   // vpart (optional, [B][H]): the graph's d att row sum instead of the d att rows (lw_conv_grads_v)
   // LDS: rows [P][HV] (x_l, then x_r, then outputs), g [P][HV], alpha, de [M] (fp32), deg [P], in_ptr / out_ptr
   //      [P+1], out_q [M] (u16), in_src / target [M] (u8)
@@ -1399,7 +1409,25 @@ __global__ __launch_bounds__(256, HV <= 24 ? 3 : 2) void lw_stage_attn_bwd_kerne
   // ---- every load in flight together
   float4 vx[KV], vd[KV], vh[KV];
   lw_block_load<HV, KV>(vx, xl + base, NE);
-  lw_block_load<HV, KV>(vd, dh + base, NE);
+  if (demb) {
+    const float inv_n = 1.f / (float)n;
+#pragma unroll
+    for (int u = 0; u < KV; ++u) {
+      const int j = i + 256 * u;
+      if (j < NE / 4) {
+        int c = (4 * j) % H;
+        float f[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          f[e] = demb[(long)b * H + c] * inv_n;  // rows >= n are zeroed below with the gate
+          if (++c == H) c = 0;
+        }
+        vd[u] = make_float4(f[0], f[1], f[2], f[3]);
+      }
+    }
+  } else {
+    lw_block_load<HV, KV>(vd, dh + base, NE);
+  }
   if (h_out) lw_block_load<HV, KV>(vh, h_out + base, NE);
   float xri[HV];
   if (i < n) lw_load_row<HV>(xri, xr + base + (long)i * H, H);
@@ -2076,9 +2104,13 @@ void lw_src_gather(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr
 // graph's x_l block fits the LDS budget, else the per-node kernels
 // vpart (optional, [B][H]): the staged kernel writes per-graph d att sums there instead of the d att rows;
 // returns whether it did (else the rows are in datt)
+// demb (optional, [B][H]): dh is the mean-pool backward of demb (the last conv): formed inside the staged
+// kernel, or written to dh by lw_pool_bwd first when another kernel runs
+void lw_pool_bwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t demb, uintptr_t dh, uintptr_t stream);
 bool lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t dh, uintptr_t h_out, uintptr_t xl,
                         uintptr_t xr, uintptr_t alpha, uintptr_t att, uintptr_t dxr, uintptr_t msg, uintptr_t datt,
-                        uintptr_t dxl, uintptr_t wl, uintptr_t wr, uintptr_t dh_in, uintptr_t stream, uintptr_t vpart) {
+                        uintptr_t dxl, uintptr_t wl, uintptr_t wr, uintptr_t dh_in, uintptr_t stream, uintptr_t vpart,
+                        uintptr_t demb) {
   const LwGraph g = lw_graph(tables, topo, B, P, H);
   GSC_CHECK(!wl || (wr && dh_in), "lw_attn_bwd_gather: the input gradient needs wl, wr, dh_in");
   if (H <= 32) {  // lane per node
@@ -2100,10 +2132,12 @@ bool lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, ui
       hipLaunchKernelGGL(ks, dim3(B), dim3(256), lst, stream_of(stream), g, ptr<float>(dh), ptr<const float>(h_out),
                          ptr<const float>(xl), ptr<const float>(xr), ptr<const float>(alpha), ptr<const float>(att),
                          ptr<float>(dxr), ptr<float>(datt), ptr<float>(dxl), ptr<const float>(wl),
-                         ptr<const float>(wr), ptr<float>(dh_in), ptr<float>(vpart));
+                         ptr<const float>(wr), ptr<float>(dh_in), ptr<float>(vpart), ptr<const float>(demb));
       check_launch();
       return vpart != 0;
     }
+    if (demb) lw_pool_bwd(tables, topo, B, P, H, demb, dh, stream);
+    demb = 0;
     const size_t ll = sizeof(float) * (2 * (size_t)P * hv + (wl && !mf ? 2 * H * hv : 0) + 5 * g.M + P + 2 * (P + 1));
     if (ll <= 80 * 1024) {  // >= 2 workgroups per CU
       auto kl = mf ? (hv == 16 ? lw_lane_attn_bwd_kernel<16, true> : hv == 24 ? lw_lane_attn_bwd_kernel<24, true>
@@ -2119,6 +2153,7 @@ bool lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, ui
       return false;
     }
   }
+  if (demb) lw_pool_bwd(tables, topo, B, P, H, demb, dh, stream);
   const size_t lds = sizeof(float) * ((size_t)P * H + (wl ? 2 * H * H : 0) + g.M + P + 2 * (P + 1) + 2 * g.M);
   if (lds <= 64 * 1024) {
     auto k = lanes_per_node(g) == 32 ? lw_graph_attn_bwd_kernel<32> : lw_graph_attn_bwd_kernel<64>;
@@ -2225,7 +2260,7 @@ void register_gnn_lw(py::module_& m) {
         "returns whether vpart holds the per-graph d att sums", py::arg("tables"), py::arg("topo"), py::arg("B"),
         py::arg("P"), py::arg("H"), py::arg("dh"), py::arg("h_out"), py::arg("xl"), py::arg("xr"), py::arg("alpha"),
         py::arg("att"), py::arg("dxr"), py::arg("msg"), py::arg("datt"), py::arg("dxl"), py::arg("wl"), py::arg("wr"),
-        py::arg("dh_in"), py::arg("stream"), py::arg("vpart") = 0);
+        py::arg("dh_in"), py::arg("stream"), py::arg("vpart") = 0, py::arg("demb") = 0);
   m.def("lw_conv_grads_v", &lw_conv_grads_v, "layer-wise GATv2: conv parameter gradients, streamed (MFMA dW with "
         "a ones column for the bias sums), d att from per-graph sums");
   m.def("lw_colsum", &lw_colsum, "deterministic column sums (two phases)");

@@ -100,11 +100,8 @@ class LayerwiseGAT:
             Fi, Wl, bl, Wr, br, att, bias = self._params(flat, blk)
             first = ()
             if l == 0:   # later convs' node linears come from the previous attention kernel
-                if Fi <= 8 and not save:   # computed inside the attention kernel, never stored
-                    first = (h.data_ptr(), Fi, Wl.data_ptr(), bl.data_ptr(), Wr.data_ptr(), br.data_ptr(), 0)
-                elif Fi <= 8:   # a backward reads x_l / x_r: one coalesced pass writes them
-                    nat.lw_node_linear(h.data_ptr(), B * P, Fi, H, Wl.data_ptr(), bl.data_ptr(), Wr.data_ptr(),
-                                       br.data_ptr(), self.xl[l].data_ptr(), self.xr[l].data_ptr(), s)
+                if Fi <= 8:   # computed inside the attention kernel (stored, coalesced, when a backward follows)
+                    first = (h.data_ptr(), Fi, Wl.data_ptr(), bl.data_ptr(), Wr.data_ptr(), br.data_ptr(), int(save))
                 else:
                     gemm(h, Wl, "nt", out32=self.xl[l], bias=bl)
                     gemm(h, Wr, "nt", out32=self.xr[l], bias=br)
@@ -126,7 +123,7 @@ class LayerwiseGAT:
         nat, s, t = self.nat, self._stream(), self.tables
         tp = self.topo32.data_ptr()
         cur, nxt = self.dh
-        nat.lw_pool_bwd(t, tp, B, P, H, demb.contiguous().data_ptr(), cur.data_ptr(), s)
+        demb_c = demb.contiguous()   # the last conv's attention backward forms the pool backward itself
         seen = set()
         for l in range(self.L - 1, -1, -1):
             blk = self.layer_of[l]
@@ -144,7 +141,8 @@ class LayerwiseGAT:
                                           att.data_ptr(), self.dxr.data_ptr(), self.msg.data_ptr(),
                                           self.datt.data_ptr(), self.dxl.data_ptr(), Wl.data_ptr() if l > 0 else 0,
                                           Wr.data_ptr() if l > 0 else 0, nxt.data_ptr() if l > 0 else 0, s,
-                                          vpart=self.vpart.data_ptr() if stream_ok else 0)
+                                          vpart=self.vpart.data_ptr() if stream_ok else 0,
+                                          demb=demb_c.data_ptr() if l == self.L - 1 else 0)
             # dW_l | db_l | dW_r | db_r | d att | d bias in one pass (the block's layout in the flat gradient)
             assert gWl.data_ptr() == grad.data_ptr() + 4 * _block_offset(blk, self.Fin, H)
             if vsum:
