@@ -102,6 +102,40 @@ __device__ __forceinline__ MfW mf_frags(const bf16x8* img, int b, int lane) {
   return w;
 }
 
+// Input rows -> bf16 image rows [rows][kMfRS] (and, SAVE_T, the transposed [k][node] image with row stride TS
+// for k < trows): the images are cleared, then the nv valid rows -- nv * Fin contiguous floats -- are loaded
+// four per lane at a time at clamped addresses (all in flight together) and scattered in.  (A
+// per-element `v < n && k < Fin ? x[..] : 0` loop compiled to a branch around each load and waited for it:
+// one HBM round trip per loop trip.)
+template <bool SAVE_T>
+__device__ __forceinline__ void mf_stage_input(const float* __restrict__ xg, int nv, int Fin, int rows, __bf16* hR,
+                                               __bf16* hT, int TS, int trows, int lane) {
+  const int nx = nv > 0 ? nv * Fin : 0;
+  for (int i = lane; i < rows * 32; i += 64) {
+    const int v = i >> 5, k = i & 31;
+    hR[v * kMfRS + k] = (__bf16)0.f;
+    if (SAVE_T && k < trows) hT[k * TS + v] = (__bf16)0.f;
+  }
+  for (int b0 = 0; b0 < nx; b0 += 256) {  // GSC shapes: one trip (11 x 3 or 32 x 3 floats)
+    float xv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = b0 + lane + 64 * u;
+      xv[u] = xg[idx < nx ? idx : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = b0 + lane + 64 * u;
+      if (idx < nx) {
+        const int v = idx / Fin, k = idx - v * Fin;
+        const __bf16 b = (__bf16)xv[u];
+        hR[v * kMfRS + k] = b;
+        if (SAVE_T) hT[k * TS + v] = b;
+      }
+    }
+  }
+}
+
 __host__ __device__ __forceinline__ int mf_vec_floats(int n_blocks) { return n_blocks * kMfVec; }
 // fp32 [node][channel] row stride (x_l, x_r, dy images): HPF + 4 floats = 16 B x odd, so the per-message
 // row gathers (ds_read_b128 / b64 at different nodes) of up to 16 distinct rows hit distinct banks

@@ -198,13 +198,7 @@ __device__ __forceinline__ float mf_layer(const MfW& w, const float* vec, const 
 template <bool SAVE_T>
 __device__ __forceinline__ void mf_load_x(const ClArgs& a, int g, int n, __bf16* hR, __bf16* hT, __bf16* E, int NV,
                                           int NVS, int lane) {
-  const float* xg = a.x + (long)g * a.P * a.Fin;
-  for (int i = lane; i < NV * 32; i += 64) {
-    const int v = i >> 5, k = i & 31;
-    const __bf16 b = (__bf16)((v < n && k < a.Fin) ? xg[v * a.Fin + k] : 0.f);
-    hR[v * kMfRS + k] = b;
-    if (SAVE_T && k < ((a.Fin + 3) & ~3)) hT[k * NVS + v] = b;
-  }
+  mf_stage_input<SAVE_T>(a.x + (long)g * a.P * a.Fin, n, a.Fin, NV, hR, hT, NVS, (a.Fin + 3) & ~3, lane);
   for (int i = lane; i < NV * NVS / 8; i += 64) reinterpret_cast<uint4*>(E)[i] = make_uint4(0, 0, 0, 0);
   cl_wave_sync();
 }

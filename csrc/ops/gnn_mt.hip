@@ -138,13 +138,8 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
     {
       __bf16* hA = reinterpret_cast<__bf16*>(G + m.hR[0]) + 32 * w * kMfRS;
       __bf16* hT = reinterpret_cast<__bf16*>(G + m.hR[1]) + 32 * w * kMfRS;
-      const float* xg = a.x + ((long)g * a.P + 32 * w) * a.Fin;
-      for (int i = lane; i < 32 * 32; i += 64) {
-        const int v = i >> 5, k = i & 31;
-        const __bf16 b = (__bf16)((v < nl && k < a.Fin) ? xg[v * a.Fin + k] : 0.f);
-        hA[v * kMfRS + k] = b;
-        if (SAVE && k < m.hTrows0) hT[k * kMtTS + v] = b;
-      }
+      mf_stage_input<SAVE>(a.x + ((long)g * a.P + 32 * w) * a.Fin, nl < 32 ? nl : 32, a.Fin, 32, hA, hT, kMtTS,
+                           m.hTrows0, lane);
       uint4* e4 = reinterpret_cast<uint4*>(E + 32 * w * m.NVS);
       for (int i = lane; i < 32 * m.NVS / 8; i += 64) e4[i] = make_uint4(0, 0, 0, 0);
     }

@@ -101,3 +101,21 @@ def test_layerwise_200_nodes_wide_hidden_per_node_kernel():
     budget, so the forward takes the per-node attention kernel."""
     gs = GraphSet([load_topology(p) for p in SYN200[:2]], 200, DEV)
     _check(gs, 200, 24, hidden=64, direct=True)
+
+
+@pytest.mark.parametrize("layers,iters,hidden", [(2, 2, 22), (1, 1, 22), (3, 1, 16), (2, 2, 32)])
+def test_layerwise_forward_without_backward(layers, iters, hidden):
+    """No-grad forwards (target / act embedders): the per-conv kernels without stored rows / alpha, and the
+    whole-embedding kernel (lw_embed_fwd, opt-in: GSC_LW_EMBED=1, read once per process -- covered by the
+    GPU run of scripts/gpurun/r4_check13.sh); same tolerance as the saved path."""
+    from gsc_amd.ops.gnn import gnn_embed_layerwise
+    gs = GraphSet([load_topology(p) for p in SYN200], 200, DEV)
+    torch.manual_seed(1)
+    emb = GNNEmbedder(3, hidden, layers, "mean", iters).to(DEV)
+    B = 64
+    topo = torch.randint(0, gs.num_topologies, (B,), device=DEV)
+    x = torch.rand(B, 200, 3, device=DEV) * gs.node_mask[topo].unsqueeze(-1)
+    with torch.no_grad():
+        ref = emb.forward_reference(x, topo, gs)
+        out = gnn_embed_layerwise(emb, x, topo, gs)
+    assert _rel(out, ref) < 1e-2, _rel(out, ref)
