@@ -78,9 +78,11 @@ __device__ __forceinline__ void mt_load_topo(MtTopo& T, const ClArgs& a, int t, 
   if (T.t == t) return;  // uniform over the workgroup: every wave holds the same T.t
   T.t = t;
   const long mo = (long)t * a.M;
-  for (int i = threadIdx.x; i < a.M; i += blockDim.x) {
-    T.isrc[i] = a.in_src[mo + i];
-    T.idst[i] = a.in_dst[mo + i];
+  // rows padded to MP with -1: the backward's one-hot operands (mt_onehot) read whole 16-message slices
+  for (int i = threadIdx.x; i < a.MP; i += blockDim.x) {
+    const bool v = i < T.m;
+    T.isrc[i] = v ? a.in_src[mo + i] : -1;
+    T.idst[i] = v ? a.in_dst[mo + i] : -1;
   }
   for (int i = threadIdx.x; i < a.P; i += blockDim.x) T.deg[i] = a.deg[(long)t * a.P + i];
 }
@@ -101,6 +103,22 @@ __device__ __forceinline__ void mt_store_T(const f32x16& acc, __bf16* img, int S
   }
 }
 
+// One-hot MFMA A operand of the message matrices, generated from the LDS topology instead of loaded
+// from the [T, NV, MP] bf16 tables in HBM: lane (row node, k half) gets 8 consecutive messages
+// p[0..7] (16-B aligned, padded with -1 past the graph's messages) -> bf16 1.0 where p[j] == node.
+// (A global fragment per MFMA step left every step waiting on an L2 round trip.)
+__device__ __forceinline__ bf16x8 mt_onehot(const int* p, int node) {
+  const int4 a = *reinterpret_cast<const int4*>(p);
+  const int4 b = *reinterpret_cast<const int4*>(p + 4);
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+  u32x4 o;
+  o[0] = (a.x == node ? 0x3F80u : 0u) | (a.y == node ? 0x3F800000u : 0u);
+  o[1] = (a.z == node ? 0x3F80u : 0u) | (a.w == node ? 0x3F800000u : 0u);
+  o[2] = (b.x == node ? 0x3F80u : 0u) | (b.y == node ? 0x3F800000u : 0u);
+  o[3] = (b.z == node ? 0x3F80u : 0u) | (b.w == node ? 0x3F800000u : 0u);
+  return __builtin_bit_cast(bf16x8, o);
+}
+
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
@@ -114,8 +132,8 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
   char* const G = reinterpret_cast<char*>(lds + mf_vec_floats(a.n_blocks) + 2 * kMfFragSet);
   MtTopo T;
   T.isrc = reinterpret_cast<int*>(G + m.topo);
-  T.idst = T.isrc + a.M;
-  T.deg = reinterpret_cast<float*>(T.idst + a.M);
+  T.idst = T.isrc + a.MP;
+  T.deg = reinterpret_cast<float*>(T.idst + a.MP);
   T.t = -1;
   float* const xl = reinterpret_cast<float*>(G + m.xl);
   float* const xr = reinterpret_cast<float*>(G + m.xr);
@@ -301,8 +319,8 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
   char* const G = reinterpret_cast<char*>(lds + mf_vec_floats(a.n_blocks) + 3 * kMfFragSet);
   MtTopo T;
   T.isrc = reinterpret_cast<int*>(G + m.topo);
-  T.idst = T.isrc + a.M;
-  T.deg = reinterpret_cast<float*>(T.idst + a.M);
+  T.idst = T.isrc + a.MP;
+  T.deg = reinterpret_cast<float*>(T.idst + a.MP);
   T.t = -1;
   {
     const int lane = tid & 63;
@@ -413,15 +431,13 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
       mf_zero(dxl);
       mf_zero(dxr);
       {
-        const long srow = ((long)T.t * m.NV + 32 * w + r) * a.MP + 8 * hh;
-        const __bf16* sd = reinterpret_cast<const __bf16*>(a.s_dst) + srow;
-        const __bf16* ss = reinterpret_cast<const __bf16*>(a.s_src) + srow;
+        const int node = 32 * w + r;
         const __bf16* gb = U + (r < HPF ? r : 0) * MS + 8 * hh;  // channels >= HPF: any finite data
         // dX_r: rows of S_dst are zero outside the own messages
         for (int s = T.q0 >> 4; 16 * s < T.q1; ++s)
-          dxr = mf_mma(*reinterpret_cast<const bf16x8*>(sd + 16 * s), *reinterpret_cast<const bf16x8*>(gb + 16 * s), dxr);
+          dxr = mf_mma(mt_onehot(T.idst + 16 * s + 8 * hh, node), *reinterpret_cast<const bf16x8*>(gb + 16 * s), dxr);
         for (int s = 0; 16 * s < T.m; ++s)
-          dxl = mf_mma(*reinterpret_cast<const bf16x8*>(ss + 16 * s), *reinterpret_cast<const bf16x8*>(gb + 16 * s), dxl);
+          dxl = mf_mma(mt_onehot(T.isrc + 16 * s + 8 * hh, node), *reinterpret_cast<const bf16x8*>(gb + 16 * s), dxl);
         const __bf16* erow = ET + (32 * w + r) * NVS + 8 * hh;
         const __bf16* yrow = reinterpret_cast<const __bf16*>(G + m.dyT[l & 1]) + (r < HPF ? r : 0) * NVS + 8 * hh;
         for (int s = 0; 16 * s < n; ++s)
@@ -596,7 +612,7 @@ static MtLayout mt_layout(const ClArgs& a, int kind, int HPF) {
   m.xl = take(fb);
   m.xr = take(fb);
   m.E = take(m.NV * m.NVS * 2);
-  m.topo = take((2 * a.M + a.P) * 4);
+  m.topo = take((2 * a.MP + a.P) * 4);
   if (kind != kMtBwd) {
     m.hR[0] = take(m.NV * kMfRS * 2);
     m.hR[1] = take(m.NV * kMfRS * 2);
@@ -665,8 +681,7 @@ static void mt_launch_fwd(ClArgs a, hipStream_t st, int cus) {
 
 template <int HPF, bool K2>
 static int mt_launch_bwd(ClArgs a, hipStream_t st, int cus, int max_rows) {
-  GSC_CHECK(a.s_dst != nullptr && a.s_src != nullptr && a.MP >= a.M && a.MP % 16 == 0,
-            "MFMA GNN backward needs the one-hot message matrices (GraphSet.s_dst / s_src)");
+  GSC_CHECK(a.MP >= a.M && a.MP % 16 == 0, "multi-tile MFMA GNN backward: message rows padded to 16");
   GSC_CHECK(a.blob != nullptr, "multi-tile MFMA GNN backward needs the forward's saved state");
   const MtLayout m = mt_layout(a, kMtBwd, HPF);
   const size_t lds = mt_lds(a, m, 3);
