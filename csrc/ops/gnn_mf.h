@@ -39,11 +39,19 @@ __device__ __forceinline__ int mf_lane() {
 // 8 weights as one bf16 fragment: W is [H][Fi] fp32 (module layout).  !trans: W[row][col0 + j]
 // (B operand of X = h W^T); trans: W[col0 + j][row] (B operand of dh = dX W).
 __device__ __forceinline__ bf16x8 mf_wfrag(const float* W, int H, int Fi, int row, int col0, bool trans) {
+  // clamped unconditional loads, masked after all are issued (a guarded load per element compiled to a
+  // branch around each load and one L2 round trip per element: ~32 serial trips per workgroup start)
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = trans ? col0 + j : row, k = trans ? row : col0 + j;
+    v[j] = W[(c < H && k < Fi) ? c * Fi + k : 0];
+  }
   bf16x8 f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = trans ? col0 + j : row, k = trans ? row : col0 + j;
-    f[j] = (__bf16)((c < H && k < Fi) ? W[c * Fi + k] : 0.f);
+    f[j] = (__bf16)((c < H && k < Fi) ? v[j] : 0.f);
   }
   return f;
 }
@@ -72,7 +80,8 @@ __device__ __forceinline__ void mf_stage_vec(const ClArgs& a, float* V, const fl
     const int Fi = b == 0 ? a.Fin : a.H;
     const float* src = params + cl_block_offset(b, a.Fin, a.H);
     const int off = which == 0 ? a.H * Fi : (which == 1 ? 2 * a.H * Fi + a.H : 2 * a.H * Fi + a.H * which);
-    V[i] = c < a.H ? src[off + c] : 0.f;
+    const float x = src[off + (c < a.H ? c : 0)];
+    V[i] = c < a.H ? x : 0.f;
   }
 }
 

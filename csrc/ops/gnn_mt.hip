@@ -68,14 +68,18 @@ struct MtTopo {
   int n, m, t, q0, q1;
 };
 
+// The per-wave scalars (q0, q1, n, m) stay in registers while the topology does not change: a graph
+// of the cached topology costs no dependent global round trip (its id is prefetched a graph ahead).
 __device__ __forceinline__ void mt_load_topo(MtTopo& T, const ClArgs& a, int t, int w) {
+  if (T.t == t) return;  // uniform over the workgroup: every wave holds the same T.t
   const int po = t * (a.P + 1);
   const int lo = 32 * w < a.P ? 32 * w : a.P, hi = 32 * w + 32 < a.P ? 32 * w + 32 : a.P;
-  T.q0 = a.in_ptr[po + lo];
-  T.q1 = a.in_ptr[po + hi];
-  T.n = a.nnodes[t];
-  T.m = a.nmsgs[t];
-  if (T.t == t) return;  // uniform over the workgroup: every wave holds the same T.t
+  // wave-uniform: held in SGPRs (a VGPR holding a loaded value makes the compiler drain vmcnt -- and
+  // with it the prefetches in flight -- in the preheader of every store loop that reads it)
+  T.q0 = __builtin_amdgcn_readfirstlane(a.in_ptr[po + lo]);
+  T.q1 = __builtin_amdgcn_readfirstlane(a.in_ptr[po + hi]);
+  T.n = __builtin_amdgcn_readfirstlane(a.nnodes[t]);
+  T.m = __builtin_amdgcn_readfirstlane(a.nmsgs[t]);
   T.t = t;
   const long mo = (long)t * a.M;
   // rows padded to MP with -1: the backward's one-hot operands (mt_onehot) read whole 16-message slices
@@ -119,6 +123,40 @@ __device__ __forceinline__ bf16x8 mt_onehot(const int* p, int node) {
   return __builtin_bit_cast(bf16x8, o);
 }
 
+// Input rows of the own tile held in registers a graph ahead (Fin <= 8: 32 Fin <= 256 floats, four per
+// lane): loads at clamped addresses inside graph g's P rows, issued while the previous graph computes.
+__device__ __forceinline__ bool mt_x_fits(const ClArgs& a) { return 32 * a.Fin <= 256; }
+__device__ __forceinline__ void mt_x_prefetch(float (&xv)[4], const ClArgs& a, int g, int w, int lane) {
+  const int rows = a.P - 32 * w, lim = (rows < 32 ? rows : 32) * a.Fin;
+  const float* xg = a.x + ((long)g * a.P + 32 * w) * a.Fin;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = lane + 64 * u;
+    xv[u] = xg[idx < lim ? idx : 0];
+  }
+}
+// prefetched rows -> cleared bf16 row image (+ the transposed image), the nv real rows only
+template <bool SAVE_T>
+__device__ __forceinline__ void mt_x_scatter(const float (&xv)[4], int nv, int Fin, __bf16* hR, __bf16* hT, int TS,
+                                             int trows, int lane) {
+  for (int i = lane; i < 32 * 32; i += 64) {
+    const int v = i >> 5, k = i & 31;
+    hR[v * kMfRS + k] = (__bf16)0.f;
+    if (SAVE_T && k < trows) hT[k * TS + v] = (__bf16)0.f;
+  }
+  const int nx = nv > 0 ? nv * Fin : 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = lane + 64 * u;
+    if (idx < nx) {
+      const int v = idx / Fin, k = idx - v * Fin;
+      const __bf16 b = (__bf16)xv[u];
+      hR[v * kMfRS + k] = b;
+      if (SAVE_T) hT[k * TS + v] = b;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
@@ -144,9 +182,15 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
   float* const sm = reinterpret_cast<float*>(G + m.sm);
   float* const pool = reinterpret_cast<float*>(G + m.pool);
   __syncthreads();
+  // graph g + gridDim.x's topology id and input rows are loaded while graph g computes
+  const bool xpre = mt_x_fits(a);
+  int t_cur = __builtin_amdgcn_readfirstlane(a.topo[blockIdx.x < a.B ? blockIdx.x : 0]);
+  float xv[4];
+  if (xpre) mt_x_prefetch(xv, a, blockIdx.x < a.B ? blockIdx.x : 0, w, tid & 63);
   for (int g = blockIdx.x; g < a.B; g += gridDim.x) {  // uniform over the workgroup
     const int lane = mf_lane(), r = lane & 31, hh = lane >> 5;
-    mt_load_topo(T, a, a.topo[g], w);
+    const int gn = g + gridDim.x < a.B ? g + gridDim.x : g;
+    mt_load_topo(T, a, __builtin_amdgcn_readfirstlane(t_cur), w);
     const int n = T.n, nl = n - 32 * w;  // real rows of the own tile (may be <= 0)
     // own rows: clear E, input features -> bf16 rows (and the saved per-tile transposed image)
     // save staging of the per-tile transposed image h^T (HPF x kMtTS bf16 <= one tile's 32 x kMfRS
@@ -156,8 +200,15 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
     {
       __bf16* hA = reinterpret_cast<__bf16*>(G + m.hR[0]) + 32 * w * kMfRS;
       __bf16* hT = reinterpret_cast<__bf16*>(G + m.hR[1]) + 32 * w * kMfRS;
-      mf_stage_input<SAVE>(a.x + ((long)g * a.P + 32 * w) * a.Fin, nl < 32 ? nl : 32, a.Fin, 32, hA, hT, kMtTS,
-                           m.hTrows0, lane);
+      if (xpre) {
+        mt_x_scatter<SAVE>(xv, nl < 32 ? nl : 32, a.Fin, hA, hT, kMtTS, m.hTrows0, lane);
+        t_cur = a.topo[gn];  // made uniform where it is used: a readfirstlane here would wait for it
+        mt_x_prefetch(xv, a, gn, w, lane);
+      } else {
+        mf_stage_input<SAVE>(a.x + ((long)g * a.P + 32 * w) * a.Fin, nl < 32 ? nl : 32, a.Fin, 32, hA, hT, kMtTS,
+                             m.hTrows0, lane);
+        t_cur = a.topo[gn];
+      }
       uint4* e4 = reinterpret_cast<uint4*>(E + 32 * w * m.NVS);
       for (int i = lane; i < 32 * m.NVS / 8; i += 64) e4[i] = make_uint4(0, 0, 0, 0);
     }
@@ -308,6 +359,26 @@ __device__ __forceinline__ void mt_att_bwd(const MtTopo& T, const float* da, con
   }
 }
 
+// issue (do not wait for) graph g's saved state of layer l: the own-tile images into this wave's ld
+// region and alpha of the own messages (16-B aligned superset) into the shared alpha region
+__device__ __forceinline__ void mt_issue_saved(const ClArgs& a, const MtLayout& m, const MtTopo& T, char* G, int g,
+                                               int l, int w, int lane) {
+  const char* src = reinterpret_cast<const char*>(a.blob) + (long)g * m.blob + m.bl_layer[l];
+  const char* st = src + w * m.bl_tile[l];
+  char* const ld = G + m.ld + w * m.ldw;
+  const int tb = m.bl_tile[l];
+  for (int o = 0; o < tb; o += 1024)
+    if (o + 16 * lane < tb)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(st + o + 16 * lane),
+                                       (__attribute__((address_space(3))) void*)(ld + o), 16, 0, 0);
+  const int a0 = (T.q0 & ~3) * 4, a1 = ((T.q1 + 3) & ~3) * 4;
+  const char* sa = src + m.NT * tb;
+  for (int o = a0; o < a1; o += 1024)
+    if (o + 16 * lane < a1)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(sa + o + 16 * lane),
+                                       (__attribute__((address_space(3))) void*)(G + m.al + o), 16, 0, 0);
+}
+
 template <int HPF, bool K2>
 __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -339,11 +410,20 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
 #pragma unroll
   for (int k = 0; k < CG; ++k) gattE[k] = gattP[k] = 0.f;
   const int NVS = m.NVS, MS = m.MS;
+  // Software pipeline over the graph loop: the next graph's topology id and d emb row are loaded during
+  // this graph's first processed conv, and each conv's saved state (plus, for a graph of the cached
+  // topology, the next graph's first one) is issued at the end of the conv before it: the loads whose
+  // round trips the one wave per SIMD used to wait out in full.
+  int t_cur = __builtin_amdgcn_readfirstlane(a.topo[blockIdx.x < a.B ? blockIdx.x : 0]), t_next = t_cur;
+  float ge_cur = a.demb[(long)(blockIdx.x < a.B ? blockIdx.x : 0) * a.H + ((tid & 31) < a.H ? (tid & 31) : 0)];
+  float ge_next = ge_cur;
+  bool pre = false;  // this graph's first processed conv's saved state is already in flight
   for (int g = blockIdx.x; g < a.B; g += gridDim.x) {
     // the partner may still read dy^T / E^T / the topology of the previous graph's first conv
     mt_barrier();
     int lane = mf_lane();
-    mt_load_topo(T, a, a.topo[g], w);
+    const int gn = g + gridDim.x < a.B ? g + gridDim.x : g;
+    mt_load_topo(T, a, __builtin_amdgcn_readfirstlane(t_cur), w);
     const int n = T.n, nl = n - 32 * w;
     float* const xl = reinterpret_cast<float*>(G + m.xl);
     float* const xr = reinterpret_cast<float*>(G + m.xr);
@@ -358,7 +438,7 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
     f32x16 dyt;
     {
       const int c = lane & 31, hh = lane >> 5;
-      const float ge = c < a.H ? a.demb[(long)g * a.H + c] / (float)n : 0.f;
+      const float ge = c < a.H ? ge_cur / (float)n : 0.f;
       const int nn = nl - 4 * hh;
 #pragma unroll
       for (int i = 0; i < 16; ++i) dyt[i] = (i & 3) + 8 * (i >> 2) < nn ? ge : 0.f;
@@ -371,22 +451,13 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
       const float* vec = lds + (l == 0 ? 0 : kMfVec);
       const int hrows = l == 0 ? m.hTrows0 : m.hTrows;
       // this layer's saved own-tile images (rows of h, per-tile h^T) and alpha of the own messages
-      {
-        const char* src = reinterpret_cast<const char*>(a.blob) + (long)g * m.blob + m.bl_layer[l];
-        const char* st = src + w * m.bl_tile[l];
-        const int tb = m.bl_tile[l];
-        for (int o = 0; o < tb; o += 1024)
-          if (o + 16 * lane < tb)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(st + o + 16 * lane),
-                                             (__attribute__((address_space(3))) void*)(ld + o), 16, 0, 0);
-        const int a0 = (T.q0 & ~3) * 4, a1 = ((T.q1 + 3) & ~3) * 4;
-        const char* sa = src + m.NT * tb;
-        for (int o = a0; o < a1; o += 1024)
-          if (o + 16 * lane < a1)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(sa + o + 16 * lane),
-                                             (__attribute__((address_space(3))) void*)(G + m.al + o), 16, 0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        cl_wave_sync();
+      if (!pre) mt_issue_saved(a, m, T, G, g, l, w, lane);
+      pre = false;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      cl_wave_sync();
+      if (l == a.L - 1) {  // the next graph's scalars ride along with this conv
+        t_next = a.topo[gn];  // made uniform where it is used
+        ge_next = a.demb[(long)gn * a.H + (r < a.H ? r : 0)];
       }
       const __bf16* hin = reinterpret_cast<const __bf16*>(ld);                  // [32][kMfRS]
       const __bf16* hT = reinterpret_cast<const __bf16*>(ld + mt_tile_hR_bytes());  // [hrows][kMtTS]
@@ -522,7 +593,20 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
       // clear the own E^T rows for the next layer's scatter (other waves write them only after B1)
       for (int i = lane; i < 32 * NVS / 8; i += 64) reinterpret_cast<uint4*>(etw)[i] = make_uint4(0, 0, 0, 0);
       cl_wave_sync();
+      // the next conv's saved state: this wave's ld images are dead (dW / dh / ReLU mask read above) and
+      // both waves are past B2, the last read of the shared alpha region.  Issued after the last LDS
+      // access of the conv: the compiler makes any later LDS access wait for LDS-DMA loads.
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (l > 0) {
+        mt_issue_saved(a, m, T, G, g, l - 1, w, lane);
+        pre = true;
+      } else if (gn != g && __builtin_amdgcn_readfirstlane(t_next) == T.t) {
+        mt_issue_saved(a, m, T, G, gn, a.L - 1, w, lane);
+        pre = true;
+      }
     }
+    t_cur = t_next;
+    ge_cur = ge_next;
   }
   // per-wave gradients -> LDS images (the whole per-graph region is free now) -> workgroup sum
   __syncthreads();

@@ -1,6 +1,5 @@
 #!/bin/bash
-# gnn_mt backward with one-hot operands generated from the LDS topology (new, in-tree) vs the ab/wt
-# checkout of HEAD (old: one-hot fragments loaded from HBM): 50-node GPU tests, then syn50 bench x3 interleaved
+# gnn_mt A/B: in-tree (new) vs the ab/wt checkout (old): 50-node GPU tests, then syn50 bench x3 interleaved
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
