@@ -491,15 +491,20 @@ class BatchedTrainer:
                 # syn50: 4.10k unmasked vs 3.56k masked).  GSC_LEARNER_MASK=0/1 forces either.
                 mask_env = os.environ.get("GSC_LEARNER_MASK", "auto")
                 small = (160 * 1024) // max(int(sim.ctx.lds_per_env), 1) >= 3
-                if mask_env == "0" or (mask_env == "auto" and not small):
+                learner_unmasked = mask_env == "0" or (mask_env == "auto" and not small)
+                if learner_unmasked:
                     self.learn_stream = torch.cuda.Stream(self.device)
                 else:
                     self.learn_stream = torch.cuda.ExternalStream(
                         nat.create_cu_masked_stream(list(range(k, n))), device=self.device)
                 # The act path (actor forward + exploration of step t+1) sits between two simulator
                 # steps, when the learner's CUs are idle too (update t done, update t+1 waits for it):
-                # GSC_ACT_STREAM=1 runs it on an unmasked stream instead of the simulator's CUs
-                if os.environ.get("GSC_ACT_STREAM", "0") == "1":
+                # an unmasked stream gives it every CU.  Auto: on when the learner is the longer chain
+                # (unmasked learner: the act path then waits on the learner and sits on the critical path;
+                # measured syn50 19.41k -> 19.63k, syn200 5.08k -> 5.13k, profiles/act_stream_ab.txt), off
+                # for simulator-bound small topologies (Abilene: measured slower).  GSC_ACT_STREAM=0/1 forces.
+                act_env = os.environ.get("GSC_ACT_STREAM", "auto")
+                if act_env == "1" or (act_env == "auto" and learner_unmasked):
                     self.act_stream = torch.cuda.Stream(self.device)
                 # persistent GNN grids sized to the CUs free while the simulator runs (one full round)
                 budget = int(os.environ.get("GSC_GNN_CU_BUDGET", str(n - k)))
