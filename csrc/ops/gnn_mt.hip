@@ -48,7 +48,7 @@ struct MtLayout {
   int NT, NV, NVS, MS;           // tiles, node rows (32 NT), bf16 stride of [.][node] images, G^T stride
   int hTrows0, hTrows;           // rows of the per-tile [k][node] images: encoder input (Fin -> 4), hidden
   // per-graph region (byte offsets)
-  int xl, xr, xlT, E, sc, mx, sm, topo, pool;  // forward (E doubles as E^T in the backward)
+  int xl, xr, xlT, E, sc, sm, topo, pool;  // forward (E doubles as E^T in the backward)
   int hR[2];                     // forward: ping-pong node images [NV][kMfRS] (save: h^T staged in dead rows)
   int ld, ldw;                   // backward: per-wave loaded layer images (own rows + own h^T), bytes per wave
   int al, da, dy, dyT[2], U, ss; // backward
@@ -65,6 +65,7 @@ __host__ __device__ __forceinline__ int mt_tile_hR_bytes() { return 32 * kMfRS *
 struct MtTopo {
   int *isrc, *idst;
   float* deg;
+  int* iptr;  // [P + 1] message range of each target node (per-node softmax / sums without atomics)
   int n, m, t, q0, q1;
 };
 
@@ -89,6 +90,7 @@ __device__ __forceinline__ void mt_load_topo(MtTopo& T, const ClArgs& a, int t, 
     T.idst[i] = v ? a.in_dst[mo + i] : -1;
   }
   for (int i = threadIdx.x; i < a.P; i += blockDim.x) T.deg[i] = a.deg[(long)t * a.P + i];
+  for (int i = threadIdx.x; i <= a.P; i += blockDim.x) T.iptr[i] = a.in_ptr[po + i];
 }
 
 // accumulator tile (rows = 32 nodes of the own tile, lane column c) -> bf16 [c][node] image at node
@@ -172,13 +174,13 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
   T.isrc = reinterpret_cast<int*>(G + m.topo);
   T.idst = T.isrc + a.MP;
   T.deg = reinterpret_cast<float*>(T.idst + a.MP);
+  T.iptr = reinterpret_cast<int*>(T.deg + a.P);
   T.t = -1;
   float* const xl = reinterpret_cast<float*>(G + m.xl);
   float* const xr = reinterpret_cast<float*>(G + m.xr);
   __bf16* const xlT = reinterpret_cast<__bf16*>(G + m.xlT);
   __bf16* const E = reinterpret_cast<__bf16*>(G + m.E);
   float* const sc = reinterpret_cast<float*>(G + m.sc);
-  int* const mx = reinterpret_cast<int*>(G + m.mx);
   float* const sm = reinterpret_cast<float*>(G + m.sm);
   float* const pool = reinterpret_cast<float*>(G + m.pool);
   __syncthreads();
@@ -234,10 +236,6 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
       mf_store_rows<HPF>(al, nl, xl + 32 * w * mf_xs(HPF), lane);
       mf_store_rows<HPF>(ar, nl, xr + 32 * w * mf_xs(HPF), lane);
       mt_store_T(al, xlT, m.NVS, 32 * w, HPF, lane, false);
-      for (int v = lane; v < 32; v += 64) {
-        mx[32 * w + v] = kMfKeyNegInf;
-        sm[32 * w + v] = 0.f;
-      }
       mt_barrier();  // B1: x_l rows and X_l^T of every tile
       // scores / softmax over the messages into the own tile (wave-local atomics)
       asm volatile("" ::: "memory");
@@ -258,14 +256,25 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
           z = a4.w + b4.w; s = fmaf(t4.w, z > 0.f ? z : kClSlope * z, s);
         }
         sc[q] = s;
-        atomicMax(mx + i, mf_key(s));
       }
       cl_wave_sync();
-      for (int q = T.q0 + lane; q < T.q1; q += 64) {
-        const int i = T.idst[q];
-        const float ex = __expf(sc[q] - mf_unkey(mx[i]));
-        sc[q] = ex;
-        atomicAdd(sm + i, ex);
+      // per-target max and exp-sum, lane = target node of the own tile over its contiguous message range
+      // (the target-sorted list): no LDS atomics -- messages of one target sat in consecutive lanes, so
+      // each atomic was an in-degree-way bank conflict
+      if (lane < 32) {
+        const int v = 32 * w + lane;
+        float sum = 0.f;
+        if (v < n) {
+          const int qa = T.iptr[v], qb = T.iptr[v + 1];
+          float mv = -INFINITY;
+          for (int q = qa; q < qb; ++q) mv = fmaxf(mv, sc[q]);
+          for (int q = qa; q < qb; ++q) {
+            const float ex = __expf(sc[q] - mv);
+            sc[q] = ex;
+            sum += ex;
+          }
+        }
+        sm[v] = sum;
       }
       cl_wave_sync();
       for (int q = T.q0 + lane; q < T.q1; q += 64) {
@@ -392,6 +401,7 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
   T.isrc = reinterpret_cast<int*>(G + m.topo);
   T.idst = T.isrc + a.MP;
   T.deg = reinterpret_cast<float*>(T.idst + a.MP);
+  T.iptr = reinterpret_cast<int*>(T.deg + a.P);
   T.t = -1;
   {
     const int lane = tid & 63;
@@ -468,7 +478,6 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
         mf_store_rows<HPF>(xa, nl, xl + 32 * w * mf_xs(HPF), lane);
         mf_store_rows<HPF>(xb, nl, xr + 32 * w * mf_xs(HPF), lane);
       }
-      for (int v = lane; v < 32; v += 64) ssum[32 * w + v] = 0.f;
       mt_barrier();  // B1: x_l rows, dy^T of every tile; E^T rows cleared
       // p_q = alpha_q (dy[i] . x_l[j]) / deg_i ; ssum_i = sum_{q -> i} p_q ; E^T[j][i] = alpha_q / deg_i
       asm volatile("" ::: "memory");
@@ -486,8 +495,16 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
         const float ad = al[q] / T.deg[i];
         const float p = ad * s;
         da[q] = p;
-        atomicAdd(ssum + i, p);
         ET[j * NVS + i] = (__bf16)ad;
+      }
+      cl_wave_sync();
+      // ssum_i per target node over its contiguous message range (no LDS atomics)
+      if (lane < 32) {
+        const int v = 32 * w + lane;
+        float sum = 0.f;
+        if (v < n)
+          for (int q = T.iptr[v]; q < T.iptr[v + 1]; ++q) sum += da[q];
+        ssum[v] = sum;
       }
       cl_wave_sync();
       // de_q = p_q - alpha_q ssum_i ; per channel z = x_l[j] + x_r[i]:
@@ -696,13 +713,12 @@ static MtLayout mt_layout(const ClArgs& a, int kind, int HPF) {
   m.xl = take(fb);
   m.xr = take(fb);
   m.E = take(m.NV * m.NVS * 2);
-  m.topo = take((2 * a.MP + a.P) * 4);
+  m.topo = take((2 * a.MP + 2 * a.P + 1) * 4);
   if (kind != kMtBwd) {
     m.hR[0] = take(m.NV * kMfRS * 2);
     m.hR[1] = take(m.NV * kMfRS * 2);
     m.xlT = take(HPF * m.NVS * 2);
     m.sc = take(M4b);
-    m.mx = take(m.NV * 4);
     m.sm = take(m.NV * 4);
     m.pool = take(m.NT * 32 * 4);
     static_assert(32 * kMtTS <= 32 * kMfRS, "the h^T staging must fit one tile's rows of hR");
