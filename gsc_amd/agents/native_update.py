@@ -169,9 +169,11 @@ class NativeDDPGUpdate:
         # output tiles of the products that stream the [B, A] action block / the A-long weights at large A
         # (scripts/gemm_tune.py syn200 at B = 25,600, profiles/gemm_tune_syn200.txt): the critic's action
         # projection 4.87 -> 3.44 ms with 128-row tiles and 64-deep K stages, its weight gradient 4.36 -> 3.91 ms
-        # with 64-deep stages, Mc 245 -> 144 us with 64 x 128 tiles
+        # with 64-deep stages, Mc 245 -> 144 us with 64 x 128 tiles.  They pay from A ~ 16k on: syn50 (A = 22,500)
+        # 19.88k -> 20.33k env-steps/s (profiles/large_a_tiles_syn50_ab.txt); Abilene (A = 1,728) keeps 64 x 64 x 32
         self.big_tiles = ({"act": {"tile": 1, "bk": 64}, "dw": {"tile": 2, "bk": 64}, "mc": {"tile": 3}}
-                          if A >= 65536 and os.environ.get("GSC_LARGE_A_TILES", "1") != "0" else {})
+                          if A >= int(os.environ.get("GSC_LARGE_A_MIN", "16384"))
+                          and os.environ.get("GSC_LARGE_A_TILES", "1") != "0" else {})
         self.slabs = mk(16 << 20)                            # split-K slabs (64 MB; bounds the split count)
         self.head_blocks = max(64, min(256, -(-B // 64)))    # one block per CU (>= 16 rows per wave)
         cm = self.critic.width(self.critic.nh - 1)
