@@ -105,14 +105,28 @@ static ClArgs make_args(py::dict t, uintptr_t params, uintptr_t x, uintptr_t top
 // CUs the launching stream may use: the device's count, or the budget of a CU-masked learner
 // stream (gnn_set_cu_budget) so persistent grids are sized to one full round on that partition.
 static int g_cu_budget = 0;
-void gnn_set_cu_budget(int n) { g_cu_budget = n > 0 ? n : 0; }
-static int num_cus() {
+// Work-queue counters of the multi-tile backward (one zeroed slot per launch, rotating; allocated with the
+// budget -- before any HIP-graph capture -- so a captured launch keeps its own slot and memset node)
+static int* g_work = nullptr;
+static unsigned g_work_next = 0;
+constexpr int kWorkSlots = 4096;
+static int device_cus() {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
     GSC_HIP_CHECK(hipGetDevice(&dev));
     GSC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
+  return cus;
+}
+void gnn_set_cu_budget(int n) {
+  g_cu_budget = n > 0 ? n : 0;
+  const char* e = getenv("GSC_GNN_WORKQ");
+  if (g_cu_budget > 0 && !g_work && !(e && e[0] == '0'))
+    GSC_HIP_CHECK(hipMalloc(&g_work, sizeof(int) * kWorkSlots));
+}
+static int num_cus() {
+  const int cus = device_cus();
   return g_cu_budget > 0 && g_cu_budget < cus ? g_cu_budget : cus;
 }
 
@@ -155,8 +169,19 @@ void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo
   c.demb = ptr<const float>(demb);
   c.partials = ptr<float>(partials);
   c.blob = reinterpret_cast<void*>(blob);
-  const int rows = path == kPathMf ? gnn_mf_backward(&c, stream, num_cus(), max_rows)
-                                   : gnn_mt_backward(&c, stream, num_cus(), max_rows);
+  int rows;
+  if (path == kPathMf) {
+    rows = gnn_mf_backward(&c, stream, num_cus(), max_rows);
+  } else if (g_work && g_cu_budget > 0) {
+    // CU-masked partner stream (overlap mode): the grid spans every CU and claims graphs from a counter,
+    // so the CUs the simulator releases mid-kernel join in (a fixed-stride grid sized to the budget left
+    // them idle until the next launch)
+    c.work = g_work + (g_work_next++ % kWorkSlots);
+    GSC_HIP_CHECK(hipMemsetAsync(c.work, 0, sizeof(int), stream_of(stream)));
+    rows = gnn_mt_backward(&c, stream, device_cus(), max_rows);
+  } else {
+    rows = gnn_mt_backward(&c, stream, num_cus(), max_rows);
+  }
   hipLaunchKernelGGL(column_sum_kernel, dim3((c.n_params + 31) / 32), dim3(256), 0, stream_of(stream),
                      (const float*)c.partials, ptr<float>(grad_out), rows, c.n_params);
   check_launch();

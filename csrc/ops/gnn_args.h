@@ -51,6 +51,7 @@ struct ClArgs {
   void* blob;                // MFMA path: per-graph forward state saved for the backward (or null)
   const float* params2;      // forward only: a second parameter set on the same graphs (or null) ...
   float* emb2;               // ... and its embeddings [B, H] (target actor + target critic in one launch)
+  int* work;                 // multi-tile backward: zeroed work-queue counter (graphs claimed by atomics), or null
 };
 
 __device__ __forceinline__ void cl_wave_sync() {

@@ -51,7 +51,7 @@ struct MtLayout {
   int xl, xr, xlT, E, sc, sm, topo, pool;  // forward (E doubles as E^T in the backward)
   int hR[2];                     // forward: ping-pong node images [NV][kMfRS] (save: h^T staged in dead rows)
   int ld, ldw;                   // backward: per-wave loaded layer images (own rows + own h^T), bytes per wave
-  int al, da, dy, dyT[2], U, ss; // backward
+  int al, da, dy, dyT[2], U, ss, wq; // backward
   int encW, encK;                // backward: per-wave encoder dW image
   int per_graph;                 // bytes of the per-graph region
   // saved blob per graph (HBM): per layer [tile chunk x NT][alpha]
@@ -424,15 +424,37 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
   // this graph's first processed conv, and each conv's saved state (plus, for a graph of the cached
   // topology, the next graph's first one) is issued at the end of the conv before it: the loads whose
   // round trips the one wave per SIMD used to wait out in full.
-  int t_cur = __builtin_amdgcn_readfirstlane(a.topo[blockIdx.x < a.B ? blockIdx.x : 0]), t_next = t_cur;
-  float ge_cur = a.demb[(long)(blockIdx.x < a.B ? blockIdx.x : 0) * a.H + ((tid & 31) < a.H ? (tid & 31) : 0)];
+  //
+  // With a.work (overlap mode: the grid covers every CU, including the simulator's, whose LDS frees up
+  // when its kernel ends) graphs are claimed from a zeroed counter instead of a fixed stride: workgroups
+  // placed late take what is left instead of a fixed share.  Wave 0 lane 0 claims the graph after next
+  // during the first conv (its round trip overlaps the conv) and publishes it in LDS for the next graph.
+  int* const wq = reinterpret_cast<int*>(G + m.wq);
+  int g = blockIdx.x, gq = blockIdx.x + gridDim.x;
+  if (a.work) {
+    if (tid == 0) {
+      wq[0] = atomicAdd(a.work, 1);
+      wq[1] = atomicAdd(a.work, 1);
+    }
+    __syncthreads();
+    g = __builtin_amdgcn_readfirstlane(wq[0]);
+    gq = __builtin_amdgcn_readfirstlane(wq[1]);
+  }
+  int claim = 0;
+  bool first = true;
+  int t_cur = __builtin_amdgcn_readfirstlane(a.topo[g < a.B ? g : 0]), t_next = t_cur;
+  float ge_cur = a.demb[(long)(g < a.B ? g : 0) * a.H + ((tid & 31) < a.H ? (tid & 31) : 0)];
   float ge_next = ge_cur;
   bool pre = false;  // this graph's first processed conv's saved state is already in flight
-  for (int g = blockIdx.x; g < a.B; g += gridDim.x) {
+  while (g < a.B) {  // uniform over the workgroup
     // the partner may still read dy^T / E^T / the topology of the previous graph's first conv
     mt_barrier();
     int lane = mf_lane();
-    const int gn = g + gridDim.x < a.B ? g + gridDim.x : g;
+    if (!a.work) gq = g + gridDim.x;
+    else if (!first) gq = __builtin_amdgcn_readfirstlane(wq[0]);  // written by wave 0 before the barrier
+    first = false;
+    const bool has_next = gq < a.B;
+    const int gn = has_next ? gq : g;
     mt_load_topo(T, a, __builtin_amdgcn_readfirstlane(t_cur), w);
     const int n = T.n, nl = n - 32 * w;
     float* const xl = reinterpret_cast<float*>(G + m.xl);
@@ -468,6 +490,7 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
       if (l == a.L - 1) {  // the next graph's scalars ride along with this conv
         t_next = a.topo[gn];  // made uniform where it is used
         ge_next = a.demb[(long)gn * a.H + (r < a.H ? r : 0)];
+        if (a.work && tid == 0) claim = atomicAdd(a.work, 1);  // the graph after next
       }
       const __bf16* hin = reinterpret_cast<const __bf16*>(ld);                  // [32][kMfRS]
       const __bf16* hT = reinterpret_cast<const __bf16*>(ld + mt_tile_hR_bytes());  // [hrows][kMtTS]
@@ -617,13 +640,15 @@ __global__ __launch_bounds__(128) void gnn_mt_bwd_kernel(ClArgs a, MtLayout m) {
       if (l > 0) {
         mt_issue_saved(a, m, T, G, g, l - 1, w, lane);
         pre = true;
-      } else if (gn != g && __builtin_amdgcn_readfirstlane(t_next) == T.t) {
+      } else if (has_next && __builtin_amdgcn_readfirstlane(t_next) == T.t) {
         mt_issue_saved(a, m, T, G, gn, a.L - 1, w, lane);
         pre = true;
       }
     }
     t_cur = t_next;
     ge_cur = ge_next;
+    if (a.work && tid == 0) wq[0] = claim;  // read by both waves after the next graph's first barrier
+    g = gq;
   }
   // per-wave gradients -> LDS images (the whole per-graph region is free now) -> workgroup sum
   __syncthreads();
@@ -732,6 +757,7 @@ static MtLayout mt_layout(const ClArgs& a, int kind, int HPF) {
     m.dyT[1] = take(HPF * m.NVS * 2);
     m.U = take(HPF * m.MS * 2);
     m.ss = take(m.NV * 4);
+    m.wq = take(16);  // work queue: the graph after next, claimed by wave 0 lane 0
     if (o < m.NT * kMfFlush * 4) o = m.NT * kMfFlush * 4;  // end-of-kernel per-wave gradient images
     m.encK = (a.Fin + 3) & ~3;
     m.encW = take(m.NT * 2 * 32 * m.encK * 4);  // beyond the end-of-kernel images

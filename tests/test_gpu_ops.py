@@ -63,6 +63,19 @@ def test_gnn_50_nodes_padded_50():
     _check_gnn(2, 2, 22, gs, 50, bf16=True)
 
 
+def test_gnn_mfma_two_tiles_work_queue():
+    """The overlap mode's two-tile backward: a CU budget set (as the trainer does for its masked learner
+    stream) switches gnn_mt's backward to a full-device grid claiming graphs from a zeroed counter; the
+    gradients must match the fp32 reference as with the fixed-stride grid."""
+    from gsc_amd.native import load
+    nat = load()
+    nat.gnn_set_cu_budget(64)
+    try:
+        _check_gnn(2, 2, 22, _mid_graphs(DEV), 64, bf16=True)
+    finally:
+        nat.gnn_set_cu_budget(0)
+
+
 @pytest.mark.parametrize("mid", [False, True], ids=["one-tile", "two-tile"])
 def test_gnn_forward_two_parameter_sets(mid):
     """gnn_forward2 (target actor + target critic embedders in one launch) == two gnn_forward launches."""
