@@ -108,8 +108,27 @@ static int g_cu_budget = 0;
 // Work-queue counters of the multi-tile backward (one zeroed slot per launch, rotating; allocated with the
 // budget -- before any HIP-graph capture -- so a captured launch keeps its own slot and memset node)
 static int* g_work = nullptr;
-static unsigned g_work_next = 0;
-constexpr int kWorkSlots = 4096;
+constexpr int kWorkSlots = 4096, kWorkCaptured = 3072;
+static int g_work_cap = 0;        // slots [0, kWorkCaptured): one per launch recorded into a HIP graph, never reused
+static unsigned g_work_eager = 0;  // slots [kWorkCaptured, kWorkSlots): eager launches, rotating (stream-ordered)
+// A zeroed counter slot for one launch on `st` (the memset is enqueued / captured with it), or null
+// (fixed-stride grid).  Captured launches get slots of their own: an eager launch on another stream
+// (the act path) must never share a counter with a replayed one.
+static int* work_slot(hipStream_t st) {
+  if (!g_work || g_cu_budget <= 0) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  GSC_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+  int slot;
+  if (cs == hipStreamCaptureStatusActive) {
+    if (g_work_cap >= kWorkCaptured) return nullptr;
+    slot = g_work_cap++;
+  } else {
+    slot = kWorkCaptured + (int)(g_work_eager++ % (kWorkSlots - kWorkCaptured));
+  }
+  int* p = g_work + slot;
+  GSC_HIP_CHECK(hipMemsetAsync(p, 0, sizeof(int), st));
+  return p;
+}
 static int device_cus() {
   static int cus = 0;
   if (!cus) {
@@ -130,6 +149,17 @@ static int num_cus() {
   return g_cu_budget > 0 && g_cu_budget < cus ? g_cu_budget : cus;
 }
 
+// Multi-tile forward: full-device grid claiming graphs from a fresh counter slot when a CU budget is set
+// (overlap mode, see gnn_backward), else the fixed-stride grid
+static void mt_forward_queued(ClArgs c, uintptr_t stream) {
+  c.work = work_slot(stream_of(stream));
+  if (c.work) {
+    gnn_mt_forward(&c, stream, device_cus());
+  } else {
+    gnn_mt_forward(&c, stream, num_cus());
+  }
+}
+
 void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo, uintptr_t emb, int B, int P, int Fin,
                  int H, std::vector<int> layer_of, uintptr_t stream, uintptr_t blob) {
   GnnPath path;
@@ -137,7 +167,7 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
   c.emb = ptr<float>(emb);
   c.blob = reinterpret_cast<void*>(blob);
   if (path == kPathMf) gnn_mf_forward(&c, stream, num_cus());
-  else gnn_mt_forward(&c, stream, num_cus());
+  else mt_forward_queued(c, stream);
 }
 
 // Two parameter sets on the same graphs (target actor + target critic embedders of next_obs).  One-tile
@@ -155,10 +185,10 @@ void gnn_forward2(py::dict tables, uintptr_t params, uintptr_t params2, uintptr_
     gnn_mf_forward(&c, stream, num_cus());
     return;
   }
-  gnn_mt_forward(&c, stream, num_cus());
+  mt_forward_queued(c, stream);
   c.params = ptr<const float>(params2);
   c.emb = ptr<float>(emb2);
-  gnn_mt_forward(&c, stream, num_cus());
+  mt_forward_queued(c, stream);
 }
 
 void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo, uintptr_t demb, uintptr_t partials,
@@ -172,12 +202,10 @@ void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo
   int rows;
   if (path == kPathMf) {
     rows = gnn_mf_backward(&c, stream, num_cus(), max_rows);
-  } else if (g_work && g_cu_budget > 0) {
+  } else if ((c.work = work_slot(stream_of(stream))) != nullptr) {
     // CU-masked partner stream (overlap mode): the grid spans every CU and claims graphs from a counter,
     // so the CUs the simulator releases mid-kernel join in (a fixed-stride grid sized to the budget left
     // them idle until the next launch)
-    c.work = g_work + (g_work_next++ % kWorkSlots);
-    GSC_HIP_CHECK(hipMemsetAsync(c.work, 0, sizeof(int), stream_of(stream)));
     rows = gnn_mt_backward(&c, stream, device_cus(), max_rows);
   } else {
     rows = gnn_mt_backward(&c, stream, num_cus(), max_rows);

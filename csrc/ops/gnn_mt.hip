@@ -185,13 +185,30 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
   float* const pool = reinterpret_cast<float*>(G + m.pool);
   __syncthreads();
   // graph g + gridDim.x's topology id and input rows are loaded while graph g computes
+  // a.work: graphs claimed from a zeroed counter by a full-device grid (as in the backward)
+  int* const wq = reinterpret_cast<int*>(G + m.wq);
+  int g = blockIdx.x, gq = blockIdx.x + gridDim.x;
+  if (a.work) {
+    if (tid == 0) {
+      wq[0] = atomicAdd(a.work, 1);
+      wq[1] = atomicAdd(a.work, 1);
+    }
+    __syncthreads();
+    g = __builtin_amdgcn_readfirstlane(wq[0]);
+    gq = __builtin_amdgcn_readfirstlane(wq[1]);
+  }
+  int claim = 0;
+  bool first = true;
   const bool xpre = mt_x_fits(a);
-  int t_cur = __builtin_amdgcn_readfirstlane(a.topo[blockIdx.x < a.B ? blockIdx.x : 0]);
+  int t_cur = __builtin_amdgcn_readfirstlane(a.topo[g < a.B ? g : 0]);
   float xv[4];
-  if (xpre) mt_x_prefetch(xv, a, blockIdx.x < a.B ? blockIdx.x : 0, w, tid & 63);
-  for (int g = blockIdx.x; g < a.B; g += gridDim.x) {  // uniform over the workgroup
+  if (xpre) mt_x_prefetch(xv, a, g < a.B ? g : 0, w, tid & 63);
+  while (g < a.B) {  // uniform over the workgroup
     const int lane = mf_lane(), r = lane & 31, hh = lane >> 5;
-    const int gn = g + gridDim.x < a.B ? g + gridDim.x : g;
+    if (!a.work) gq = g + gridDim.x;
+    else if (!first) gq = __builtin_amdgcn_readfirstlane(wq[0]);  // published before the last graph's pool barrier
+    first = false;
+    const int gn = gq < a.B ? gq : g;
     mt_load_topo(T, a, __builtin_amdgcn_readfirstlane(t_cur), w);
     const int n = T.n, nl = n - 32 * w;  // real rows of the own tile (may be <= 0)
     // own rows: clear E, input features -> bf16 rows (and the saved per-tile transposed image)
@@ -206,10 +223,12 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
         mt_x_scatter<SAVE>(xv, nl < 32 ? nl : 32, a.Fin, hA, hT, kMtTS, m.hTrows0, lane);
         t_cur = a.topo[gn];  // made uniform where it is used: a readfirstlane here would wait for it
         mt_x_prefetch(xv, a, gn, w, lane);
+        if (a.work && tid == 0) claim = atomicAdd(a.work, 1);  // the graph after next
       } else {
         mf_stage_input<SAVE>(a.x + ((long)g * a.P + 32 * w) * a.Fin, nl < 32 ? nl : 32, a.Fin, 32, hA, hT, kMtTS,
                              m.hTrows0, lane);
         t_cur = a.topo[gn];
+        if (a.work && tid == 0) claim = atomicAdd(a.work, 1);
       }
       uint4* e4 = reinterpret_cast<uint4*>(E + 32 * w * m.NVS);
       for (int i = lane; i < 32 * m.NVS / 8; i += 64) e4[i] = make_uint4(0, 0, 0, 0);
@@ -330,6 +349,7 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
       const int lane = mf_lane(), c = lane & 31, hh = lane >> 5;
       pl += __shfl_xor(pl, 32);
       if (hh == 0) pool[32 * w + c] = pl;
+      if (a.work && tid == 0) wq[0] = claim;
       mt_barrier();
       if (w == 0 && hh == 0 && c < a.H) {
         float s = 0.f;
@@ -337,6 +357,7 @@ __global__ __launch_bounds__(128) void gnn_mt_fwd_kernel(ClArgs a, MtLayout m) {
         a.emb[(long)g * a.H + c] = s / (float)n;
       }
     }
+    g = gq;
   }
 }
 
@@ -746,6 +767,7 @@ static MtLayout mt_layout(const ClArgs& a, int kind, int HPF) {
     m.sc = take(M4b);
     m.sm = take(m.NV * 4);
     m.pool = take(m.NT * 32 * 4);
+    m.wq = take(16);  // work queue: the graph after next, claimed by wave 0 lane 0
     static_assert(32 * kMtTS <= 32 * kMfRS, "the h^T staging must fit one tile's rows of hR");
   } else {
     m.ldw = (mt_tile_hR_bytes() + HPF * kMtTS * 2 + 15) & ~15;
