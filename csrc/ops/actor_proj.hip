@@ -22,6 +22,8 @@
 #include <hip/hip_bf16.h>
 #include <pybind11/pybind11.h>
 
+#include <cstdlib>
+
 #include "../common.h"
 
 namespace py = pybind11;
@@ -265,6 +267,8 @@ int actor_proj(uintptr_t h, long ldh, uintptr_t w, long ldw, uintptr_t bias, uin
   // left 200 workgroups walking every tile (1.2 ms at B = 25,600): 8 splits, one per XCD.  Small
   // batches: >= 256 workgroups with S a multiple of 8 (XCD grouping).
   int S = rbs >= 128 ? (tiles >= 128 ? 8 : 1) : ((256 + rbs - 1) / rbs + 7) / 8 * 8;
+  static const int s_env = getenv("GSC_APROJ_SPLITS") ? atoi(getenv("GSC_APROJ_SPLITS")) : 0;  // tuning override
+  if (s_env > 0) S = s_env;
   while (S > 1 && (long)S * M * J > slab_floats) S = S > 8 ? S - 8 : 1;
   GSC_CHECK((long)S * M * J <= slab_floats, "actor_proj: slabs too small");
   if (S > tiles) S = tiles;
