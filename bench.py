@@ -212,6 +212,7 @@ def main():
                 "global_batch": trainer.batch_size * info.world_size,
                 "seq_len": sim.episode_steps,
                 "parallelism": f"dp{info.world_size}",
+                **({"dist_forced": True, "dist_backend": info.backend} if info.forced else {}),
                 "envs_per_gpu": args.envs,
                 "total_envs": total_envs,
                 "learner_batch_per_gpu": trainer.batch_size,

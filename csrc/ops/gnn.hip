@@ -15,6 +15,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -120,7 +121,16 @@ static int* work_slot(hipStream_t st) {
   GSC_HIP_CHECK(hipStreamIsCapturing(st, &cs));
   int slot;
   if (cs == hipStreamCaptureStatusActive) {
-    if (g_work_cap >= kWorkCaptured) return nullptr;
+    if (g_work_cap >= kWorkCaptured) {
+      // (slots of destroyed graphs are not recycled: a long run of re-captures ends up here)
+      static bool warned = false;
+      if (!warned) {
+        warned = true;
+        fprintf(stderr, "[gsc_amd] gnn: %d captured work-queue slots used up; further captured launches use "
+                        "the fixed-stride grid (slower)\n", kWorkCaptured);
+      }
+      return nullptr;
+    }
     slot = g_work_cap++;
   } else {
     slot = kWorkCaptured + (int)(g_work_eager++ % (kWorkSlots - kWorkCaptured));

@@ -585,6 +585,10 @@ static void parallel_for(int n, int threads, F&& fn) {
 // ------------------------------------------------------------------------------------------------
 // Context object owned by Python
 // ------------------------------------------------------------------------------------------------
+#ifdef GSC_SIM_ISA_ONLY
+// register / ISA analysis build (scripts/sim_resources.py): only the named instantiation
+template __global__ void sim_step_kernel<GSC_SIM_ISA_ONLY>(SimArgs);
+#else
 class SimContext {
  public:
   SimContext(py::dict dims, py::dict cfg, py::list topos, bool device, int host_threads)
@@ -862,5 +866,6 @@ void register_sim(py::module_& m) {
   m.attr("SIM_NUM_STATS") = kNumStats;
   m.attr("SIM_HEADER_BYTES") = (int)sizeof(Header);
 }
+#endif  // GSC_SIM_ISA_ONLY
 
 }  // namespace gsc

@@ -61,6 +61,8 @@ class DDPGLearner:
         if zero is None:
             zero = os.environ.get("GSC_DP_ZERO", "0") == "1"
         self.zero = bool(zero and self.dist.enabled)
+        # bf16 gradient all-reduce (half the bytes on xGMI; fp32 master weights / moments): opt-in
+        self.grad_bf16 = self.dist.enabled and not self.zero and os.environ.get("GSC_DP_GRAD_BF16", "0") == "1"
         ba = 8 * self.dist.world_size if self.zero else 0   # equal shards per bucket
         self.actor_flat = FlatParams(self.actor, bucket_align=ba)
         self.critic_flat = FlatParams(self.critic, bucket_align=ba)
@@ -139,10 +141,17 @@ class DDPGLearner:
             self._act_native = NativeAct(self, E)
 
     def _allreduce(self, flat: FlatParams, lo: int = 0, hi: Optional[int] = None):
+        """Issue the sum-all-reduce of ``flat.grad[lo:hi]`` (fp32, or bf16 with ``GSC_DP_GRAD_BF16=1``)."""
         if not self.dist.enabled:
             return None
-        g = flat.grad if (lo == 0 and hi is None) else flat.grad[lo:hi]
-        return allreduce_sum_(g, async_op=True)
+        from gsc_amd.parallel.dist import GradReduce
+        sl = slice(lo, hi)
+        staging = None
+        if self.grad_bf16:
+            if getattr(flat, "grad16", None) is None:
+                flat.grad16 = torch.zeros_like(flat.grad, dtype=torch.bfloat16)
+            staging = flat.grad16[sl]
+        return GradReduce(flat.grad[sl], staging)
 
     # -- update stages of the autograd path (CPU; GPU reference with GSC_NATIVE_LEARNER=0) -------
     def _target(self, b: Batch) -> torch.Tensor:
@@ -346,9 +355,9 @@ class DDPGLearner:
         graphs = []
         # one process: one graph; data parallel: one graph per stage (collectives between them, eager);
         # a stage that launches nothing (autograd path's embedder stage) gets no graph
-        groups = [stages] if self.dist.world_size == 1 else [[f] for f in stages]
+        groups = [stages] if not self.dist.enabled else [[f] for f in stages]
         for k, grp in enumerate(groups):
-            if self.dist.world_size > 1 and not self.native_ok and k == 3:
+            if self.dist.enabled and not self.native_ok and k == 3:
                 graphs.append(None)
                 continue
             g = torch.cuda.CUDAGraph()
@@ -360,22 +369,42 @@ class DDPGLearner:
         # capture recorded but did not execute the update: the caller's replay performs it
 
     # checkpointing --------------------------------------------------------------------------
+    # Parameters and Adam moments are stored packed (per parameter, no alignment padding): the flat layout
+    # depends on the ZeRO bucket alignment (world size), the packed form does not, so a checkpoint resumes
+    # under any rank count with or without the sharded optimizer.  ZeRO: state_dict is a collective.
+    _NETS = (("actor", "actor_flat"), ("critic", "critic_flat"), ("target_actor", "target_actor_flat"),
+             ("target_critic", "target_critic_flat"))
+
     def state_dict(self) -> dict:
-        return {"actor": self.actor_flat.view().detach().clone(), "critic": self.critic_flat.view().detach().clone(),
-                "target_actor": self.target_actor_flat.view().detach().clone(),
-                "target_critic": self.target_critic_flat.view().detach().clone(),
-                "actor_opt": self.actor_opt.state_dict(), "critic_opt": self.critic_opt.state_dict(),
-                "updates": self.updates}
+        sd = {"layout": "packed", "updates": self.updates}
+        for key, attr in self._NETS:
+            fp = getattr(self, attr)
+            sd[key] = fp.pack(fp.flat.detach()).clone()
+        for key, opt in (("actor_opt", self.actor_opt), ("critic_opt", self.critic_opt)):
+            o = opt.state_dict()
+            o["m"], o["v"] = opt.fp.pack(o["m"]).clone(), opt.fp.pack(o["v"]).clone()
+            sd[key] = o
+        return sd
 
     def load_state_dict(self, sd: dict) -> None:
-        self.actor_flat.load_flat_(sd["actor"].to(self.device))
-        self.critic_flat.load_flat_(sd["critic"].to(self.device))
-        self.target_actor_flat.load_flat_(sd["target_actor"].to(self.device))
-        self.target_critic_flat.load_flat_(sd["target_critic"].to(self.device))
-        self.actor_opt.load_state_dict({k: (v.to(self.device) if torch.is_tensor(v) else v)
-                                        for k, v in sd["actor_opt"].items()})
-        self.critic_opt.load_state_dict({k: (v.to(self.device) if torch.is_tensor(v) else v)
-                                         for k, v in sd["critic_opt"].items()})
+        """Every rank validates every tensor's length before any collective runs (a mismatch raises on all
+        ranks alike instead of leaving some of them blocked in the ZeRO moment scatter)."""
+        packed = sd.get("layout") == "packed"
+        tens = {}
+        for key, attr in self._NETS:
+            fp = getattr(self, attr)
+            t = sd[key].to(self.device).reshape(-1)
+            tens[key] = fp.unpack(t if packed else fp.pack_legacy(t))
+        opts = {}
+        for key, opt in (("actor_opt", self.actor_opt), ("critic_opt", self.critic_opt)):
+            o = {k: (v.to(self.device) if torch.is_tensor(v) else v) for k, v in sd[key].items()}
+            for mk in ("m", "v"):
+                o[mk] = opt.fp.unpack(o[mk] if packed else opt.fp.pack_legacy(o[mk]))
+            opts[key] = o
+        for key, attr in self._NETS:
+            getattr(self, attr).load_flat_(tens[key])
+        self.actor_opt.load_state_dict(opts["actor_opt"])
+        self.critic_opt.load_state_dict(opts["critic_opt"])
         self.updates = int(sd.get("updates", 0))
         if self._act_native is not None:  # weights written outside the optimizer
             self._act_native.rowtab_dirty = True

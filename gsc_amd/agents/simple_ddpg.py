@@ -375,8 +375,12 @@ class SimpleDDPG(RLSPAgent):
             why = "missing"
             if os.path.exists(rp):
                 dr = ckpt.load_checkpoint(rp)
-                got = dr.get("meta", {}).get("stamp")
-                want = ckpt.save_stamp(sd, self.dist.world_size, stamp.get("nonce", ""))
+                # stamps written before the per-save nonce existed have none: compare them as nonce ''
+                got = dict(dr.get("meta", {}).get("stamp") or {})
+                got.setdefault("nonce", "")
+                stamp = dict(stamp)
+                stamp.setdefault("nonce", "")
+                want = ckpt.save_stamp(sd, self.dist.world_size, stamp["nonce"])
                 if got == stamp and stamp == want:
                     local = dr["state"]
                     local["trainer"]["learner"] = sd["trainer"]["learner"]

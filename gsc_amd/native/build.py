@@ -10,6 +10,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import glob
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -55,14 +56,33 @@ def _headers():
     return glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
 
 
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _deps(path: str, seen=None) -> set:
+    """Local headers a source includes, transitively (quoted includes resolved next to the includer)."""
+    seen = set() if seen is None else seen
+    try:
+        text = open(path).read()
+    except OSError:
+        return seen
+    for inc in _INC.findall(text):
+        h = os.path.normpath(os.path.join(os.path.dirname(path), inc))
+        if h not in seen and os.path.exists(h):
+            seen.add(h)
+            _deps(h, seen)
+    return seen
+
+
 def _obj(src: str, sanitize: bool = False) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
     return os.path.join(BUILD + ("_asan" if sanitize else ""), rel + ".o")
 
 
-def _compile(src: str, newest_header: float, sanitize: bool = False) -> str:
+def _compile(src: str, sanitize: bool = False) -> str:
     obj = _obj(src, sanitize)
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), newest_header):
+    newest = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _deps(src)])
+    if os.path.exists(obj) and os.path.getmtime(obj) >= newest:
         return obj
     cmd = [HIPCC, "-c", src, "-o", obj] + _flags(src) + _includes() + (SAN_COMPILE if sanitize else [])
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -74,9 +94,8 @@ def _compile(src: str, newest_header: float, sanitize: bool = False) -> str:
 def build(verbose: bool = True, jobs: int = 8, sanitize: bool = False) -> str:
     os.makedirs(BUILD + ("_asan" if sanitize else ""), exist_ok=True)
     srcs = _sources()
-    newest_header = max([os.path.getmtime(h) for h in _headers()] + [0.0])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, newest_header, sanitize), srcs))
+        objs = list(ex.map(lambda s: _compile(s, sanitize), srcs))
     out = ext_path(sanitize)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):

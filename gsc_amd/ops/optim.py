@@ -20,6 +20,7 @@ class FlatParams:
         """``bucket_align`` > 0 (sharded optimizer, :mod:`gsc_amd.parallel.zero`): the block after the
         embedder and the buffer end start on multiples of it, so both buckets split into equal shards."""
         self.module = module
+        self.matrix_align = matrix_align
         named = list(module.named_parameters())
         self.params: List[nn.Parameter] = [p for _, p in named]
         self.names = [n for n, _ in named]
@@ -107,6 +108,43 @@ class FlatParams:
     def load_flat_(self, src: torch.Tensor) -> None:
         self.flat[: self.numel].copy_(src[: self.numel])
         self.refresh_shadow()
+
+    # -- layout-independent form (checkpoints) -------------------------------------------------------
+    # The flat layout depends on bucket_align (ZeRO on/off, world size), so checkpoints store every
+    # parameter-shaped tensor (weights, Adam moments) *packed*: the parameters' elements back to back in
+    # named_parameters() order, no alignment padding.  Loading re-packs into the current layout.
+    def packed_numel(self) -> int:
+        return sum(p.numel() for p in self.params)
+
+    def pack(self, t: torch.Tensor) -> torch.Tensor:
+        """Packed copy of a flat-layout tensor (this buffer's layout) — layout-free checkpoint form."""
+        return torch.cat([t[o:o + p.numel()].reshape(-1) for p, o in zip(self.params, self.offsets)])
+
+    def unpack(self, packed: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Flat-layout tensor (padding zero) from a packed one."""
+        if packed.numel() != self.packed_numel():
+            raise ValueError(f"packed tensor has {packed.numel()} elements, the network {self.packed_numel()}")
+        out = torch.zeros_like(self.flat) if out is None else out
+        k = 0
+        for p, o in zip(self.params, self.offsets):
+            n = p.numel()
+            out[o:o + n].copy_(packed[k:k + n])
+            k += n
+        return out
+
+    def legacy_offsets(self) -> List[int]:
+        """Offsets of the unsharded layout (bucket_align 0): the layout of format-2 checkpoints."""
+        total, out = 0, []
+        for name, p in zip(self.names, self.params):
+            if p.dim() == 2 and not name.startswith("embedder."):
+                total = -(-total // self.matrix_align) * self.matrix_align
+            out.append(total)
+            total += p.numel()
+        return out
+
+    def pack_legacy(self, t: torch.Tensor) -> torch.Tensor:
+        """Packed form of a tensor stored in the unsharded layout (pre-packed checkpoints)."""
+        return torch.cat([t[o:o + p.numel()].reshape(-1) for p, o in zip(self.params, self.legacy_offsets())])
 
 
 class FusedAdamPolyak:
@@ -204,12 +242,14 @@ class FusedAdamPolyak:
                               self.tau if t is not None else 0.0, f16.data_ptr() if f16 is not None else 0,
                               t16.data_ptr() if t16 is not None else 0, skip, stream)
             return
-        bad = torch.tensor([0 if bool(torch.isfinite(g).all()) else 1], dtype=torch.int32)
         if self.guard_enabled:
+            # one decision on every rank (the shards differ); with the guard off every rank steps and
+            # all-gathers unconditionally, like the unsharded path
+            bad = torch.tensor([0 if bool(torch.isfinite(g).all()) else 1], dtype=torch.int32)
             agree_any(bad)
-        if int(bad[0]):
-            self.guard[1] += 1
-            return
+            if int(bad[0]):
+                self.guard[1] += 1
+                return
         self._host_step += 1
         self.step_t.add_(1)
         for b in range(len(z.buckets)):

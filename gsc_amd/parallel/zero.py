@@ -18,8 +18,8 @@ are separate buckets (the MLP bucket's reduce-scatter overlaps the embedder back
 does on the unsharded path).  Every bucket is padded to a multiple of 8 W elements inside the flat buffer
 (``FlatParams(bucket_align=8 W)``), so all shards are equal and no shard straddles two buckets.
 
-gloo has no reduce-scatter: the CPU rehearsal all-reduces the bucket and keeps its shard (same result,
-twice the bytes).  SURVEY §2.8 D1 / §5.8 (new capability: the reference is single-process).
+The CPU rehearsal (gloo) issues the same ``reduce_scatter_tensor`` / ``all_gather_into_tensor`` calls as
+RCCL does on GPUs, and ``GSC_DIST_FORCE=1`` runs them through a world-size-1 RCCL group on one GPU.  SURVEY §2.8 D1 / §5.8 (new capability: the reference is single-process).
 """
 from __future__ import annotations
 
@@ -59,36 +59,19 @@ class ZeroShards:
 
 def reduce_scatter_bucket(full: torch.Tensor, lo: int, hi: int, out: torch.Tensor, world: int, rank: int,
                           async_op: bool = False):
-    """Sum ``full[lo:hi]`` over ranks; ``out`` receives this rank's contiguous 1/W of the sum."""
-    src = full[lo:hi]
-    if dist.get_backend() == "nccl":
-        return dist.reduce_scatter_tensor(out, src, op=dist.ReduceOp.SUM, async_op=async_op)
-    # gloo: no reduce-scatter -- all-reduce in place, keep the shard (the rehearsal path)
-    work = dist.all_reduce(src, op=dist.ReduceOp.SUM, async_op=async_op)
-    c = (hi - lo) // world
-
-    class _Shard:
-        def wait(self_inner):
-            if work is not None and async_op:
-                work.wait()
-            out.copy_(src[rank * c:(rank + 1) * c])
-
-    if async_op:
-        return _Shard()
-    out.copy_(src[rank * c:(rank + 1) * c])
-    return None
+    """Sum ``full[lo:hi]`` over ranks; ``out`` receives this rank's contiguous 1/W of the sum (one
+    ``reduce_scatter_tensor``: RCCL on GPUs, gloo on the CPU -- the same call, shapes and semantics)."""
+    assert out.numel() * world == hi - lo
+    return dist.reduce_scatter_tensor(out, full[lo:hi], op=dist.ReduceOp.SUM, async_op=async_op)
 
 
 def all_gather_bucket(full: torch.Tensor, lo: int, hi: int, world: int, rank: int) -> None:
-    """Every rank's shard of ``full[lo:hi]`` to every rank (in place: the own shard is the input)."""
+    """Every rank's shard of ``full[lo:hi]`` to every rank (the own shard is the input; it is copied out
+    first because the output buffer contains it)."""
     c = (hi - lo) // world
     dst = full[lo:hi]
-    mine = dst[rank * c:(rank + 1) * c]
-    if dist.get_backend() == "nccl":
-        dist.all_gather_into_tensor(dst, mine)
-        return
-    parts = [dst[k * c:(k + 1) * c] for k in range(world)]
-    dist.all_gather(parts, mine.clone())
+    mine = dst[rank * c:(rank + 1) * c].clone()
+    dist.all_gather_into_tensor(dst, mine)
 
 
 def agree_any(flag: torch.Tensor) -> None:

@@ -160,6 +160,89 @@ def test_dp_sharded_optimizer_matches_single_process():
                                atol=1e-7)
 
 
+def _zero_resume_worker(rank, port, out_dir, src):
+    """ZeRO-1 at W=2: resume from ``src`` (a non-ZeRO, single-process checkpoint) when given, else train
+    2 updates and write the (collective) checkpoint; then one more update from a fresh learner that
+    loads it."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from gsc_amd.agents import Batch
+    from gsc_amd.parallel.dist import init_distributed, shutdown
+    info = init_distributed("cpu")
+    bs = _batches(3)
+    sl = slice(rank * B_PER_RANK, (rank + 1) * B_PER_RANK)
+    if src:
+        sd = torch.load(src, weights_only=True)
+    else:
+        learner, _ = _learner(info, seed=3, zero=True)
+        for b in bs[:2]:
+            learner.update(Batch(*(t[sl] for t in b)))
+        sd = learner.state_dict()              # collective (moments all-gathered)
+        if rank == 0:
+            torch.save(sd, os.path.join(out_dir, "zero_sd.pt"))
+    fresh, _ = _learner(info, seed=77, zero=True)
+    fresh.load_state_dict(sd)
+    fresh.update(Batch(*(t[sl] for t in bs[2])))
+    torch.save({f"{net}.{n}": p.detach().clone() for net in ("actor", "critic", "target_actor")
+                for n, p in getattr(fresh, net).named_parameters()}, os.path.join(out_dir, f"zr{rank}.pt"))
+    shutdown()
+
+
+def test_dp_resume_across_zero_and_world_size():
+    """Checkpoints are layout-free (packed per parameter): a ZeRO W=2 checkpoint resumes in one process
+    without ZeRO, and a single-process checkpoint resumes under ZeRO W=2 -- both equal to the uninterrupted
+    single-process run (the flat layout's bucket padding depends on the world size)."""
+    from gsc_amd.agents import Batch  # noqa: F401
+    bs = _batches(3)
+    ref, _ = _learner(None, seed=3)
+    for b in bs:
+        ref.update(b)
+    want = {f"{net}.{n}": p.detach().clone() for net in ("actor", "critic", "target_actor")
+            for n, p in getattr(ref, net).named_parameters()}
+    with tempfile.TemporaryDirectory() as d:
+        # (1) ZeRO W=2 -> checkpoint -> ZeRO W=2 resume
+        mp.start_processes(_zero_resume_worker, args=(_free_port(), d, ""), nprocs=WORLD, join=True,
+                           start_method="spawn")
+        got = torch.load(os.path.join(d, "zr0.pt"), weights_only=True)
+        for k in want:
+            torch.testing.assert_close(got[k], want[k], rtol=1e-5, atol=1e-6)
+        # (2) the ZeRO checkpoint resumed by one process without ZeRO
+        one, _ = _learner(None, seed=55)
+        one.load_state_dict(torch.load(os.path.join(d, "zero_sd.pt"), weights_only=True))
+        one.update(bs[2])
+        for net in ("actor", "critic", "target_actor"):
+            for n, p in getattr(one, net).named_parameters():
+                torch.testing.assert_close(p.detach(), want[f"{net}.{n}"], rtol=1e-5, atol=1e-6)
+        # (3) a single-process checkpoint resumed under ZeRO W=2
+        two, _ = _learner(None, seed=3)
+        for b in bs[:2]:
+            two.update(b)
+        src = os.path.join(d, "single_sd.pt")
+        torch.save(two.state_dict(), src)
+        mp.start_processes(_zero_resume_worker, args=(_free_port(), d, src), nprocs=WORLD, join=True,
+                           start_method="spawn")
+        got = torch.load(os.path.join(d, "zr1.pt"), weights_only=True)
+        for k in want:
+            torch.testing.assert_close(got[k], want[k], rtol=1e-5, atol=1e-6)
+
+
+def test_learner_loads_legacy_flat_checkpoint():
+    """Pre-packed checkpoints (flat views of the unsharded layout) still load."""
+    a, _ = _learner(None, seed=3)
+    a.update(_batches(1)[0])
+    sd = a.state_dict()
+    legacy = {k: v for k, v in sd.items() if k != "layout"}
+    for key, attr in a._NETS:
+        legacy[key] = getattr(a, attr).view().clone()
+    for key, opt in (("actor_opt", a.actor_opt), ("critic_opt", a.critic_opt)):
+        legacy[key] = dict(sd[key], m=opt.m[:opt.fp.numel].clone(), v=opt.v[:opt.fp.numel].clone())
+    b, _ = _learner(None, seed=9)
+    b.load_state_dict(legacy)
+    assert torch.equal(b.actor_flat.flat, a.actor_flat.flat)
+    assert torch.equal(b.critic_opt.v, a.critic_opt.v)
+
+
 def test_dp_batched_trainer_replicas_identical():
     """Ranks step different envs (different seeds) yet hold identical parameters after every update;
     metrics are all-reduced (both ranks report the same whole-job counts)."""
@@ -306,3 +389,100 @@ def test_checkpoint_format_1_rejected(tmp_path):
     torch.save({"format": "gsc_amd.checkpoint/1", "meta": {}, "state": {}}, p)
     with pytest.raises(ValueError, match="no longer readable"):
         ck.load_checkpoint(p)
+
+
+def _forced_worker(rank, out_dir, zero):
+    """One process, GSC_DIST_FORCE=1: a world-size-1 process group; every collective is issued."""
+    os.environ["GSC_DIST_FORCE"] = "1"
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from gsc_amd.parallel.dist import init_distributed, shutdown
+    info = init_distributed("cpu")
+    assert info.forced and info.enabled and info.world_size == 1 and dist.is_initialized()
+    learner, _ = _learner(info, seed=3, zero=zero)
+    assert learner.zero == zero
+    for b in _batches(3):
+        learner.update(b)
+    torch.save({f"{net}.{n}": p.detach().clone() for net in ("actor", "critic", "target_actor", "target_critic")
+                for n, p in getattr(learner, net).named_parameters()}, os.path.join(out_dir, f"f{int(zero)}.pt"))
+    shutdown()
+
+
+@pytest.mark.parametrize("zero", [False, True])
+def test_forced_world1_process_group_bit_identical(zero):
+    """GSC_DIST_FORCE=1 routes the update through the data-parallel code path (collectives between the
+    update stages; ZeRO-1 reduce-scatter / all-gather) over a world-size-1 group: bit-identical to the
+    process-local learner (the GPU twin runs the same over RCCL: tests/test_gpu_dp.py)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_forced_worker, args=(d, zero), nprocs=1, join=True, start_method="spawn")
+        got = torch.load(os.path.join(d, f"f{int(zero)}.pt"), weights_only=True)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)   # the worker's CPU GEMM reduction order
+    try:
+        ref, _ = _learner(None, seed=3)
+        for b in _batches(3):
+            ref.update(b)
+    finally:
+        torch.set_num_threads(nt)
+    for net in ("actor", "critic", "target_actor", "target_critic"):
+        for n, p in getattr(ref, net).named_parameters():
+            assert torch.equal(got[f"{net}.{n}"], p.detach()), f"{net}.{n}"
+
+
+def _bf16_worker(rank, port, out_dir, big):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from gsc_amd.parallel.dist import GradReduce, init_distributed, shutdown
+    info = init_distributed("cpu")
+    if big:
+        # a config-5-sized gradient (the syn200 actor: ~185 M fp32 values, SURVEY R1), bf16 vs fp32 sums
+        g = torch.Generator().manual_seed(100 + rank)
+        n = big
+        grad = torch.randn(n, generator=g) * 1e-3
+        ref = grad.clone()
+        GradReduce(ref, None).wait()
+        got = grad.clone()
+        GradReduce(got, torch.zeros(n, dtype=torch.bfloat16)).wait()
+        rel = ((got - ref).abs().max() / ref.abs().max()).item()
+        torch.save({"rel": torch.tensor(rel)}, os.path.join(out_dir, f"big{rank}.pt"))
+    else:
+        from gsc_amd.agents import Batch
+        os.environ["GSC_DP_GRAD_BF16"] = "1"
+        learner, _ = _learner(info, seed=3)
+        assert learner.grad_bf16
+        for b in _batches(3):
+            sl = slice(rank * B_PER_RANK, (rank + 1) * B_PER_RANK)
+            learner.update(Batch(*(t[sl] for t in b)))
+        torch.save({"actor": learner.actor_flat.flat.clone(), "critic": learner.critic_flat.flat.clone()},
+                   os.path.join(out_dir, f"bf{rank}.pt"))
+    shutdown()
+
+
+def test_dp_bf16_gradient_allreduce_close_to_fp32():
+    """GSC_DP_GRAD_BF16=1: replicas stay bit-identical, and 3 updates stay within bf16
+    rounding of the fp32-reduced single-process update (Adam's step is ~lr per element, so a relative
+    gradient error of ~2^-8 moves a parameter by far less than lr)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_bf16_worker, args=(_free_port(), d, 0), nprocs=WORLD, join=True, start_method="spawn")
+        r = [torch.load(os.path.join(d, f"bf{i}.pt"), weights_only=True) for i in range(WORLD)]
+    assert torch.equal(r[0]["actor"], r[1]["actor"]) and torch.equal(r[0]["critic"], r[1]["critic"])
+    ref, _ = _learner(None, seed=3)
+    for b in _batches(3):
+        ref.update(b)
+    for k, fp in (("actor", ref.actor_flat), ("critic", ref.critic_flat)):
+        d = (r[0][k] - fp.flat).abs().max().item()
+        assert d < 3 * 1e-3, (k, d)   # 3 updates of at most ~lr each; fp32 reduction differs by ~1e-7
+
+
+@pytest.mark.slow
+def test_dp_bf16_gradient_allreduce_config5_size():
+    """The bf16 all-reduce of a config-5-sized gradient (185 M values, 2 gloo ranks): max error relative
+    to the largest sum within bf16 rounding of the inputs and of the sum (2^-8 each)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_bf16_worker, args=(_free_port(), d, 185_000_000), nprocs=WORLD, join=True,
+                           start_method="spawn")
+        rel = [float(torch.load(os.path.join(d, f"big{i}.pt"), weights_only=True)["rel"]) for i in range(WORLD)]
+    assert max(rel) < 2 ** -7, rel
