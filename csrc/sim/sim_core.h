@@ -59,7 +59,8 @@ GSC_HD int target_flow(int32_t t) { return (int)(int16_t)((uint32_t)t >> 16); }
 struct alignas(16) Proc {  // 32 B
   uint8_t type, state;
   int16_t flow, parent, a, b, c, ret, pad;
-  double x, y;
+  double x;
+  int16_t n1, e1, len, pad1;  // forwarder: the next hop's node / edge (prefetched), path length
 };
 
 // A pending link-capacity return: return_link_resources' timeout, keyed like the SimPy event it replaces.
@@ -106,8 +107,7 @@ struct TopoDev {
   const int16_t* plen;      // [n*n]
   const int16_t* pnodes;    // [n*n*H]
   const int16_t* pedges;    // [n*n*H] edge id of each path hop (from the previous path node)
-  const double* phd;        // [n*n*H] delay of each path hop (pdelay[previous path node][hop]); null when
-                            // the topology is staged in LDS (pdelay is a cheap LDS lookup there)
+  const double* phd;        // [n*n*H] delay of each path hop (pdelay[previous path node][hop])
   const int16_t* edge_id;   // [n*n]
   const double* edge_cap;   // [E]
   const int16_t* ingress;   // [n_ing]
@@ -266,28 +266,40 @@ struct Env {
 // ------------------------------------------------------------------------------------------------
 // RNG helpers (per-env Philox stream; deterministic configs draw nothing)
 // ------------------------------------------------------------------------------------------------
-// The key schedule (10 round keys per word) is loop-invariant inside the event loop; an opaque copy
-// of the keys stops LICM from pinning all 20 round keys in SGPRs for the whole window (they are one
-// scalar add each to recompute; pinned, they pushed other values into spills).
-GSC_HD Philox4 env_philox(Env& S) {
-  uint32_t k0 = S.h->key0, k1 = S.h->key1;
+// Random draws and the fp64 transcendental functions behind them are kept out of the event loop's
+// instruction stream: on the device they are out-of-line functions taking scalars (the deterministic
+// configurations, e.g. the headline's, never call them; inlined, Philox rounds and fp64 log / exp / cos
+// sequences sat between the hot handler blocks -- ~30 % of the kernel's code).  Host: inline.
 #if defined(__HIP_DEVICE_COMPILE__)
-  k0 = __builtin_amdgcn_readfirstlane(k0);
-  k1 = __builtin_amdgcn_readfirstlane(k1);
-  asm volatile("" : "+s"(k0), "+s"(k1));
+#define GSC_COLD __device__ __attribute__((noinline))
+#else
+#define GSC_COLD inline
 #endif
-  return philox4x32_10(k0, k1, S.h->ctr++);
-}
-GSC_HD double rng_u01(Env& S) {
-  Philox4 r = env_philox(S);
+GSC_COLD double rng_u01_draw(uint32_t k0, uint32_t k1, uint64_t c) {
+  const Philox4 r = philox4x32_10(k0, k1, c);
   return u01_53(r.v[0], r.v[1]);
 }
-GSC_HD double rng_normal(Env& S, double mean, double std) {
-  if (std == 0.0) return mean;
-  Philox4 r = env_philox(S);
+GSC_COLD double rng_normal_draw(uint32_t k0, uint32_t k1, uint64_t c, double mean, double std) {
+  const Philox4 r = philox4x32_10(k0, k1, c);
   const double u1 = 1.0 - u01_53(r.v[0], r.v[1]);  // (0, 1]
   const double u2 = u01_53(r.v[2], r.v[3]);
   return mean + std * (sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+}
+GSC_COLD double exp_from_u01(double u, double mean) { return -log(1.0 - u) * mean; }     // expovariate(1/mean)
+GSC_COLD double pareto_from_u01(double u, double shape) { return exp(-log(1.0 - u) / shape); }  // pareto + 1
+GSC_COLD double log10_cold(double x) { return log10(x); }
+
+GSC_HD uint32_t env_key(uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+#else
+  return k;
+#endif
+}
+GSC_HD double rng_u01(Env& S) { return rng_u01_draw(env_key(S.h->key0), env_key(S.h->key1), S.h->ctr++); }
+GSC_HD double rng_normal(Env& S, double mean, double std) {
+  if (std == 0.0) return mean;
+  return rng_normal_draw(env_key(S.h->key0), env_key(S.h->key1), S.h->ctr++, mean, std);
 }
 GSC_HD int rng_int(Env& S, int n) {
   if (n <= 1) return 0;
@@ -336,6 +348,17 @@ __device__ __forceinline__ double wave_max_f64(double v) {
 }
 #endif
 
+// Topology-table read.  TLDS (device kernels whose topology tables are staged in LDS, known at compile
+// time): the generic table pointer is cast to the LDS address space, so the read is a ds_read rather
+// than a flat load (which waits on both the vector-memory and the LDS counters).
+template <bool TLDS, class V>
+GSC_HD V tab(const V* p, long i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (TLDS) return ((const __attribute__((address_space(3))) V*)p)[i];
+#endif
+  return p[i];
+}
+
 // ------------------------------------------------------------------------------------------------
 // Event / process primitives (SimPy contract)
 // ------------------------------------------------------------------------------------------------
@@ -367,7 +390,8 @@ GSC_HD int alloc_proc(Env& S, uint8_t type, uint8_t state, int flow, int parent)
   h->proc_head = h->proc_top > 0 ? (int)S.proc_free[h->proc_top - 1] : -1;
   Proc& p = S.procs[pid];
   p.type = type; p.state = state; p.flow = (int16_t)flow; p.parent = (int16_t)parent;
-  p.a = p.b = p.c = p.ret = 0; p.x = p.y = 0.0;
+  p.a = p.b = p.c = p.ret = 0; p.x = 0.0;
+  p.n1 = p.e1 = p.len = p.pad1 = 0;
   const int used = S.d.proc_cap - h->proc_top;
   if (used > h->max_procs) h->max_procs = used;
   return pid;
@@ -440,9 +464,9 @@ GSC_HD void ledger_push(Env& S, double t, int e, double dr) {
 }
 
 // Apply link e's returns that precede the current event, in key order, then refresh link_next[e].
-GSC_HD_CALL void ledger_apply(Env& S, int e) {
+GSC_HD_CALL void ledger_apply(Env& S, int e, double lnext) {
   const double now = S.h->now;
-  if (GSC_UNI(now < S.link_next[e])) return;  // nothing due (the common case: one LDS read)
+  if (GSC_UNI(now < lnext)) return;  // nothing due (the common case)
   const uint32_t ck = S.h->cur_key;
 #if defined(__HIP_DEVICE_COMPILE__)
   const int lane = wave_lane();
@@ -766,33 +790,47 @@ GSC_HD_CALL void run_decide(Env& S, const SimConst& K, const TopoDev& T, int pid
 }
 
 // DefaultFlowForwarder.forward_flow (default_forwarder.py:21-90); return_link_resources -> ledger_push.
-// BIG: unstaged topology tables (HBM): the hop delay comes from the per-hop table (T.phd).
-template <bool BIG = false>
+// The record carries the path state: a = path source, b = destination, c = index of the hop just
+// scheduled, ret / pad = its node / edge (its capacity return is recorded after the hop's timeout),
+// x = path delay, len = path length, n1 / e1 = the NEXT hop's node / edge, prefetched when this hop was
+// scheduled.  So a hop event needs one LDS round trip after the dispatch load: the link's capacity, next
+// return time and passed-traffic counter, read together with the following hop's node / edge / delay.
+template <bool BIG = false, bool TLDS = false>
 GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P0, const Flow& f0) {
   Proc P = P0;
   const int fid = GSC_UNI(P.flow);
   Flow f = f0;
-  const int n = GSC_UNI(T.n);
+  const int n = GSC_UNI(T.n), H = GSC_UNI(T.H);
   const int nxt = GSC_UNI(P.b);
   int rel_e = -1;  // link of the hop just taken: its capacity return is recorded after this step's event
+  int c, hop, e;   // the hop to take now: index on the path, node, edge
+  long pidx;
   if (GSC_UNI(P.state) == F_INIT) {
     const int cur = GSC_UNI(f.node);
-    const double pd = (cur != nxt) ? T.pdelay[cur * n + nxt] : 0.0;
+    const int row = cur * n + nxt;
+    pidx = (long)row * H;
+    // path delay, length and the first two hops in one round trip (H > 1: pidx + 1 stays in the table)
+    const double pd = (cur != nxt) ? tab<TLDS>(T.pdelay, row) : 0.0;
+    const int len = tab<TLDS>(T.plen, row);
+    hop = tab<TLDS>(T.pnodes, pidx);
+    e = tab<TLDS>(T.pedges, pidx);
+    P.n1 = H > 1 ? tab<TLDS>(T.pnodes, pidx + 1) : (int16_t)-1;
+    P.e1 = H > 1 ? tab<TLDS>(T.pedges, pidx + 1) : (int16_t)-1;
     if (GSC_UNI(f.ttl - pd <= 0)) { S.flows[fid].ttl = 0; proc_return(S, pid, P, 0); return; }
     if (GSC_UNI(cur == f.egress && f.fwd_eg)) { f.departed = 1; S.flows[fid].departed = 1; }
     if (cur == nxt) { proc_return(S, pid, P, 1); return; }
     P.a = (int16_t)cur;
-    P.c = 0;
+    P.len = (int16_t)len;
     P.x = pd;
+    c = 0;
+    hop = GSC_UNI(hop);
+    e = GSC_UNI(e);
   } else {  // F_AFTER_HOP
-    const int pa = GSC_UNI(P.a), pc = GSC_UNI(P.c);
-    // the hop just taken and its edge were kept in the record (ret / pad: a forwarder has no
-    // children) when it was scheduled: no dependent path-table / edge-table lookups here
-    const int hop = GSC_UNI(P.ret);
+    const int pc = GSC_UNI(P.c);
     rel_e = GSC_UNI(P.pad);
-    f.node = (int16_t)hop;
-    P.c = (int16_t)(pc + 1);
-    if (GSC_UNI(pc + 1 >= T.plen[pa * n + nxt])) {
+    f.node = (int16_t)GSC_UNI(P.ret);
+    c = pc + 1;
+    if (GSC_UNI(c >= P.len)) {
       add_path_delay(S, P.x);
       f.e2e += P.x;
       f.ttl -= P.x;
@@ -804,19 +842,24 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
       ledger_push(S, S.h->now + f.duration, rel_e, f.dr);
       return;
     }
+    pidx = (long)(GSC_UNI(P.a) * n + nxt) * H + c;
+    hop = GSC_UNI(P.n1);
+    e = GSC_UNI(P.e1);
+    // the hop after this one (c + 1 < H: still inside this path's row)
+    P.n1 = c + 1 < H ? tab<TLDS>(T.pnodes, pidx + 1) : (int16_t)-1;
+    P.e1 = c + 1 < H ? tab<TLDS>(T.pedges, pidx + 1) : (int16_t)-1;
   }
-  // next hop
-  const int pidx = (GSC_UNI(P.a) * n + nxt) * T.H + GSC_UNI(P.c);
-  const int hop = GSC_UNI(T.pnodes[pidx]);
-  const int cur = GSC_UNI(f.node);
-  const int e = GSC_UNI(T.pedges[pidx]);  // == edge_id[cur * n + hop]
-  // hop delay: from the per-hop table (HBM: issued with the hop's node / edge loads, not after them)
-  // or the LDS-staged APSP table
-  const double hd_tab = (BIG && T.phd) ? T.phd[pidx] : 0.0;
+  // this hop's link state and delay, loaded together (the ledger check needs no separate round trip)
+  const double lnext = S.link_next[e];
+  double lrem = S.link_rem[e];
+  const double lpass = S.link_passed[e];
+  const double hd = tab<TLDS>(T.phd, pidx);  // == pdelay[previous path node][hop]
   Flow& fm = S.flows[fid];
   fm.node = f.node;
-  ledger_apply(S, e);
-  const double lrem = S.link_rem[e];
+  if (GSC_UNI(!(S.h->now < lnext))) {  // capacity returns of this link are due first
+    ledger_apply(S, e, lnext);
+    lrem = S.link_rem[e];
+  }
   if (GSC_UNI(lrem - f.dr >= 0)) {
     S.link_rem[e] = lrem - f.dr;
   } else {
@@ -824,10 +867,10 @@ GSC_HD_CALL void run_forward(Env& S, const SimConst& K, const TopoDev& T, int pi
     if (rel_e >= 0) ledger_push(S, S.h->now + f.duration, rel_e, f.dr);
     return;
   }
-  S.link_passed[e] += f.dr;
-  const double hd = (BIG && T.phd) ? hd_tab : T.pdelay[cur * n + hop];
+  S.link_passed[e] = lpass + f.dr;
   if (GSC_UNI(hop == f.egress && f.fwd_eg)) fm.departed = 1;
   P.state = F_AFTER_HOP;
+  P.c = (int16_t)c;
   P.ret = (int16_t)hop;
   P.pad = (int16_t)e;
   S.procs[pid] = P;
@@ -955,21 +998,22 @@ GSC_HD_CALL void run_finish(Env& S, const SimConst& K, int pid, const Proc& P, c
 }
 
 // FlowSimulator.init_arrival + DefaultFlowGenerator.generate_flow.
+template <bool TLDS = false>
 GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pid, const Proc& P) {
   const int node = GSC_UNI(P.a);
   const double mean = S.inter_arr[node];
   if (GSC_UNI(mean != mean)) { proc_return(S, pid, P, 0); return; }  // None: arrivals at this node stop
   Header* h = S.h;
   h->total_flow_count++;
-  const double inter = K.det_arrival ? mean : -log(1.0 - rng_u01(S)) * mean;
+  const double inter = K.det_arrival ? mean : exp_from_u01(rng_u01(S), mean);
   double dr, size;
   for (;;) {
     dr = rng_normal(S, K.dr_mean, K.dr_std);
-    size = K.det_size ? K.size_shape : exp(-log(1.0 - rng_u01(S)) / K.size_shape);  // pareto(a) + 1
+    size = K.det_size ? K.size_shape : pareto_from_u01(rng_u01(S), K.size_shape);  // pareto(a) + 1
     if (GSC_UNI(dr >= 0.0 && size >= 0.0)) break;
   }
   const int sfc = rng_int(S, K.C);
-  const int eg = T.n_eg > 0 ? T.egress[rng_int(S, T.n_eg)] : -1;
+  const int eg = T.n_eg > 0 ? tab<TLDS>(T.egress, rng_int(S, T.n_eg)) : -1;
   const double ttl = K.ttl[rng_int(S, K.n_ttl)];
   const int fid = alloc_flow(S);
   if (fid >= 0) {
@@ -1076,7 +1120,7 @@ GSC_HD_CALL void run_trace(Env& S, const SimConst& K, const TopoDev& T, int pid)
 
 // Resume process pid; `fid` = its flow as carried by the event (-1: none).  The process record and
 // the flow record are loaded together (one LDS round trip instead of two dependent ones).
-template <bool BIG = false>
+template <bool BIG = false, bool TLDS = false>
 GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid, int fid) {
   const Proc P = S.procs[pid];
   Flow f;
@@ -1085,11 +1129,11 @@ GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid, int f
   switch (GSC_UNI(P.type)) {
     case P_HANDLE: run_handle(S, K, T, pid, P, f); break;
     case P_DECIDE: run_decide<BIG>(S, K, T, pid, P, f); break;
-    case P_FORWARD: run_forward<BIG>(S, K, T, pid, P, f); break;
+    case P_FORWARD: run_forward<BIG, TLDS>(S, K, T, pid, P, f); break;
     case P_PROCESS: run_process(S, K, T, pid, P, f); break;
     case P_REQUEST: run_request(S, K, pid, P, f); break;
     case P_FINISH: run_finish(S, K, pid, P, f); break;
-    case P_ARRIVAL: run_arrival(S, K, T, pid, P); break;
+    case P_ARRIVAL: run_arrival<TLDS>(S, K, T, pid, P); break;
     case P_WRITER: run_writer<BIG>(S, K, T, pid, P); break;
     case P_MMPP: run_mmpp(S, K, T, pid); break;
     case P_TRACE: run_trace(S, K, T, pid); break;
@@ -1171,12 +1215,19 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
     const int pid = spawn(S, P_ARRIVAL, A_LOOP, -1, -1);
     if (pid >= 0) S.procs[pid].a = T.ingress[i];
   }
-  // DurationController.get_init_state: env.step()
+  // DurationController.get_init_state: env.step().  The writer was spawned first (URGENT, the smallest
+  // event id at time 0), so that one step is always the writer's W_BEGIN -- run it directly instead of
+  // inlining a second copy of every handler into the kernel (the event loop's dispatch is the only one)
   const int idx = argmin_event_serial(S);
   const Event ev = S.events[idx];
   remove_event(S, idx);
   h->now = ev.t;
-  if (ev.proc >= 0) dispatch<BIG>(S, K, T, ev.proc, ev.flow);
+  if (ev.proc >= 0 && S.procs[ev.proc].type == P_WRITER) {
+    const Proc P = S.procs[ev.proc];
+    run_writer<BIG>(S, K, T, ev.proc, P);
+  } else {
+    h->flags |= FLAG_BAD_STATE;
+  }
 }
 
 // SimulatorWrapper.apply (placement derivation) + DurationController.get_next_state prologue.
@@ -1400,7 +1451,7 @@ GSC_HD_CALL float compute_reward(Env& S, const SimConst& K, const TopoDev& T) {
       fr = nr = ir = 0;
       double util = 1.0;
       if (delay > K.soft_deadline) {
-        util = -log10((1.0 / K.dropoff) * (delay - K.soft_deadline));
+        util = -log10_cold((1.0 / K.dropoff) * (delay - K.soft_deadline));
         util = util < 0 ? 0 : (util > 1 ? 1 : util);
       }
       dr = succ_ratio * util;

@@ -140,12 +140,12 @@ __device__ __forceinline__ int argmin_event_wave(const Env& S, int lane) {
 }
 
 // Bytes of LDS used to stage SimConst + the env's topology tables in front of the state blob.
-// (pedges: the per-hop edge table is staged too; else it is read from L2)
+// (pedges: the per-hop edge and delay tables are staged too; else they are read from L2)
 __host__ __device__ inline long topo_stage_bytes(const Dims& D, int H, bool pedges = true) {
   const long n2 = (long)D.N * D.N;
   return align16(sizeof(TopoDev)) + align16((int)(8 * D.N)) + align16((int)(8 * n2)) + align16((int)(2 * n2)) +
-         (pedges ? 2 : 1) * align16((int)(2 * n2 * H)) + align16((int)(2 * n2)) + align16((int)(8 * D.E)) +
-         2 * align16(2 * D.N);
+         (pedges ? 2 : 1) * align16((int)(2 * n2 * H)) + (pedges ? align16((int)(8 * n2 * H)) : 0) +
+         align16((int)(2 * n2)) + align16((int)(8 * D.E)) + 2 * align16(2 * D.N);
 }
 __host__ __device__ inline long const_stage_bytes() { return align16(sizeof(SimConst)); }
 
@@ -179,8 +179,10 @@ __device__ __forceinline__ TopoDev stage_topo(const TopoDev& g, char* dst, int l
   t.pdelay = (const double*)put(g.pdelay, 8 * n2);
   t.plen = (const int16_t*)put(g.plen, 2 * n2);
   t.pnodes = (const int16_t*)put(g.pnodes, 2 * n2 * g.H);
-  t.phd = nullptr;  // staged: the hop delay is an LDS pdelay lookup
-  if (pedges) t.pedges = (const int16_t*)put(g.pedges, 2 * n2 * g.H);
+  if (pedges) {  // the per-hop edge and delay tables (else both are read from HBM / L2)
+    t.pedges = (const int16_t*)put(g.pedges, 2 * n2 * g.H);
+    t.phd = (const double*)put(g.phd, 8 * n2 * g.H);
+  }
   t.edge_id = (const int16_t*)put(g.edge_id, 2 * n2);
   t.edge_cap = (const double*)put(g.edge_cap, 8 * (g.E > 0 ? g.E : 1));
   t.ingress = (const int16_t*)put(g.ingress, 2 * (g.n_ing > 0 ? g.n_ing : 1));
@@ -286,34 +288,24 @@ __device__ __forceinline__ void rq_merge_inbox(RegQueue<QS>& q, Env& S, int lane
 // Every lane runs the handlers on its own (identical) copy of the header and the same LDS state, so
 // loaded values are wave-uniform and control flow stays scalar; loops over nodes / destinations
 // inside a handler spread over the lanes (sim_core.h wave helpers).
-// Layout source of a step kernel: DynLayout = the runtime layout in the kernel arguments; a dims
-// bucket (struct with a constexpr dims()) = compile-time dims, every state offset / stride a constant.
-// (Measured on MI355X for an Abilene-class bucket: no gain over the runtime layout once the event loop
-// stopped spilling, so no bucket is instantiated; kept as the extension point.  Re-measured after the
-// round-2 simulator changes: bit-identical results, 104.2k vs 104.3k env-steps/s, 115 vs 123 SGPR spills.)
-struct DynLayout {};
-template <class B>
-struct BucketLayout {
-  static constexpr Dims D = B::dims();
-  static constexpr Layout L = make_layout(B::dims());
-};
-
-template <class B, int QS, bool PROF, bool BIG>
+// TLDS: the topology tables are staged in LDS (compile-time): every table pointer derives from the
+// kernel's LDS array, so the handlers' table reads are ds_read (LDS address space) instead of flat
+// loads through generic pointers (a runtime choice between an LDS copy and the HBM tables).
+template <int QS, bool PROF, bool BIG, bool TLDS>
 __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst& K, char* base, char* topo_lds,
                                                 int env, int lane, char* cold = nullptr) {
   const unsigned long long t_entry = PROF ? __builtin_amdgcn_s_memtime() : 0;
-  Env S = [&] {
-    if constexpr (std::is_same<B, DynLayout>::value) return Env(base, a.L, a.D, cold);
-    else return Env(base, BucketLayout<B>::L, BucketLayout<B>::D, cold);
-  }();
+  Env S(base, a.L, a.D, cold);
   // Keep the env header in registers for the whole window (written back once at the end).
   Header* const h_mem = S.h;
   // (measured: header in LDS instead = 2.83 vs 2.30 ms/step for 256 Abilene envs)
   Header h_reg = *h_mem;
   S.h = &h_reg;
   if constexpr (BIG) S.act = a.actions + (long)env * a.action_stride;  // read in place of the schedule table
-  const TopoDev T = a.topo_stage ? stage_topo(a.topos[S.h->topo], topo_lds, lane, a.stage_pedges)
-                                 : a.topos[S.h->topo];
+  const TopoDev T = [&] {
+    if constexpr (TLDS) return stage_topo(a.topos[S.h->topo], topo_lds, lane, a.stage_pedges);
+    else return a.topo_stage ? stage_topo(a.topos[S.h->topo], topo_lds, lane, a.stage_pedges) : a.topos[S.h->topo];
+  }();
   load_action<BIG>(S, K, T, a.actions + (long)env * a.action_stride, lane, 64);
   __syncthreads();
   const unsigned long long t_act = PROF ? __builtin_amdgcn_s_memtime() : 0;
@@ -363,7 +355,7 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
         S.h->cur_key = k;
         const unsigned long long td = prof ? __builtin_amdgcn_s_memtime() : 0;
         const int ptype = prof ? S.procs[p].type * 4 + (S.procs[p].state < 3 ? S.procs[p].state : 3) : 0;
-        dispatch<BIG>(S, K, T, p, pf);
+        dispatch<BIG, TLDS>(S, K, T, p, pf);
         ++n_disp;
         if (prof && lane == 0) {
           a.prof_types[((long)env * 64 + ptype) * 2] += __builtin_amdgcn_s_memtime() - td;
@@ -469,7 +461,8 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
 
 // LDS_STATE: 0 = the state blob stays in HBM, 1 = the whole blob is staged in LDS, 2 = only its hot
 // prefix is (the [N, C, S, N] schedule / WRR tables stay in HBM: 50- and 200-node topologies).
-template <int QSETS, int LDS_STATE, bool PROF = false, class B = DynLayout>
+// TLDS: the topology tables are staged in LDS (SimContext: topo_stage_ > 0), known at compile time.
+template <int QSETS, int LDS_STATE, bool PROF = false, bool TLDS = false>
 __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int env = blockIdx.x;
@@ -480,11 +473,8 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
   if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
   else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
   else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
-  constexpr bool STATIC = !std::is_same<B, DynLayout>::value;
-  // LDS: [state blob or its hot prefix (LDS modes)][SimConst][topology tables] -- the blob at offset
-  // 0, so with a compile-time layout every state address is a constant
-  long sbytes = a.lds_state_bytes;
-  if constexpr (STATIC) sbytes = LDS_STATE == 2 ? BucketLayout<B>::L.hot : BucketLayout<B>::L.total;
+  // LDS: [state blob or its hot prefix (LDS modes)][SimConst][topology tables]
+  const long sbytes = a.lds_state_bytes;
   const long sb = LDS_STATE ? align16((int)sbytes) : 0;
   SimConst* Ks = reinterpret_cast<SimConst*>(smem + sb);
   if (lane == 0) *Ks = a.K;
@@ -499,7 +489,7 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
     copy16(smem, g, sbytes, lane);
     __syncthreads();
     const unsigned long long t1 = PROF ? __builtin_amdgcn_s_memtime() : 0;
-    device_step_env<B, QSETS, PROF, LDS_STATE == 2>(a, *Ks, smem, topo_lds, env, lane, LDS_STATE == 2 ? g : nullptr);
+    device_step_env<QSETS, PROF, LDS_STATE == 2, TLDS>(a, *Ks, smem, topo_lds, env, lane, LDS_STATE == 2 ? g : nullptr);
     const unsigned long long t2 = PROF ? __builtin_amdgcn_s_memtime() : 0;
     copy16(g, smem, sbytes, lane);
     if (PROF && lane == 0) {  // state blob HBM -> LDS / LDS -> HBM
@@ -510,12 +500,16 @@ __global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
     }
   } else {
     __syncthreads();
-    device_step_env<B, QSETS, false, true>(a, *Ks, g, topo_lds, env, lane);
+    device_step_env<QSETS, false, true, TLDS>(a, *Ks, g, topo_lds, env, lane);
   }
   if (PROF && lane == 0) {
     a.prof_types[((long)env * 64 + 58) * 2] += __builtin_amdgcn_s_memtime() - c_begin;
     a.prof_types[((long)env * 64 + 58) * 2 + 1] += 1;
-    a.prof_types[((long)env * 64 + 59) * 2] += __builtin_amdgcn_s_memrealtime() - r_begin;
+    const unsigned long long r_end = __builtin_amdgcn_s_memrealtime();
+    a.prof_types[((long)env * 64 + 59) * 2] += r_end - r_begin;
+    // this step's wave start / end (100 MHz ticks; overwritten every step): dispatch skew vs wave duration
+    a.prof_types[((long)env * 64 + 56) * 2] = r_begin;
+    a.prof_types[((long)env * 64 + 56) * 2 + 1] = r_end;
     a.prof_types[((long)env * 64 + 59) * 2 + 1] += 1;
   }
 }
@@ -589,6 +583,26 @@ static void parallel_for(int n, int threads, F&& fn) {
 // register / ISA analysis build (scripts/sim_resources.py): only the named instantiation
 template __global__ void sim_step_kernel<GSC_SIM_ISA_ONLY>(SimArgs);
 #else
+// The instantiated step kernels: QS = register-queue sets (64 pending events each), LDS mode, cycle-counting
+// variant, topology staged in LDS.  TLDS kernels exist for the whole-state-in-LDS mode (Abilene-class
+// topologies, the headline); larger topologies read unstaged tables through generic pointers.
+template <int QS>
+static const void* step_kernel_q(int mode, bool prof, bool tlds) {
+  if (mode == 1 && tlds) return prof ? (const void*)sim_step_kernel<QS, 1, true, true> : (const void*)sim_step_kernel<QS, 1, false, true>;
+  if (mode == 1) return prof ? (const void*)sim_step_kernel<QS, 1, true, false> : (const void*)sim_step_kernel<QS, 1, false, false>;
+  if (mode == 2) return prof ? (const void*)sim_step_kernel<QS, 2, true, false> : (const void*)sim_step_kernel<QS, 2, false, false>;
+  if (mode == 0) return (const void*)sim_step_kernel<QS, 0, false, false>;  // (no cycle-counting variant)
+  return nullptr;
+}
+static const void* step_kernel(int qs, int mode, bool prof, bool tlds) {
+  switch (qs) {
+    case 1: return step_kernel_q<1>(mode, prof, tlds);
+    case 2: return step_kernel_q<2>(mode, prof, tlds);
+    case 4: return step_kernel_q<4>(mode, prof, tlds);
+    default: return step_kernel_q<8>(mode, prof, tlds);
+  }
+}
+
 class SimContext {
  public:
   SimContext(py::dict dims, py::dict cfg, py::list topos, bool device, int host_threads)
@@ -652,32 +666,27 @@ class SimContext {
       lds_mode_ = fits(total) ? 1 : (fits(hot) ? 2 : 0);
       const long state = lds_mode_ == 1 ? total : (lds_mode_ == 2 ? hot : 0);
       const long fixed = const_stage_bytes() + topo_stage_;
-      // the per-hop edge table saves one dependent lookup per hop, but not at the price of a
-      // workgroup per CU (50-node topologies with the state blob in HBM: 112 vs 72 KB of tables)
+      // the per-hop edge / delay tables save dependent lookups per hop, but not at the price of a workgroup
+      // per CU below one wave per SIMD (50-node topologies with the state blob in HBM: 112 vs 72 KB of
+      // tables).  Four env workgroups per CU (one per SIMD: the waves are issue-bound) are enough.
       if (topo_stage_) {
         const long without = topo_stage_bytes(D_, maxH, false);
         const long cu_lds = 160 * 1024;
-        if (cu_lds / (const_stage_bytes() + topo_stage_ + state) < cu_lds / (const_stage_bytes() + without + state)) {
+        const long with_n = cu_lds / (const_stage_bytes() + topo_stage_ + state);
+        if (with_n < 4 && with_n < cu_lds / (const_stage_bytes() + without + state)) {
           topo_stage_ = without;
           stage_pedges_ = 0;
         }
       }
       const long need = fixed + state;
       qsets_ = D_.event_cap <= 64 ? 1 : (D_.event_cap <= 128 ? 2 : (D_.event_cap <= 256 ? 4 : 8));
-      if (need > 65536) {
-        const void* fns[] = {
-            (const void*)sim_step_kernel<1, 1>, (const void*)sim_step_kernel<2, 1>,
-            (const void*)sim_step_kernel<4, 1>, (const void*)sim_step_kernel<8, 1>,
-            (const void*)sim_step_kernel<1, 2>, (const void*)sim_step_kernel<2, 2>,
-            (const void*)sim_step_kernel<4, 2>, (const void*)sim_step_kernel<8, 2>,
-            (const void*)sim_step_kernel<1, 0>, (const void*)sim_step_kernel<2, 0>,
-            (const void*)sim_step_kernel<4, 0>, (const void*)sim_step_kernel<8, 0>,
-            (const void*)sim_step_kernel<1, 1, true>, (const void*)sim_step_kernel<2, 1, true>,
-            (const void*)sim_step_kernel<4, 1, true>, (const void*)sim_step_kernel<8, 1, true>,
-            (const void*)sim_step_kernel<1, 2, true>, (const void*)sim_step_kernel<2, 2, true>,
-            (const void*)sim_step_kernel<4, 2, true>, (const void*)sim_step_kernel<8, 2, true>};
-        for (auto f : fns) GSC_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
-      }
+      if (need > 65536)
+        for (int q : {1, 2, 4, 8})
+          for (int m : {0, 1, 2})
+            for (int pr : {0, 1})
+              for (int tl : {0, 1})
+                if (const void* f = step_kernel(q, m, pr, tl))
+                  GSC_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need));
     }
   }
   ~SimContext() {
@@ -723,19 +732,11 @@ class SimContext {
         hipLaunchKernelGGL(sim_pmask_kernel, dim3(E, (pmask_rows(D_) + 3) / 4), dim3(256), 0, st, a);
         check_launch();
       }
-#define GSC_LAUNCH_SIM(QS)                                                                                     \
-  if (lds_mode_ == 1 && a.prof) hipLaunchKernelGGL((sim_step_kernel<QS, 1, true>), dim3(E), dim3(64), lds, st, a); \
-  else if (lds_mode_ == 1) hipLaunchKernelGGL((sim_step_kernel<QS, 1>), dim3(E), dim3(64), lds, st, a);           \
-  else if (lds_mode_ == 2 && a.prof) hipLaunchKernelGGL((sim_step_kernel<QS, 2, true>), dim3(E), dim3(64), lds, st, a); \
-  else if (lds_mode_ == 2) hipLaunchKernelGGL((sim_step_kernel<QS, 2>), dim3(E), dim3(64), lds, st, a);           \
-  else hipLaunchKernelGGL((sim_step_kernel<QS, 0>), dim3(E), dim3(64), lds, st, a);
-      switch (qsets_) {
-        case 1: GSC_LAUNCH_SIM(1) break;
-        case 2: GSC_LAUNCH_SIM(2) break;
-        case 4: GSC_LAUNCH_SIM(4) break;
-        default: GSC_LAUNCH_SIM(8) break;
-      }
-#undef GSC_LAUNCH_SIM
+      // GSC_SIM_TLDS=0: the generic-pointer kernel even when the topology is staged (A/B diagnostics)
+      static const bool tlds_ok = !(getenv("GSC_SIM_TLDS") && getenv("GSC_SIM_TLDS")[0] == '0');
+      const void* f = step_kernel(qsets_, lds_mode_, a.prof != nullptr, tlds_ok && lds_mode_ == 1 && topo_stage_ > 0 && stage_pedges_);
+      GSC_CHECK(f, "no simulator kernel instantiated for this (queue sets, LDS mode, profiling) combination");
+      hipLaunchKernelGGL(reinterpret_cast<void (*)(SimArgs)>(const_cast<void*>(f)), dim3(E), dim3(64), lds, st, a);
       check_launch();
     } else {
       parallel_for(E, host_threads_, [&](int e) { host_step_env(a, e); });

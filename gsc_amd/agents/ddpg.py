@@ -543,10 +543,13 @@ class BatchedTrainer:
 
     @staticmethod
     def auto_sim_cus(sim) -> int:
-        """CUs for one round of the simulator's env workgroups, at most 4 envs (waves) per CU so every
-        simulator wave keeps a SIMD to itself, rounded up to whole XCDs (MI355X: 8 XCDs x 32 CUs, each
-        with its own L2; contiguous CU-mask bits fill one XCD after the other), capped at half the device.
-        Measured on MI355X, 256 Abilene envs, 39.9 KB of LDS per env (env-steps/s, round 3): 64 CUs (two
+        """CUs for one round of the simulator's env workgroups, at most 3 envs (waves) per CU, rounded up
+        to whole XCDs (MI355X: 8 XCDs x 32 CUs, each with its own L2; contiguous CU-mask bits fill one XCD
+        after the other), capped at half the device.  The simulator waves are issue- and fetch-latency
+        bound: four per CU (one per SIMD) share the CU's instruction fetch, and per-wave speed drops
+        (round 5, 256 Abilene envs standalone: 2.29 ms/step on 64 CUs = 4 per CU, 2.06 on 96, 1.99 on 128;
+        bench 108.5k at 64, 113.7k at 96).
+        Earlier, on MI355X, 256 Abilene envs, 39.9 KB of LDS per env (env-steps/s, round 3): 64 CUs (two
         XCDs, 4 envs per CU) 113.3k; 96 CUs 111.0k; 128 CUs 96.4k (the learner becomes the longer
         chain); 72 / 80 / 88 / 112 CUs 71-84k (an XCD shared between simulator and learner); 32 CUs
         57.8k (two rounds).  Round 2, when an env took more LDS than 40 KB, 3 envs per CU (96 CUs) was
@@ -555,7 +558,7 @@ class BatchedTrainer:
         n = nat.cu_count()
         xcd = max(n // 8, 8)
         lds = max(int(sim.ctx.lds_per_env), 1)
-        per_cu = max(1, min(4, (160 * 1024) // lds))
+        per_cu = max(1, min(3, (160 * 1024) // lds))
         need = -(-sim.E // per_cu)
         # Mid-size topologies (33..64 nodes: two envs per CU by LDS, the learner's two-tile GATv2 kernels
         # need 52-81 KB of LDS and cannot share those CUs) are learner-bound: half a round's CUs, so the

@@ -73,14 +73,23 @@ if args.profile:
              "finish", "retlink"]
     phases = {60: "copy-in (state HBM->LDS)", 61: "copy-out (LDS->HBM)", 62: "prologue",
               57: "  of which topology stage + action load", 63: "epilogue"}
-    tot = ty[:57, 0].sum()
-    for i in range(57):
+    tot = ty[:56, 0].sum()
+    for i in range(56):
         if ty[i, 1] > 0:
             print(f"  {names[i // 4]:8s} state {i % 4} events/env-step={ty[i, 1] / (args.envs * args.steps):7.1f} "
                   f"cycles/dispatch={ty[i, 0] / ty[i, 1]:7.0f} share={ty[i, 0] / tot:.3f}")
     for i, nm in phases.items():
         if ty[i, 1] > 0:
             print(f"  {nm:26s} cycles/env-step={ty[i, 0] / ty[i, 1]:9.0f}")
+    per = pr[args.envs * 4:].view(args.envs, 64, 2)
+    t0s, t1s = per[:, 56, 0], per[:, 56, 1]
+    if float(t1s.max()) > 0:  # the last step's wave start skew and durations (100 MHz ticks -> us)
+        b = (t0s - t0s.min()) / 100.0
+        d = (t1s - t0s) / 100.0
+        q = torch.tensor([0.0, 0.5, 0.9, 1.0], dtype=torch.float64)
+        print(f"  last step: wave start offset us (min/med/p90/max) {[round(float(x), 1) for x in b.quantile(q)]}  "
+              f"wave duration us {[round(float(x), 1) for x in d.quantile(q)]}  "
+              f"kernel span us {float((t1s.max() - t0s.min()) / 100.0):.1f}")
     if ty[59, 0] > 0:  # whole-workgroup shader cycles / 100 MHz wall ticks
         print(f"  effective engine clock  {ty[58, 0] / ty[59, 0] * 100:.0f} MHz")
     print(f"cycles/event: select={p[0] / p[3]:.0f} dispatch={p[1] / p[3]:.0f} merge={p[2] / p[3]:.0f} "
