@@ -78,6 +78,7 @@ struct alignas(16) Flow {  // 64 B: four 16-byte LDS accesses per copy
   int32_t pad0, pad1;
 };
 
+// Control state the event loop reads (device: held in registers for the whole window).
 struct Header {
   double now;
   uint32_t eid;
@@ -86,16 +87,24 @@ struct Header {
   uint32_t key0, key1;
   uint64_t ctr;
   int32_t total_flow_count, trace_index, flags, n;
-  int32_t gen, processed, dropped, active;
-  int32_t run_gen, run_processed, run_dropped, num_path_delays;
-  int32_t drop_reason[4];
-  int32_t num_proc_delays, max_events, max_procs, max_flows;
-  double total_e2e, total_path_delay, total_proc_delay;
-  double run_e2e, run_max_e2e, run_total_path_delay, run_avg_path_delay;
-  double ewma_flows, episode_return;
+  int32_t max_events, max_procs, max_flows;
   int32_t proc_head;         // proc_free[proc_top - 1] (the next pid to allocate), cached off the LDS stack
   uint32_t cur_key;          // key of the event being dispatched (orders the release ledger against it)
   int32_t n_rel, max_rel;    // pending link releases, high-water mark
+};
+
+// Metric accumulators (reference coordsim/metrics/metrics.py): written by the handlers, read only by the
+// epilogue (reward, stats).  Device: stay in LDS and are updated by one lane's LDS atomics (no read-back on
+// the event loop's dependent chain, no registers held for them across the loop).
+struct Stats {
+  int32_t gen, processed, dropped, active;
+  int32_t run_gen, run_processed, run_dropped, num_path_delays;
+  int32_t drop_reason[4];
+  int32_t num_proc_delays, pad0;
+  double total_e2e, total_path_delay, total_proc_delay;
+  double run_e2e, run_total_path_delay, run_avg_path_delay;
+  uint64_t run_max_e2e;      // bits of a non-negative double (integer max == float max)
+  double ewma_flows, episode_return;
 };
 
 // Read-only per-topology tables (device or host memory).
@@ -154,7 +163,7 @@ struct Dims {
 // Topologies whose whole blob exceeds LDS (50 / 200 nodes: the tables alone are 270 KB / 4.3 MB)
 // stage only the hot prefix [0, hot) in LDS and keep the cold tables in HBM (served from L2).
 struct Layout {
-  int hdr, node_cap, node_rem, inter_arr, max_usage, run_drop_node, mmpp_state, sf_load, sf_start, proc_traffic,
+  int hdr, stats, node_cap, node_rem, inter_arr, max_usage, run_drop_node, mmpp_state, sf_load, sf_start, proc_traffic,
       requested, drop_locs, link_rem, link_passed, link_next, rel, flows, procs, events, flow_free, proc_free,
       sf_present, placement, hot, sched, wrr, pmask, total;
 };
@@ -177,6 +186,7 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
   int o = 0;
 #define GSC_TAKE(field, bytes) L.field = o; o += align16((int)(bytes));
   GSC_TAKE(hdr, sizeof(Header));
+  GSC_TAKE(stats, sizeof(Stats));
   GSC_TAKE(node_cap, 8 * d.N);
   GSC_TAKE(node_rem, 8 * d.N);
   GSC_TAKE(inter_arr, 8 * d.N);
@@ -215,6 +225,7 @@ __host__ __device__ constexpr Layout make_layout(const Dims& d) {
 // blob unless the hot prefix was staged into LDS on its own).
 struct Env {
   Header* h;
+  Stats* st;
   double *node_cap, *node_rem, *inter_arr, *max_usage, *sf_load, *sf_start, *proc_traffic, *requested, *sched,
       *link_rem, *link_passed, *link_next;
   int32_t *run_drop_node, *mmpp_state, *drop_locs, *wrr;
@@ -233,6 +244,7 @@ struct Env {
   GSC_HD Env(char* base, const Layout& L, const Dims& dims, char* cold = nullptr) : d(dims) {
     char* const cb = cold ? cold : base;
     h = (Header*)(base + L.hdr);
+    st = (Stats*)(base + L.stats);
     node_cap = (double*)(base + L.node_cap);
     node_rem = (double*)(base + L.node_rem);
     inter_arr = (double*)(base + L.inter_arr);
@@ -572,9 +584,10 @@ GSC_HD void lanes_sync(int ls) {
 // (200 nodes: 1.4 MB of counters per env and window otherwise, written by one wave)
 template <bool BIG = false>
 GSC_HD_CALL void reset_run_metrics(Env& S, const SimConst& K, int n, int l0, int ls) {
-  Header* h = S.h;
-  h->run_gen = h->run_processed = h->run_dropped = 0;
-  h->run_e2e = h->run_max_e2e = h->run_total_path_delay = h->run_avg_path_delay = 0.0;
+  Stats* st = S.st;
+  st->run_gen = st->run_processed = st->run_dropped = 0;
+  st->run_e2e = st->run_total_path_delay = st->run_avg_path_delay = 0.0;
+  st->run_max_e2e = 0;
   const int N = S.d.N, Sd = S.d.S, C = S.d.C;
   for (int v = l0; v < N; v += ls) { S.run_drop_node[v] = 0; S.max_usage[v] = 0.0; }
   for (int i = l0; i < N * Sd; i += ls) S.proc_traffic[i] = 0.0;
@@ -590,36 +603,64 @@ GSC_HD_CALL void reset_run_metrics(Env& S, const SimConst& K, int n, int l0, int
   (void)K; (void)n;
 }
 
+// Device: one lane updates the accumulators with LDS atomics (every lane runs the handler; the others
+// skip), in program order -- the same sums, in the same order, as the host's plain updates.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GSC_ST_LANE0 if (wave_lane() == 0)
+template <class T, class V>
+__device__ __forceinline__ void st_add(T* p, V v) {
+  __hip_atomic_fetch_add(p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void st_max(uint64_t* p, uint64_t v) {
+  __hip_atomic_fetch_max((unsigned long long*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+#else
+#define GSC_ST_LANE0
+template <class T, class V>
+inline void st_add(T* p, V v) { *p += (T)v; }
+inline void st_max(uint64_t* p, uint64_t v) { if (v > *p) *p = v; }
+#endif
+GSC_HD uint64_t dbits(double x) {
+  uint64_t u;
+  __builtin_memcpy(&u, &x, 8);
+  return u;
+}
+
 GSC_HD_CALL void dropped_flow(Env& S, const Flow& f, int reason) {
-  Header* h = S.h;
-  h->dropped++; h->active--; h->run_dropped++;
-  const int sf = f.cur_sf < 0 ? S.d.S : f.cur_sf;
-  S.drop_locs[f.node * (S.d.S + 1) + sf]++;
-  S.run_drop_node[f.node]++;
-  if (f.ttl <= 0) reason = R_TTL;
-  // constant-index updates keep the header promotable to registers
-  switch (reason) {
-    case R_TTL: h->drop_reason[0]++; break;
-    case R_DECISION: h->drop_reason[1]++; break;
-    case R_LINK: h->drop_reason[2]++; break;
-    default: h->drop_reason[3]++; break;
+  const int sf = GSC_UNI(f.cur_sf < 0 ? S.d.S : f.cur_sf), node = GSC_UNI(f.node);
+  if (GSC_UNI(f.ttl <= 0)) reason = R_TTL;
+  Stats* st = S.st;
+  GSC_ST_LANE0 {
+    st_add(&st->dropped, 1);
+    st_add(&st->active, -1);
+    st_add(&st->run_dropped, 1);
+    st_add(&S.drop_locs[node * (S.d.S + 1) + sf], 1);
+    st_add(&S.run_drop_node[node], 1);
+    st_add(&st->drop_reason[reason], 1);
   }
 }
 
 GSC_HD_CALL void completed_flow(Env& S, const Flow& f) {
-  Header* h = S.h;
-  h->processed++; h->run_processed++; h->active--;
-  h->total_e2e += f.e2e;
-  h->run_e2e += f.e2e;
-  if (f.e2e > h->run_max_e2e) h->run_max_e2e = f.e2e;
+  Stats* st = S.st;
+  GSC_ST_LANE0 {
+    st_add(&st->processed, 1);
+    st_add(&st->run_processed, 1);
+    st_add(&st->active, -1);
+    st_add(&st->total_e2e, f.e2e);
+    st_add(&st->run_e2e, f.e2e);
+    st_max(&st->run_max_e2e, dbits(f.e2e));  // e2e >= 0
+  }
 }
 
+// (run_avg_path_delay = run_total_path_delay / run_gen is derived in the epilogue: nothing reads it
+// inside the window)
 GSC_HD void add_path_delay(Env& S, double d) {
-  Header* h = S.h;
-  h->num_path_delays++;
-  h->total_path_delay += d;
-  h->run_total_path_delay += d;
-  if (h->run_gen > 0) h->run_avg_path_delay = h->run_total_path_delay / h->run_gen;
+  Stats* st = S.st;
+  GSC_ST_LANE0 {
+    st_add(&st->num_path_delays, 1);
+    st_add(&st->total_path_delay, d);
+    st_add(&st->run_total_path_delay, d);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -893,8 +934,11 @@ GSC_HD_CALL void run_process(Env& S, const SimConst& K, const TopoDev& T, int pi
     if (!GSC_UNI(S.placement[node * Sd + sf])) { proc_return(S, pid, P, 0); return; }
     const double pd = fabs(rng_normal(S, K.pd_mean[sf], K.pd_std[sf]));
     if (GSC_UNI(f.ttl - pd <= 0)) { fm.ttl = 0; proc_return(S, pid, P, 0); return; }
-    S.h->num_proc_delays++;
-    S.h->total_proc_delay += pd;
+    Stats* st = S.st;
+    GSC_ST_LANE0 {
+      st_add(&st->num_proc_delays, 1);
+      st_add(&st->total_proc_delay, pd);
+    }
     fm.e2e = f.e2e + pd;
     fm.ttl = f.ttl - pd;
     if (GSC_UNI(pd == 0.0)) { proc_return(S, pid, P, 0); return; }  // reference: `if not processing_delay`
@@ -1034,7 +1078,12 @@ GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pi
     f.pad0 = 0;
     f.pad1 = 0;
     S.flows[fid] = f;
-    h->gen++; h->run_gen++; h->active++;
+    Stats* st = S.st;
+    GSC_ST_LANE0 {
+      st_add(&st->gen, 1);
+      st_add(&st->run_gen, 1);
+      st_add(&st->active, 1);
+    }
     if (spawn(S, P_HANDLE, H_LOOP, fid, -1) < 0) free_flow(S, fid);
   } else {
     h->eid++;  // keep event ids aligned with the oracle even on overflow
@@ -1167,10 +1216,16 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
                           int l0 = 0, int ls = 1) {
   Header* h = S.h;
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
-  const double ewma = h->ewma_flows;
+  const double ewma = S.st->ewma_flows, ep_ret = S.st->episode_return;
+  lanes_sync(ls);  // every lane has read the values kept across the reset
   *h = Header{};
+  if (l0 == 0) {
+    *S.st = Stats{};
+    S.st->ewma_flows = episode <= 1 ? 1.0 : ewma;
+    S.st->episode_return = ep_ret;
+  }
+  lanes_sync(ls);
   h->topo = topo;
-  h->ewma_flows = episode <= 1 ? 1.0 : ewma;
   h->episode = episode;
   h->n = n;
   h->run_times = 1;
@@ -1402,8 +1457,15 @@ GSC_HD_CALL void write_obs(const Env& S, const SimConst& K, const TopoDev& T, fl
   }
 }
 
+// End of a run window: the window's mean path delay (the reference updates it at every path; nothing
+// reads it inside the window, so it is derived once here from the window's totals)
+GSC_HD void finish_run_stats(Env& S) {
+  Stats* st = S.st;
+  st->run_avg_path_delay = st->run_gen > 0 ? st->run_total_path_delay / st->run_gen : 0.0;
+}
+
 GSC_HD_CALL float compute_reward(Env& S, const SimConst& K, const TopoDev& T) {
-  Header* h = S.h;
+  Stats* h = S.st;
   const int succ = h->run_processed, drop = h->run_dropped, Sd = K.S, n = T.n;  // real SF count (dims may be padded)
   double succ_ratio = 0.0, fr = 0.0;
   if (succ + drop > 0) {
@@ -1464,7 +1526,8 @@ GSC_HD_CALL float compute_reward(Env& S, const SimConst& K, const TopoDev& T) {
 }
 
 GSC_HD void write_stats(const Env& S, float* st) {
-  const Header* h = S.h;
+  const Stats* h = S.st;
+  const Header* hc = S.h;
   st[0] = (float)h->run_processed;
   st[1] = (float)h->run_dropped;
   st[2] = (float)h->run_gen;
@@ -1477,10 +1540,10 @@ GSC_HD void write_stats(const Env& S, float* st) {
   st[9] = (float)h->drop_reason[1];
   st[10] = (float)h->drop_reason[2];
   st[11] = (float)h->drop_reason[3];
-  st[12] = (float)h->flags;
-  st[13] = (float)h->max_events;
-  st[14] = (float)h->max_procs;
-  st[15] = (float)h->max_flows;
+  st[12] = (float)hc->flags;
+  st[13] = (float)hc->max_events;
+  st[14] = (float)hc->max_procs;
+  st[15] = (float)hc->max_flows;
 }
 
 // Copy this step's (post-processed) action block into the schedule table.

@@ -57,15 +57,16 @@ GSC_HD void step_epilogue(Env& S, const SimArgs& a, const SimConst& K, int env) 
   const TopoDev& T = a.topos[S.h->topo];
   const long ostride = (long)K.n_pad * K.n_obs;
   S.h->run_times++;
+  finish_run_stats(S);
   const float r = compute_reward(S, K, T);
   write_stats(S, a.stats + (long)env * kNumStats);
   write_obs(S, K, T, a.next_obs + env * ostride);
   a.reward[env] = r;
-  S.h->episode_return += r;
+  S.st->episode_return += r;
   S.h->run_count++;
   if (S.h->run_count >= K.episode_steps) {
     a.done[env] = 1;
-    a.ep_return[env] = (float)S.h->episode_return;
+    a.ep_return[env] = (float)S.st->episode_return;
     const int topo = a.topo_next[env];
     if (a.topo_cur) a.topo_cur[env] = topo;
     const int ep = S.h->episode + 1;
@@ -79,8 +80,8 @@ GSC_HD void step_epilogue(Env& S, const SimArgs& a, const SimConst& K, int env) 
 
 GSC_HD void reset_one(Env& S, const SimArgs& a, int env) {
   const int topo = a.topo_next[env];
-  S.h->episode_return = 0.0;
-  S.h->ewma_flows = 1.0;
+  S.st->episode_return = 0.0;
+  S.st->ewma_flows = 1.0;
   env_init(S, a.K, a.topos[topo], topo, a.seeds[env], 1);
   write_obs(S, a.K, a.topos[topo], a.obs + (long)env * a.K.n_pad * a.K.n_obs);
 }
@@ -430,14 +431,15 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
   int done = 0;
   if (lane == 0) {
     S.h->run_times++;
+    finish_run_stats(S);
     const float r = compute_reward(S, K, T);
     write_stats(S, a.stats + (long)env * kNumStats);
     a.reward[env] = r;
-    S.h->episode_return += r;
+    S.st->episode_return += r;
     S.h->run_count++;
     done = S.h->run_count >= K.episode_steps;
     a.done[env] = (uint8_t)done;
-    if (done) a.ep_return[env] = (float)S.h->episode_return;
+    if (done) a.ep_return[env] = (float)S.st->episode_return;
   }
   done = __builtin_amdgcn_readfirstlane(done);
   write_obs_wave(S, K, T.n, a.next_obs + env * ostride, done ? nullptr : a.obs + env * ostride, lane);

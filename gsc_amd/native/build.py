@@ -44,6 +44,9 @@ def _flags(src: str):
     f = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result", "-Wno-unused-command-line-argument"]
     if os.sep + "sim" + os.sep in src:
         f.append("-ffp-contract=off")  # bit-exact float semantics vs the Python oracle
+        # the simulator's metric atomics are issued by one lane on purpose (every lane runs the handler):
+        # no wave-level reduction rewrite of uniform-address atomics
+        f += ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
     return f
 
 
