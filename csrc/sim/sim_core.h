@@ -70,12 +70,11 @@ struct alignas(8) Release {  // 24 B
   int32_t edge;
 };
 
-struct alignas(16) Flow {  // 64 B: four 16-byte LDS accesses per copy
+struct alignas(16) Flow {  // 64 B = 16 dwords (one per lane in load_proc_flow)
   double dr, duration, e2e, ttl, creation;
   int32_t id;
   int16_t node, egress, sfc, pos, cur_sf, ingress;
   uint8_t departed, fwd_eg, dropped, proc_idx;
-  int32_t pad0, pad1;
 };
 
 // Control state the event loop reads (device: held in registers for the whole window).
@@ -1075,8 +1074,6 @@ GSC_HD_CALL void run_arrival(Env& S, const SimConst& K, const TopoDev& T, int pi
     f.pos = 0;
     f.cur_sf = -1;
     f.departed = f.fwd_eg = f.dropped = f.proc_idx = 0;
-    f.pad0 = 0;
-    f.pad1 = 0;
     S.flows[fid] = f;
     Stats* st = S.st;
     GSC_ST_LANE0 {
@@ -1169,11 +1166,36 @@ GSC_HD_CALL void run_trace(Env& S, const SimConst& K, const TopoDev& T, int pid)
 
 // Resume process pid; `fid` = its flow as carried by the event (-1: none).  The process record and
 // the flow record are loaded together (one LDS round trip instead of two dependent ones).
+#if defined(__HIP_DEVICE_COMPILE__)
+// The process record (8 dwords) and the flow record (16 dwords) read with ONE ds_read_b32: lane k < 8
+// holds dword k of the process record, lane 8 + j dword j of the flow record; each field is then taken
+// from its lane with v_readlane (an SGPR: wave-uniform by construction).  A broadcast ds_read_b128 of
+// the same 96 bytes into every lane moves 6 KB through the CU's LDS pipe (64 copies), which the up to
+// four simulator waves of a CU queue on.
+__device__ __forceinline__ void load_proc_flow(const Env& S, int pid, int fid, Proc& P, Flow& f) {
+  static_assert(sizeof(Proc) == 32 && sizeof(Flow) == 64, "record layouts");
+  const int lane = wave_lane();
+  const uint32_t* pp = reinterpret_cast<const uint32_t*>(S.procs + pid);
+  const uint32_t* fp = reinterpret_cast<const uint32_t*>(S.flows + (fid >= 0 ? fid : 0));
+  const uint32_t v = lane < 8 ? pp[lane] : fp[(lane - 8) & 15];
+  uint32_t w[24];
+#pragma unroll
+  for (int k = 0; k < 24; ++k) w[k] = (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+  __builtin_memcpy(&P, w, 32);
+  __builtin_memcpy(&f, w + 8, 64);
+}
+#endif
+
 template <bool BIG = false, bool TLDS = false>
 GSC_HD void dispatch(Env& S, const SimConst& K, const TopoDev& T, int pid, int fid) {
-  const Proc P = S.procs[pid];
+  Proc P;
   Flow f;
+#if defined(__HIP_DEVICE_COMPILE__)
+  load_proc_flow(S, pid, fid, P, f);
+#else
+  P = S.procs[pid];
   if (fid >= 0) f = S.flows[fid];
+#endif
   if (GSC_UNI(P.flow) != fid) S.h->flags |= FLAG_BAD_STATE;  // event / process flow mismatch
   switch (GSC_UNI(P.type)) {
     case P_HANDLE: run_handle(S, K, T, pid, P, f); break;

@@ -736,7 +736,8 @@ class SimContext {
       }
       // GSC_SIM_TLDS=0: the generic-pointer kernel even when the topology is staged (A/B diagnostics)
       static const bool tlds_ok = !(getenv("GSC_SIM_TLDS") && getenv("GSC_SIM_TLDS")[0] == '0');
-      const void* f = step_kernel(qsets_, lds_mode_, a.prof != nullptr, tlds_ok && lds_mode_ == 1 && topo_stage_ > 0 && stage_pedges_);
+      const bool tlds = tlds_ok && lds_mode_ == 1 && topo_stage_ > 0 && stage_pedges_;
+      const void* f = step_kernel(qsets_, lds_mode_, a.prof != nullptr, tlds);
       GSC_CHECK(f, "no simulator kernel instantiated for this (queue sets, LDS mode, profiling) combination");
       hipLaunchKernelGGL(reinterpret_cast<void (*)(SimArgs)>(const_cast<void*>(f)), dim3(E), dim3(64), lds, st, a);
       check_launch();

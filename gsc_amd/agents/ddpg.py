@@ -511,7 +511,9 @@ class BatchedTrainer:
                 n = nat.cu_count()
                 k = max(8, min(int(sim_cus), n - 8))
                 self.sim_cus = k
-                self.sim_stream = torch.cuda.ExternalStream(nat.create_cu_masked_stream(list(range(k))),
+                sim_list = self.sim_cu_list(n, k)
+                rest = [c for c in range(n) if c not in set(sim_list)]
+                self.sim_stream = torch.cuda.ExternalStream(nat.create_cu_masked_stream(sim_list),
                                                             device=self.device)
                 # The learner stream is restricted to the complement, so no learner wave shares a SIMD
                 # with a simulator wave -- when the simulator is the critical path (small topologies whose
@@ -525,7 +527,7 @@ class BatchedTrainer:
                     self.learn_stream = torch.cuda.Stream(self.device)
                 else:
                     self.learn_stream = torch.cuda.ExternalStream(
-                        nat.create_cu_masked_stream(list(range(k, n))), device=self.device)
+                        nat.create_cu_masked_stream(rest), device=self.device)
                 # The act path (actor forward + exploration of step t+1) sits between two simulator
                 # steps, when the learner's CUs are idle too (update t done, update t+1 waits for it):
                 # an unmasked stream gives it every CU.  Auto: on when the learner is the longer chain
@@ -540,6 +542,19 @@ class BatchedTrainer:
                 nat.gnn_set_cu_budget(budget)
             else:
                 self.sim_stream = torch.cuda.Stream(self.device)
+
+    @staticmethod
+    def sim_cu_list(n: int, k: int) -> List[int]:
+        """The simulator's CU-mask bits.  ``GSC_SIM_CU_LAYOUT=xcd`` (default): k / 8 bits of every 32-bit block
+        (the same CU count in each of MI355X's 8 XCDs); ``contig``: bits 0 .. k-1.  Measured round 5, 256
+        Abilene envs (4 per CU) standalone: 64 contiguous bits 2.21 ms/step, 64 spread 8 per block 1.98 ms
+        (= 96 contiguous bits: 1.95) -- with the contiguous mask the simulator's waves contend for issue
+        (SQ_WAIT_INST_ANY 2.85e7 vs 8.0e4 per dispatch at one wave per CU)."""
+        layout = os.environ.get("GSC_SIM_CU_LAYOUT", "xcd")
+        if layout == "xcd" and n % 32 == 0 and k % (n // 32) == 0:
+            per = k // (n // 32)
+            return [c for c in range(n) if c % 32 < per]
+        return list(range(k))
 
     @staticmethod
     def auto_sim_cus(sim) -> int:

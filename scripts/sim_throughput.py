@@ -23,6 +23,8 @@ ap.add_argument("--net", default="configs/networks/abilene/abilene-in4-rand-cap1
 ap.add_argument("--profile", action="store_true")
 ap.add_argument("--simcfg", default="configs/config/simulator/sample_config.yaml")
 ap.add_argument("--cus", type=int, default=0, help="run on a stream CU-masked to this many CUs (0: all)")
+ap.add_argument("--cu-per-xcd", type=int, default=0,
+                help="with --cus: take the CUs as this many per 32-CU XCD block instead of contiguous bits")
 ap.add_argument("--preset", default=None, help="bench.py preset (network / service / simulator / agent config)")
 ap.add_argument("--episode-steps", type=int, default=None, help="override the agent config's episode length "
                 "(default: the preset's, else the config's)")
@@ -45,7 +47,10 @@ a[:n, :, :, :n] = rng.random((n, sim.C, sim.F, n))
 a = threshold_normalize(a.reshape(-1), P, 0.1, 2).astype(np.float32)
 A = torch.from_numpy(np.tile(a, (args.envs, 1))).to(args.device)
 if args.cus:
-    stream = torch.cuda.ExternalStream(sim.native.create_cu_masked_stream(list(range(args.cus))))
+    cus = list(range(args.cus))
+    if args.cu_per_xcd:
+        cus = [c for c in range(sim.native.cu_count()) if c % 32 < args.cu_per_xcd][: args.cus]
+    stream = torch.cuda.ExternalStream(sim.native.create_cu_masked_stream(cus))
     torch.cuda.set_stream(stream)
 sim.reset()
 for _ in range(5):
@@ -62,7 +67,7 @@ if args.device == "cuda":
     torch.cuda.synchronize()
 dt = time.perf_counter() - t
 sim.check_flags()
-print(f"cus={args.cus or 'all'} envs={args.envs} steps={args.steps} state_bytes={sim.state_bytes} "
+print(f"cus={args.cus or 'all'}{'/xcd' + str(args.cu_per_xcd) if args.cu_per_xcd else ''} envs={args.envs} steps={args.steps} state_bytes={sim.state_bytes} "
       f"lds_mode={sim.ctx.lds_mode} lds_per_env={sim.ctx.lds_per_env} "
       f"env_steps_per_s={args.envs * args.steps / dt:.1f} ms_per_step={dt / args.steps * 1e3:.3f}")
 if args.profile:
