@@ -153,8 +153,11 @@ def main():
     m = trainer.metrics(reset=True)
     if diag:
         ty = sim.prof[sim.E * 4:].view(sim.E, 64, 2).sum(0).double().cpu()
+        ph = {k: ty[i, 0] / max(float(ty[i, 1]), 1) for k, i in (("copy_in", 60), ("copy_out", 61), ("prologue", 62),
+                                                                  ("epilogue", 63))}
         print(f"diag: sim cycles/env-step={ty[58, 0] / max(float(ty[58, 1]), 1):.0f} "
-              f"effective engine clock {ty[58, 0] / max(float(ty[59, 0]), 1) * 100:.0f} MHz", file=sys.stderr)
+              f"effective engine clock {ty[58, 0] / max(float(ty[59, 0]), 1) * 100:.0f} MHz "
+              + " ".join(f"{k}={v:.0f}" for k, v in ph.items()), file=sys.stderr)
 
     if args.check_replicas and info.enabled:
         import torch.distributed as dist

@@ -511,7 +511,8 @@ class BatchedTrainer:
                 n = nat.cu_count()
                 k = max(8, min(int(sim_cus), n - 8))
                 self.sim_cus = k
-                sim_list = self.sim_cu_list(n, k)
+                small_env = (160 * 1024) // max(int(sim.ctx.lds_per_env), 1) >= 4
+                sim_list = self.sim_cu_list(n, k, spread_default=small_env)
                 rest = [c for c in range(n) if c not in set(sim_list)]
                 self.sim_stream = torch.cuda.ExternalStream(nat.create_cu_masked_stream(sim_list),
                                                             device=self.device)
@@ -530,12 +531,12 @@ class BatchedTrainer:
                         nat.create_cu_masked_stream(rest), device=self.device)
                 # The act path (actor forward + exploration of step t+1) sits between two simulator
                 # steps, when the learner's CUs are idle too (update t done, update t+1 waits for it):
-                # an unmasked stream gives it every CU.  Auto: on when the learner is the longer chain
-                # (unmasked learner: the act path then waits on the learner and sits on the critical path;
-                # measured syn50 19.41k -> 19.63k, syn200 5.08k -> 5.13k, profiles/act_stream_ab.txt), off
-                # for simulator-bound small topologies (Abilene: measured slower).  GSC_ACT_STREAM=0/1 forces.
+                # an unmasked stream gives it every CU.  Measured: syn50 19.41k -> 19.63k, syn200 5.08k ->
+                # 5.13k (profiles/act_stream_ab.txt) and, since the simulator kernel's round-5 diet made
+                # the headline simulator-bound with the learner finishing first, Abilene 114.4k -> 120.4k
+                # (xcd-spread 64 simulator CUs).  GSC_ACT_STREAM=0 keeps it on the simulator's stream.
                 act_env = os.environ.get("GSC_ACT_STREAM", "auto")
-                if act_env == "1" or (act_env == "auto" and learner_unmasked):
+                if act_env != "0":
                     self.act_stream = torch.cuda.Stream(self.device)
                 # persistent GNN grids sized to the CUs free while the simulator runs (one full round)
                 budget = int(os.environ.get("GSC_GNN_CU_BUDGET", str(n - k)))
@@ -544,13 +545,17 @@ class BatchedTrainer:
                 self.sim_stream = torch.cuda.Stream(self.device)
 
     @staticmethod
-    def sim_cu_list(n: int, k: int) -> List[int]:
-        """The simulator's CU-mask bits.  ``GSC_SIM_CU_LAYOUT=xcd`` (default): k / 8 bits of every 32-bit block
-        (the same CU count in each of MI355X's 8 XCDs); ``contig``: bits 0 .. k-1.  Measured round 5, 256
-        Abilene envs (4 per CU) standalone: 64 contiguous bits 2.21 ms/step, 64 spread 8 per block 1.98 ms
-        (= 96 contiguous bits: 1.95) -- with the contiguous mask the simulator's waves contend for issue
-        (SQ_WAIT_INST_ANY 2.85e7 vs 8.0e4 per dispatch at one wave per CU)."""
-        layout = os.environ.get("GSC_SIM_CU_LAYOUT", "xcd")
+    def sim_cu_list(n: int, k: int, spread_default: bool = True) -> List[int]:
+        """The simulator's CU-mask bits.  ``GSC_SIM_CU_LAYOUT=xcd``: k / 8 bits of every 32-bit block (the same
+        CU count in each of MI355X's 8 XCDs); ``contig``: bits 0 .. k-1; auto (default): xcd for envs that
+        pack four per CU (Abilene-class), else contig.  Measured round 5: 256 Abilene envs (4 per CU)
+        standalone 64 contiguous bits 2.21 ms/step vs 64 spread 1.98 ms (the contiguous mask's waves stall
+        on issue: SQ_WAIT_INST_ANY 2.85e7 vs 8.0e4 per dispatch at one wave per CU), bench 120.3k spread;
+        syn50 23.8k contiguous vs 16.3k spread, syn200 5.24k vs 4.32k (their learner kernels need whole
+        XCDs)."""
+        layout = os.environ.get("GSC_SIM_CU_LAYOUT", "auto")
+        if layout == "auto":
+            layout = "xcd" if spread_default else "contig"
         if layout == "xcd" and n % 32 == 0 and k % (n // 32) == 0:
             per = k // (n // 32)
             return [c for c in range(n) if c % 32 < per]
@@ -558,12 +563,11 @@ class BatchedTrainer:
 
     @staticmethod
     def auto_sim_cus(sim) -> int:
-        """CUs for one round of the simulator's env workgroups, at most 3 envs (waves) per CU, rounded up
-        to whole XCDs (MI355X: 8 XCDs x 32 CUs, each with its own L2; contiguous CU-mask bits fill one XCD
-        after the other), capped at half the device.  The simulator waves are issue- and fetch-latency
-        bound: four per CU (one per SIMD) share the CU's instruction fetch, and per-wave speed drops
-        (round 5, 256 Abilene envs standalone: 2.29 ms/step on 64 CUs = 4 per CU, 2.06 on 96, 1.99 on 128;
-        bench 108.5k at 64, 113.7k at 96).
+        """CUs for one round of the simulator's env workgroups, at most 4 envs (waves) per CU with the
+        default per-XCD spread mask (3 with contiguous mask bits), rounded up to a multiple of 8 (one per
+        XCD block), capped at half the device.  Round 5, 256 Abilene envs: 64 spread CUs (8 per XCD)
+        1.98 ms/step standalone vs 2.21 on 64 contiguous bits (2.06 on 96, 1.99 on 128 contiguous);
+        bench 120.4k at 64 spread (with the act path on an unmasked stream), 113.7k at 96 contiguous.
         Earlier, on MI355X, 256 Abilene envs, 39.9 KB of LDS per env (env-steps/s, round 3): 64 CUs (two
         XCDs, 4 envs per CU) 113.3k; 96 CUs 111.0k; 128 CUs 96.4k (the learner becomes the longer
         chain); 72 / 80 / 88 / 112 CUs 71-84k (an XCD shared between simulator and learner); 32 CUs
@@ -573,7 +577,7 @@ class BatchedTrainer:
         n = nat.cu_count()
         xcd = max(n // 8, 8)
         lds = max(int(sim.ctx.lds_per_env), 1)
-        per_cu = max(1, min(3, (160 * 1024) // lds))
+        per_cu = max(1, min(4 if os.environ.get("GSC_SIM_CU_LAYOUT", "auto") != "contig" else 3, (160 * 1024) // lds))
         need = -(-sim.E // per_cu)
         # Mid-size topologies (33..64 nodes: two envs per CU by LDS, the learner's two-tile GATv2 kernels
         # need 52-81 KB of LDS and cannot share those CUs) are learner-bound: half a round's CUs, so the
