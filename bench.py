@@ -223,6 +223,10 @@ def main():
                 "sim_learner_overlap": not args.no_overlap,
                 "sim_cus": getattr(trainer, "sim_cus", 0),
                 "episode_steps": ep_steps,
+                "replay_capacity": trainer.replay.capacity,
+                "replay_actions": "sparse rows" if getattr(trainer.replay, "sparse_rows", 0) else "dense",
+                **({"peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 1)}
+                   if device.type == "cuda" else {}),
                 "scheduler_period": period,
                 "topology_switches_timed": switches,
                 "topology": ",".join(os.path.basename(n) for n in networks),

@@ -3,7 +3,8 @@
 // Lane-parallel over each (env, src, sfc, sf) slice of n_pad destination weights: two slices per
 // wave (32 lanes each) up to n_pad = 32, one slice per wave with up to four consecutive weights per
 // lane up to n_pad = 256 (the 200-node configs).  Noise comes from a counter-based Philox stream keyed
-// by (seed, step, weight index), so results do not depend on launch shape.  The two
+// by (seed, step, flat quad index) -- one draw per four weights -- so results do not depend on launch
+// shape.  The two
 // threshold/normalise passes run in fp64 (cross-lane sums; the reference sums Python floats left to
 // right, so results agree to float32 rounding) with the residual of the rounded sum added to the
 // first weight that can absorb it, found by a ballot.
@@ -16,24 +17,54 @@ namespace py = pybind11;
 
 namespace gsc {
 
-__device__ __forceinline__ double round10(double x) { return rint(x * 1e10) / 1e10; }
+// Round to 10 decimals: x * 1e10 to the nearest integer, scaled back by a multiply (1 ulp of fp64 from the
+// division the reference's round(x, 10) implies; invisible after the float32 store)
+__device__ __forceinline__ double round10(double x) { return rint(x * 1e10) * 1e-10; }
 
-// Noisy (or warm-up uniform) weight i of the slice starting at flat index base: one Philox4x32-10
-// draw per pair of weights (keyed by the pair's first index), fp32 Box-Muller, both outputs used.
+// Noise of the 4 weights of flat quad f4 (= flat index & ~3): ONE Philox4x32-10 draw keyed by (seed, step, f4),
+// its four uniforms -> warm-up: the uniforms; else two fp32 Box-Muller pairs (v0, v1) -> weights 0, 1 and
+// (v2, v3) -> weights 2, 3.  The value of a weight depends only on (seed, step, flat index).
+struct Quad { float x[4]; };
+__device__ __forceinline__ Quad explore_quad(uint64_t f4, int warmup, uint32_t seed, uint32_t step) {
+  const Philox4 r = philox4x32_10(seed, step, f4);
+  Quad q;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) q.x[j] = (float)(r.v[j] >> 8) * (1.0f / 16777216.0f);  // [0, 1)
+  if (warmup) return q;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float rad = sqrtf(-2.0f * __logf(1.0f - q.x[2 * p]));  // 1 - u in (0, 1]
+    float sn, cs;
+    __sincosf(6.283185307179586f * q.x[2 * p + 1], &sn, &cs);
+    q.x[2 * p] = rad * cs;
+    q.x[2 * p + 1] = rad * sn;
+  }
+  return q;
+}
+
+// Weight from its noise value z (normal, or the warm-up uniform) and mu / mask.
+__device__ __forceinline__ float explore_apply(float z, float mu, float m, int warmup, float rand_mu, float rand_sigma) {
+  if (warmup) return z * m;
+  const float sv = 2.0f * mu - 1.0f + rand_mu + rand_sigma * z;
+  const float a = 0.5f * (sv + 1.0f);
+  return a < 0.f ? 0.f : (a > 1.f ? 1.f : a);
+}
+
+// Noisy (or warm-up uniform) weight i of the slice starting at flat index base (explore_quad's value for it,
+// with only its own Box-Muller pair evaluated).
 __device__ __forceinline__ float explore_weight(const float* __restrict__ mu, const float* __restrict__ mrow, long base,
                                                 int i, int warmup, float rand_mu, float rand_sigma, uint32_t seed,
                                                 uint32_t step) {
-  const int i0 = i & ~1;
-  const Philox4 r = philox4x32_10(seed, step, (uint64_t)(base + i0));
-  const float u0 = (float)(r.v[0] >> 8) * (1.0f / 16777216.0f);  // [0, 1)
-  const float u1 = (float)(r.v[1] >> 8) * (1.0f / 16777216.0f);
-  if (warmup) return (i & 1 ? u1 : u0) * mrow[i];
-  const float rad = sqrtf(-2.0f * __logf(1.0f - u0));  // 1 - u0 in (0, 1]
+  const uint64_t f = (uint64_t)(base + i);
+  const Philox4 r = philox4x32_10(seed, step, f & ~3ull);
+  const int j = (int)(f & 3);
+  const uint32_t va = (j & 2) ? r.v[2] : r.v[0], vb = (j & 2) ? r.v[3] : r.v[1];
+  const float u0 = (float)(va >> 8) * (1.0f / 16777216.0f), u1 = (float)(vb >> 8) * (1.0f / 16777216.0f);
+  if (warmup) return ((j & 1) ? u1 : u0) * mrow[i];
+  const float rad = sqrtf(-2.0f * __logf(1.0f - u0));
   float sn, cs;
   __sincosf(6.283185307179586f * u1, &sn, &cs);
-  const float sv = 2.0f * mu[base + i] - 1.0f + rand_mu + rand_sigma * (rad * (i & 1 ? sn : cs));
-  const float a = 0.5f * (sv + 1.0f);
-  return a < 0.f ? 0.f : (a > 1.f ? 1.f : a);
+  return explore_apply(rad * ((j & 1) ? sn : cs), mu[base + i], 0.f, 0, rand_mu, rand_sigma);
 }
 
 // n_pad <= 32: 32 lanes per slice (one weight per lane), two slices per wave.
@@ -65,7 +96,7 @@ __global__ __launch_bounds__(256) void explore_postprocess_lanes_kernel(const fl
     w = on && w >= thr ? w : 0.0;
     const double s = half_sum(w);
     if (s == 0.0) w = on ? round10(1.0 / P) : 0.0;
-    else if (fabs(1.0 - s) > acc && on) w = round10(w / s);
+    else if (fabs(1.0 - s) > acc && on) w = round10(w * (1.0 / s));
     const double r = 1.0 - half_sum(w);
     if (r != 0.0) {
       // first element that can absorb the residual (the last one otherwise)
@@ -91,32 +122,19 @@ __device__ __forceinline__ double wave_sum(double v) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63), __builtin_amdgcn_readlane(__double2loint(v), 63));
 }
 
-// Noisy (or warm-up uniform) weights i0, i0 + 1 of a slice from ONE Philox draw (the pair's two uniforms,
-// both Box-Muller outputs) -- explore_weight's values for both members of the pair.
-__device__ __forceinline__ void explore_pair(const float* __restrict__ mu, const float* __restrict__ mrow, long base,
-                                            int i0, int warmup, float rand_mu, float rand_sigma, uint32_t seed,
-                                            uint32_t step, float& w0, float& w1) {
-  const Philox4 r = philox4x32_10(seed, step, (uint64_t)(base + i0));
-  const float u0 = (float)(r.v[0] >> 8) * (1.0f / 16777216.0f);
-  const float u1 = (float)(r.v[1] >> 8) * (1.0f / 16777216.0f);
-  if (warmup) {
-    w0 = u0 * mrow[i0];
-    w1 = u1 * mrow[i0 + 1];
-    return;
-  }
-  const float rad = sqrtf(-2.0f * __logf(1.0f - u0));
-  float sn, cs;
-  __sincosf(6.283185307179586f * u1, &sn, &cs);
-  const float s0 = 2.0f * mu[base + i0] - 1.0f + rand_mu + rand_sigma * (rad * cs);
-  const float s1 = 2.0f * mu[base + i0 + 1] - 1.0f + rand_mu + rand_sigma * (rad * sn);
-  const float a0 = 0.5f * (s0 + 1.0f), a1 = 0.5f * (s1 + 1.0f);
-  w0 = a0 < 0.f ? 0.f : (a0 > 1.f ? 1.f : a0);
-  w1 = a1 < 0.f ? 0.f : (a1 > 1.f ? 1.f : a1);
-}
-
 // 32 < n_pad <= 256: one slice per wave, K <= 4 consecutive weights per lane (lane l holds weights
 // K l .. K l + K - 1, so "the first weight that can absorb the residual" is the first lane of a
 // ballot, then the first of its K).
+// Optional simulator hand-off (PMask.base != 0): the positive-destination bitset of every post-processed row,
+// written into the simulator state's pmask block (what sim_pmask_kernel would derive from the stored action
+// block in a second HBM pass).  Row (src, c, sf) of env e -> 4 x u64 at base + e stride + 32 ((src Cd + c) Sd
+// + sf); bit d = (weight d > 0 and mask d > 0), i.e. a positive weight on a real destination of the topology.
+struct PMask {
+  char* base;
+  long stride;
+  int C, F, Cd, Sd;
+};
+
 template <int K>
 __global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const float* __restrict__ mu,
                                                                       const float* __restrict__ mask,
@@ -124,29 +142,39 @@ __global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const flo
                                                                       float* __restrict__ out, int E, int A, int P,
                                                                       int warmup, float rand_mu, float rand_sigma,
                                                                       uint32_t seed, uint32_t step, double thr,
-                                                                      int passes) {
+                                                                      int passes, PMask pm) {
   const int R = A / P;
   const long slice = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (slice >= (long)E * R) return;  // whole waves exit together
   const long base = slice * P;
   const float* mrow = topo ? mask + topo[slice / R] * (long)A + (slice % R) * P : mask + base;
+  // lane's weights: flat indices f0 .. f0 + K - 1, within one or two Philox quads
   double w[K];
-  if constexpr (K % 2 == 0) {  // K even: lanes own whole pairs (one Philox draw per pair)
-#pragma unroll
-    for (int k = 0; k < K; k += 2) {
-      const int i = K * lane + k;
-      float a = 0.f, b = 0.f;
-      if (i + 1 < P) explore_pair(mu, mrow, base, i, warmup, rand_mu, rand_sigma, seed, step, a, b);
-      else if (i < P) a = explore_weight(mu, mrow, base, i, warmup, rand_mu, rand_sigma, seed, step);  // odd P
-      w[k] = a;
-      w[k + 1] = b;
+  {
+    const int i0 = K * lane;
+    const uint64_t f0 = (uint64_t)(base + i0);
+    const bool any = i0 < P;
+    Quad qa{}, qb{};
+    if (any) {
+      qa = explore_quad(f0 & ~3ull, warmup, seed, step);
+      const uint64_t fl = f0 + K - 1;
+      if ((fl >> 2) != (f0 >> 2) && i0 + (int)(((f0 & ~3ull) + 4) - f0) < P)
+        qb = explore_quad(fl & ~3ull, warmup, seed, step);
     }
-  } else {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int i = K * lane + k;
-      w[k] = i < P ? (double)explore_weight(mu, mrow, base, i, warmup, rand_mu, rand_sigma, seed, step) : 0.0;
+      const int i = i0 + k;
+      const int j = (int)((f0 & 3) + k);  // 0..6: quad a below 4, quad b from 4
+      float z = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (j == t) z = qa.x[t];
+        if (j == t + 4) z = qb.x[t];
+      }
+      w[k] = i < P ? (double)explore_apply(z, warmup ? 0.f : mu[base + i], warmup ? mrow[i] : 0.f, warmup, rand_mu,
+                                           rand_sigma)
+                   : 0.0;
     }
   }
   const double acc = 1.4901161193847656e-08;  // sqrt(float64 eps)
@@ -160,12 +188,13 @@ __global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const flo
     }
     const double s = wave_sum(ps);
     const bool renorm = fabs(1.0 - s) > acc;
+    const double inv = s != 0.0 ? 1.0 / s : 0.0;  // one division per slice and pass
     ps = 0.0;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const bool on = K * lane + k < P;
       if (s == 0.0) w[k] = on ? uni : 0.0;
-      else if (renorm && on) w[k] = round10(w[k] / s);
+      else if (renorm && on) w[k] = round10(w[k] * inv);
       ps += w[k];
     }
     const double r = 1.0 - wave_sum(ps);
@@ -187,12 +216,50 @@ __global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const flo
 #pragma unroll
   for (int k = 0; k < K; ++k)
     if (K * lane + k < P) out[base + K * lane + k] = (float)w[k];
+  if (pm.base) {
+    uint64_t bk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = K * lane + k;
+      bk[k] = (uint64_t)__ballot(i < P && w[k] > 0.0 && mrow[i] > 0.f);
+    }
+    // destination d = K l + k sits at bit l of bk[k]: regroup into 64-destination words (lane q keeps word q)
+    uint64_t word = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int d = 64 * q + lane;
+      const int kk = d % K, l = d / K;
+      uint64_t b = bk[0];
+#pragma unroll
+      for (int k = 1; k < K; ++k)
+        if (kk == k) b = bk[k];
+      const uint64_t wq = (uint64_t)__ballot(d < P && ((b >> (l & 63)) & 1ull) && l < 64);
+      if (lane == q) word = wq;
+    }
+    const int row = (int)(slice % R);
+    const int sf = row % pm.F, c = (row / pm.F) % pm.C, src = row / (pm.F * pm.C);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(pm.base + (slice / R) * pm.stride) + 4L * ((src * pm.Cd + c) * pm.Sd + sf);
+    if (lane < 4) dst[lane] = word;
+  }
 }
 
 void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t out, int E, int A, int P, int warmup, float rand_mu,
-                         float rand_sigma, uint32_t seed, uint32_t step, double thr, int passes, uintptr_t stream) {
+                         float rand_sigma, uint32_t seed, uint32_t step, double thr, int passes, uintptr_t stream,
+                         py::object pmask) {
   GSC_CHECK(A % P == 0, "action dim must be a multiple of n_pad");
   GSC_CHECK(P <= 256, "n_pad > 256 not supported by the exploration kernel");
+  PMask pm{nullptr, 0, 1, 1, 1, 1};
+  if (!pmask.is_none()) {  // (base, stride, C, F, Cd, Sd)
+    py::tuple t = pmask.cast<py::tuple>();
+    pm.base = ptr<char>(t[0].cast<uintptr_t>());
+    pm.stride = t[1].cast<long>();
+    pm.C = t[2].cast<int>();
+    pm.F = t[3].cast<int>();
+    pm.Cd = t[4].cast<int>();
+    pm.Sd = t[5].cast<int>();
+    GSC_CHECK(P > 32 && (long)P * P * pm.C * pm.F == A && pm.C <= pm.Cd && pm.F <= pm.Sd,
+              "explore pmask hand-off: n_pad > 32 and A = n_pad^2 C F within the simulator dims");
+  }
   const long slices = (long)E * (A / P);
   if (P <= 32) {
     const int sl_per_block = 8;
@@ -204,7 +271,7 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, stream_of(stream), ptr<const float>(mu), ptr<const float>(mask),
                          ptr<const long long>(topo), ptr<float>(out), E, A, P, warmup, rand_mu, rand_sigma, seed, step, thr,
-                         passes);
+                         passes, pm);
     };
     if (P <= 64) go(explore_postprocess_wave_kernel<1>);
     else if (P <= 128) go(explore_postprocess_wave_kernel<2>);
@@ -215,7 +282,10 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t
 }
 
 void register_explore(py::module_& m) {
-  m.def("explore_postprocess", &explore_postprocess, "fused exploration + threshold/normalise (device)");
+  m.def("explore_postprocess", &explore_postprocess, "fused exploration + threshold/normalise (device)",
+        py::arg("mu"), py::arg("mask"), py::arg("topo"), py::arg("out"), py::arg("E"), py::arg("A"), py::arg("P"),
+        py::arg("warmup"), py::arg("rand_mu"), py::arg("rand_sigma"), py::arg("seed"), py::arg("step"), py::arg("thr"),
+        py::arg("passes"), py::arg("stream"), py::arg("pmask") = py::none());
 }
 
 }  // namespace gsc

@@ -10,6 +10,7 @@ void register_streams(py::module_& m);
 void register_replay(py::module_& m);
 void register_gnn_lw(py::module_& m);
 void register_actor_proj(py::module_& m);
+void register_sparse_act(py::module_& m);
 void register_ops(py::module_& m) {
   register_explore(m);
   register_gnn(m);
@@ -19,5 +20,6 @@ void register_ops(py::module_& m) {
   register_replay(m);
   register_gnn_lw(m);
   register_actor_proj(m);
+  register_sparse_act(m);
 }
 }  // namespace gsc

@@ -700,6 +700,13 @@ class SimContext {
   bool use_lds() const { return lds_mode_ != 0; }
   // 0: state in HBM, 1: whole state blob in LDS, 2: its hot prefix in LDS (schedule / WRR tables in HBM)
   int lds_mode() const { return lds_mode_; }
+  bool uses_pmask() const { return device_ && lds_mode_ != 1 && pmask_rows(D_) > 0; }
+  // where a producer of the action block may write the step kernel's destination bitsets (explore.hip PMask):
+  // (offset of the pmask block in an env's state, its C and S dims), or None when the kernel does not read them
+  py::object pmask_layout() const {
+    if (!uses_pmask()) return py::none();
+    return py::make_tuple((long)L_.pmask, D_.C, D_.S);
+  }
   long lds_state() const { return lds_mode_ == 1 ? L_.total : (lds_mode_ == 2 ? L_.hot : 0); }
   // LDS bytes one env's workgroup needs on the device (SimConst + topology tables + staged state)
   long lds_per_env() const { return const_stage_bytes() + topo_stage_ + lds_state(); }
@@ -719,7 +726,7 @@ class SimContext {
 
   void step(uintptr_t states, uintptr_t topo_next, uintptr_t seeds, uintptr_t actions, long action_stride,
             uintptr_t obs, uintptr_t next_obs, uintptr_t reward, uintptr_t done, uintptr_t stats,
-            uintptr_t ep_return, int E, uintptr_t stream, uintptr_t prof, uintptr_t topo_cur) {
+            uintptr_t ep_return, int E, uintptr_t stream, uintptr_t prof, uintptr_t topo_cur, bool pmask_ready) {
     SimArgs a = args(states, topo_next, seeds, actions, action_stride, obs, next_obs, reward, done, stats,
                      ep_return, E);
     a.topo_cur = ptr<int32_t>(topo_cur);
@@ -730,7 +737,8 @@ class SimContext {
     if (device_) {
       const size_t lds = (size_t)lds_per_env();
       const hipStream_t st = stream_of(stream);
-      if (lds_mode_ != 1 && pmask_rows(D_) > 0) {  // HBM-resident tables (BIG kernels), > 64 nodes
+      // HBM-resident tables (BIG kernels), > 64 nodes; pmask_ready: the exploration kernel wrote the bitsets
+      if (uses_pmask() && !pmask_ready) {
         hipLaunchKernelGGL(sim_pmask_kernel, dim3(E, (pmask_rows(D_) + 3) / 4), dim3(256), 0, st, a);
         check_launch();
       }
@@ -862,11 +870,12 @@ void register_sim(py::module_& m) {
       .def_property_readonly("lds_per_env", &SimContext::lds_per_env)
       .def_property_readonly("lds_mode", &SimContext::lds_mode)
       .def_property_readonly("hot_bytes", &SimContext::hot_bytes)
+      .def_property_readonly("pmask_layout", &SimContext::pmask_layout)
       .def("reset", &SimContext::reset)
       .def("step", &SimContext::step, py::arg("states"), py::arg("topo_next"), py::arg("seeds"), py::arg("actions"),
            py::arg("action_stride"), py::arg("obs"), py::arg("next_obs"), py::arg("reward"), py::arg("done"),
            py::arg("stats"), py::arg("ep_return"), py::arg("E"), py::arg("stream"), py::arg("prof") = 0,
-           py::arg("topo_cur") = 0);
+           py::arg("topo_cur") = 0, py::arg("pmask_ready") = false);
   m.attr("SIM_NUM_STATS") = kNumStats;
   m.attr("SIM_HEADER_BYTES") = (int)sizeof(Header);
 }

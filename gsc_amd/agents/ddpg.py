@@ -454,17 +454,37 @@ class BatchedTrainer:
         self.learner = DDPGLearner(cfg, sim.n_obs, sim.action_dim, self.graphs, sim.C, sim.F, self.device,
                                    self.dist, amp_bf16=tcfg.amp_bf16, seed=tcfg.seed)
         cap = tcfg.replay_capacity or min(int(cfg.get("mem_limit", 10000)) * self.E, tcfg.replay_cap_max)
-        # byte budget: large action spaces (50/200-node topologies, A = N^2 C F) bound the ring size
         adt = torch.bfloat16 if self.learner.amp else torch.float32
-        per = 4 * (2 * sim.n_pad * sim.n_obs + 4) + torch.empty((), dtype=adt).element_size() * sim.action_dim
-        budget = tcfg.replay_bytes_max or (0.25 * torch.cuda.get_device_properties(self.device).total_memory
+        # Ring representation.  Dense: bf16 [A]-wide action rows.  Sparse (csrc/ops/sparse_act.hip): the
+        # post-processed action as row records -- base value + <= 11 exceptions per n_pad-wide row, exact -- 48 B
+        # per row instead of 2 n_pad B.  GSC_SPARSE_REPLAY=auto (default) picks sparse only when the dense ring
+        # cannot hold the reference's min(mem_limit E, replay_cap_max) transitions in 60 % of HBM (config 5:
+        # 2M x 720 KB; config 4's 2M x 45 KB fits dense, whose GEMMs are faster at small A); 1 forces it where
+        # the native kernels apply (n_pad <= 240, critic first layer 64 wide), 0 disables it.
+        R_rows = sim.action_dim // sim.n_pad
+        obs_bytes = 4 * (2 * sim.n_pad * sim.n_obs + 4)
+        dense_per = obs_bytes + torch.empty((), dtype=adt).element_size() * sim.action_dim
+        sparse_per = obs_bytes + 48 * R_rows
+        hbm = torch.cuda.get_device_properties(self.device).total_memory if self.device.type == "cuda" else 0
+        mode = os.environ.get("GSC_SPARSE_REPLAY", "auto")
+        eligible = bool(self.learner.native_ok and self.device.type == "cuda" and sim.n_pad <= 240
+                        and self.learner.critic.mlp.layers[0].weight.shape[0] == 64 and mode != "0")
+        self.sparse_replay = eligible and (mode == "1" or cap * dense_per > 0.6 * hbm)
+        if self.sparse_replay:
+            per, frac = sparse_per, 0.65  # syn200: 2M x 91 KB = 182 GB of 288 GB; the learner needs < 40 GB
+        else:
+            per, frac = dense_per, 0.6
+        # byte budget of the ring (the dense [A]-wide rows of large action spaces bound its size)
+        budget = tcfg.replay_bytes_max or (frac * torch.cuda.get_device_properties(self.device).total_memory
                                            if self.device.type == "cuda" else 4e9)
         cap = int(min(cap, budget // per))
         # on the GPU actions are stored in bf16: the critic consumes them as bf16 GEMM operands
         # (bf16 rows padded to 8 columns: 16-byte aligned operand rows for the native learner's GEMMs)
         self.replay = DeviceReplay(max(cap, self.E), sim.n_pad, sim.n_obs, sim.action_dim, self.device,
                                    action_dtype=adt, seed=tcfg.seed + 7919 * self.dist.rank,
-                                   action_row_align=8 if adt == torch.bfloat16 else 1)
+                                   action_row_align=8 if adt == torch.bfloat16 else 1,
+                                   sparse_rows=R_rows if self.sparse_replay else 0)
+        self._pmask_ready = False   # this step's action producer wrote the simulator's destination bitsets
         self.batch_size = tcfg.batch_size or 100 * self.E
         self.learning_starts = (tcfg.learning_starts if tcfg.learning_starts is not None
                                 else int(cfg.get("nb_steps_warmup_critic", 200)))
@@ -665,9 +685,13 @@ class BatchedTrainer:
         with trace_range("act"):
             mu = self.learner.act(obs, topo)
         with trace_range("explore"):
+            # topologies beyond 64 nodes: the exploration kernel also writes the simulator's destination
+            # bitsets from the rows it holds in registers (no second pass over the action block)
+            pm = self.sim.pmask_target() if (mu.is_cuda and os.environ.get("GSC_EXPLORE_PMASK", "1") != "0") else None
+            self._pmask_ready = pm is not None
             return explore_postprocess(mu, self.masks, self.sim.n_pad, warm, self.rand_mu, self.rand_sigma,
                                        seed=self.t.seed * 131 + self.dist.rank, step=self.global_step,
-                                       out=self._act_bufs[k], topo=topo)
+                                       out=self._act_bufs[k], topo=topo, pmask=pm)
 
     def _step(self) -> None:
         warm = self.global_step < self.learning_starts
@@ -698,7 +722,7 @@ class BatchedTrainer:
                     ev_act = self._event()
                     ev_act.record(self.sim_stream)
                 self._schedule_next()
-                out = self.sim.step(act, buffer_set=k, obs_out=obs_next)
+                out = self.sim.step(act, buffer_set=k, obs_out=obs_next, pmask_ready=self._pmask_ready)
                 ev_sim = self._event()
                 ev_sim.record(self.sim_stream)
                 if episode_end:
@@ -716,7 +740,7 @@ class BatchedTrainer:
             # insert and the learner update, which samples transitions up to the previous step
             self.sim_stream.wait_stream(main)
             with torch.cuda.stream(self.sim_stream):
-                out = self.sim.step(act, buffer_set=k, obs_out=obs_next)
+                out = self.sim.step(act, buffer_set=k, obs_out=obs_next, pmask_ready=self._pmask_ready)
             self._flush_pending()
             with trace_range("learn"):
                 self._learn()
@@ -727,7 +751,7 @@ class BatchedTrainer:
             self._schedule_next()
             self._flush_pending()
             with trace_range("sim"):
-                out = self.sim.step(act, buffer_set=k, obs_out=obs_next)
+                out = self.sim.step(act, buffer_set=k, obs_out=obs_next, pmask_ready=self._pmask_ready)
             self._record(obs, topo, act, out)
             if train:
                 with trace_range("learn"):
@@ -742,22 +766,30 @@ class BatchedTrainer:
             if overlap and self.t.act_on_sim_stream:
                 main.wait_stream(self.sim_stream)
             self.sim.check_flags()
+            self.replay.check_sparse()
 
     def _learn(self) -> None:
         if _DIAG_NO_LEARN:  # diagnostics only (never in bench numbers): measures the act + sim chain alone
             return
         for _ in range(self.t.updates_per_step):
-            if self.graphed:
+            if self.graphed or self.replay.sparse_rows:
                 if self._batch is None:
                     B = self.batch_size
                     fused = self.fused_action_gather()
                     self._batch = self.replay.empty_batch(B, actions=not fused)
                     out = self._batch
                     if fused:  # the critic's action GEMMs read the sampled ring rows in place
-                        self.learner.native_update(B).act_rows = self.replay.indices(B)
+                        nu = self.learner.native_update(B)
+                        nu.act_rows = self.replay.indices(B)
+                        if self.replay.sparse_rows:
+                            nu.set_sparse(self.replay.actions, self.replay.sparse_rows, self.replay.n_pad)
                     sink = self._topo_sink = self.learner.topo32_buffer(B)
                     self._sampler = lambda: self.replay.sample(B, out=out, topo32=sink, actions=not fused)
-                self.learner.update_graphed(self._batch, pre=self._sampler, topo_ready=self._topo_sink is not None)
+                if self.graphed:
+                    self.learner.update_graphed(self._batch, pre=self._sampler, topo_ready=self._topo_sink is not None)
+                else:
+                    self._sampler()
+                    self.learner.update(self._batch)
             else:
                 self.learner.update(self.replay.sample(self.batch_size))
 
@@ -765,6 +797,8 @@ class BatchedTrainer:
         """Replayed actions read in place by the native learner's GEMMs (row-indexed operands) instead of
         gathered into a [B, A] batch: on by default once that batch copy exceeds 256 MB (50/200-node
         topologies: 1.2 / 18 GB at B = 25,600); GSC_FUSED_GATHER=0/1 forces it."""
+        if self.replay.sparse_rows:
+            return True   # sparse records are only ever read in place
         if not (self.learner.native_ok and self.replay.actions.dtype == torch.bfloat16):
             return False
         env = os.environ.get("GSC_FUSED_GATHER")

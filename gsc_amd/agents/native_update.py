@@ -57,6 +57,27 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 
 
+def sparse_fwd_splits(B: int, R: int, max_splits: int, dev=None) -> int:
+    """Row-block splits of ``sparse_fwd`` (256 samples x R / S row blocks per workgroup, one workgroup per CU):
+    the S in 1..min(R, max_splits, 64) whose ceil(B / 256) S workgroups best fill whole rounds of the device's
+    CUs (at least two rounds): the smallest S within 95 % of a whole number of rounds (fewer partial sums to
+    reduce), else the best."""
+    cus = 256
+    if dev is not None and torch.cuda.is_available():
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    tiles = -(-B // 256)
+    best, best_eff = 1, -1.0
+    for S in range(1, max(1, min(R, max_splits, 64)) + 1):
+        wgs = tiles * S
+        rounds = -(-wgs // cus)
+        eff = wgs / (rounds * cus) if rounds >= 2 else wgs / (2 * cus)
+        if eff >= 0.95:
+            return S
+        if eff > best_eff + 1e-9:
+            best, best_eff = S, eff
+    return best
+
+
 class _Net:
     """Pointers/views of one Actor or QNetwork inside its FlatParams (fp32 master, bf16 shadow, grad)."""
 
@@ -204,6 +225,19 @@ class NativeDDPGUpdate:
         # replayed actions read in place from the ring: ``b.actions`` is then the ring and these are the
         # sampled rows (DeviceReplay.sample(actions=False)); None: ``b.actions`` is the gathered [B, A] batch
         self.act_rows: Optional[torch.Tensor] = None
+        # sparse replay rings (DeviceReplay(sparse_rows=R), csrc/ops/sparse_act.hip): set_sparse() binds the
+        # record ring; the critic's action products then run on the row records instead of a [B, A] block
+        self.sparse = None
+
+    def set_sparse(self, ring: torch.Tensor, R: int, P: int) -> None:
+        if self.critic.width(0) != 64:
+            raise ValueError("sparse replayed actions need the critic's first layer width 64 (GSC_SPARSE_REPLAY=0)")
+        if P > 240:
+            raise ValueError("sparse replayed actions: at most 240 destinations per row (GSC_SPARSE_REPLAY=0)")
+        self.sparse = (ring, int(R), int(P))
+        # row-block splits of the forward (one 138 KB-LDS workgroup per CU): the split count whose workgroup
+        # total best fills whole dispatch rounds of the CUs, within the split-K slabs
+        self.sp_splits = sparse_fwd_splits(self.B, int(R), self.slabs.numel() // (self.B * 64), self.dev)
 
     # ------------------------------------------------------------------------------------------
     def _stream(self) -> int:
@@ -367,10 +401,14 @@ class NativeDDPGUpdate:
         self._critic_tail(tc, self.hid_c, 0, None, b)
         # critic on (s, a): loss + gradients
         self._gnn_fwd(c, b.obs, self.emb["c"], self.blob["c"], key="c")
-        acts = b.actions[:, :A]   # replay rows are padded to 8 columns (16-byte aligned)
         rows = self.act_rows      # the ring itself, addressed by the sampled rows (no [B, A] batch copy)
-        self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], extra=acts, wa=self._wa(c, "c"),
-                    extra_rows=rows)
+        if self.sparse is not None:
+            self._sparse_first(c, rows)
+            acts = None
+        else:
+            acts = b.actions[:, :A]   # replay rows are padded to 8 columns (16-byte aligned)
+            self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], extra=acts, wa=self._wa(c, "c"),
+                        extra_rows=rows)
         self._hidden_fwd(c, self.hid_c)
         C = c.width(c.nh - 1)
         dh = self.dh[0][:, :C]
@@ -378,7 +416,30 @@ class NativeDDPGUpdate:
         self._head_reduce(c, C, 1)
         dh0 = self._hidden_bwd(c, self.hid_c, dh, grads=True)
         self._first_bwd(c, self.emb["c"], dh0, extra=acts, extra_rows=rows)
+        if self.sparse is not None:
+            self._sparse_wgrad(c, dh0, rows)
         self._gnn_bwd(c, b.obs, self.demb, self.blob["c"], key="c")
+
+    # -- sparse replayed actions (csrc/ops/sparse_act.hip) ----------------------------------------------------
+    def _sparse_first(self, c: _Net, rows: torch.Tensor) -> None:
+        """Critic first layer on replayed sparse actions: hacc = a W_a^T from the row records (row-block partial
+        sums + split-K reduction), then + emb W_d^T + bias + mask block (the shared epilogue GEMM)."""
+        ring, R, P = self.sparse
+        H, A, c1 = self.H, self.A, c.width(0)
+        wa, st, S = self._wa(c, "c"), self._stream(), self.sp_splits
+        self.nat.sparse_fwd(ring.data_ptr(), rows.data_ptr(), self.B, R, P, wa.data_ptr(), wa.stride(0), c1,
+                            self.slabs.data_ptr(), S, st)
+        self.nat.splitk_reduce(self.slabs.data_ptr(), self.B * c1, S, self.B, c1, c1, self.hacc.data_ptr(),
+                               self.hacc.stride(0), 1.0, 0, st)
+        self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], acc_ready=True)
+
+    def _sparse_wgrad(self, c: _Net, dh0: torch.Tensor, rows: torch.Tensor) -> None:
+        """dW_a = dh0^T a from the row records: one workgroup per row block writes its [c1, n_pad] gradient."""
+        ring, R, P = self.sparse
+        H, A, c1 = self.H, self.A, c.width(0)
+        gw = c.gw(0)[:, H + A:]
+        self.nat.sparse_wgrad(ring.data_ptr(), rows.data_ptr(), self.B, R, P, dh0.data_ptr(), dh0.stride(0), c1,
+                              gw.data_ptr(), gw.stride(0), self._stream())
 
     def stage_actor_fwd(self, b) -> None:
         """Actor embedding + hidden layers on s (independent of the critic step: overlaps its all-reduce)."""

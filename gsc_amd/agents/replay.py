@@ -36,7 +36,10 @@ class DeviceReplay:
     ``seed`` (rank-specific) and the draw counter -- the same stream on the host path."""
 
     def __init__(self, capacity: int, n_pad: int, n_obs: int, action_dim: int, device,
-                 action_dtype=torch.float32, seed: int = 0, action_row_align: int = 1):
+                 action_dtype=torch.float32, seed: int = 0, action_row_align: int = 1, sparse_rows: int = 0):
+        """``sparse_rows`` = R > 0 (GPU): actions are stored as R row records of n_pad destinations each
+        (``csrc/ops/sparse_act.hip``: base value + <= 11 exceptions, exactly the bf16 row), ~8x smaller than
+        dense bf16 at 200-node topologies; ``actions`` is then the int32 [capacity, R, 12] record ring."""
         from gsc_amd.native import load as load_native
         self.nat = load_native()
         self.capacity = int(capacity)
@@ -52,7 +55,15 @@ class DeviceReplay:
         self.action_dim = int(action_dim)
         al = max(1, int(action_row_align))
         self.action_cols = -(-self.action_dim // al) * al
-        self.actions = torch.zeros((self.capacity, self.action_cols), dtype=action_dtype, device=dev)
+        self.sparse_rows = int(sparse_rows)
+        self.n_pad = int(n_pad)
+        if self.sparse_rows:
+            assert self.is_dev and self.sparse_rows * self.n_pad == self.action_dim, "sparse rows: R * n_pad == A"
+            self.actions = torch.zeros((self.capacity, self.sparse_rows, self.nat.SPARSE_ACT_WORDS), dtype=torch.int32,
+                                       device=dev)
+            self.sparse_bad = torch.zeros(1, dtype=torch.int32, device=dev)   # rows that did not compress
+        else:
+            self.actions = torch.zeros((self.capacity, self.action_cols), dtype=action_dtype, device=dev)
         self.rewards = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
         self.dones = torch.zeros(self.capacity, dtype=torch.float32, device=dev)
         self.state = torch.zeros(4, dtype=torch.int64, device=dev)   # pos, full, draws, -
@@ -86,7 +97,12 @@ class DeviceReplay:
                 (next_obs.data_ptr(), self.next_obs.data_ptr(), ob, 0, 0),
                 (topo.data_ptr(), self.topo.data_ptr(), 8, 0, 0), (rewards.data_ptr(), self.rewards.data_ptr(), 4, 0, 0)]
         A, Ap = self.action_dim, self.action_cols
-        if self.actions.dtype == torch.bfloat16 and actions.dtype == torch.float32:
+        if self.sparse_rows:
+            # compressed rows at the cursor, before the column insert advances it
+            a = actions.contiguous().float()
+            nat.sparse_compress(a.data_ptr(), a.stride(0), E, self.sparse_rows, self.n_pad, self.actions.data_ptr(), st,
+                                cap, self.sparse_bad.data_ptr(), s)
+        elif self.actions.dtype == torch.bfloat16 and actions.dtype == torch.float32:
             a = actions.contiguous()
             cols.append((a.data_ptr(), self.actions.data_ptr(), A, 1, Ap))
         else:
@@ -130,6 +146,8 @@ class DeviceReplay:
             out = self.empty_batch(B, actions=actions)
         nat, s, dev = self.nat, self._stream(), self.is_dev
         cols = []
+        if self.sparse_rows and actions:
+            raise ValueError("a sparse action ring is read in place (sample(actions=False))")
         for src, dst in zip((self.obs, self.topo, self.actions, self.rewards, self.next_obs, self.dones), out):
             if src is self.actions and not actions:
                 assert dst is self.actions
@@ -163,10 +181,23 @@ class DeviceReplay:
         self.state.copy_(t[:4].to(self.device))
         self.seed = int(t[4])
 
+    def check_sparse(self) -> None:
+        """Raise if a stored row did not fit the sparse record (not a post-processed action row)."""
+        if self.sparse_rows and int(self.sparse_bad.item()) > 0:
+            raise RuntimeError(f"{int(self.sparse_bad.item())} replayed action rows exceeded the sparse record's "
+                               "exceptions (post-processed rows hold <= 11); run with GSC_SPARSE_REPLAY=0")
+
+    def dense_actions(self, rows: torch.Tensor) -> torch.Tensor:
+        """bf16 [len(rows), A] actions of ring rows (sparse rings decompressed; tests and checkpoints)."""
+        if not self.sparse_rows:
+            return self.actions[rows.long(), :self.action_dim].to(torch.bfloat16)
+        return decompress_actions(self.actions[rows.long()], self.n_pad)
+
     def state_dict(self) -> dict:
         n = len(self)
+        acts = self.actions[:n].cpu() if self.sparse_rows else self.actions[:n, :self.action_dim].cpu()
         return {"pos": self.pos, "full": self.full, "obs": self.obs[:n].cpu(), "next_obs": self.next_obs[:n].cpu(),
-                "topo": self.topo[:n].cpu(), "actions": self.actions[:n, :self.action_dim].cpu(),
+                "topo": self.topo[:n].cpu(), "actions": acts,
                 "rewards": self.rewards[:n].cpu(),
                 "dones": self.dones[:n].cpu()}
 
@@ -174,10 +205,33 @@ class DeviceReplay:
         n = sd["obs"].shape[0]
         for k in ("obs", "next_obs", "topo", "rewards", "dones"):
             getattr(self, k)[:n].copy_(sd[k].to(self.device))
-        self.actions[:n, :self.action_dim].copy_(sd["actions"].to(self.device))
+        if self.sparse_rows:
+            if sd["actions"].dim() != 3:
+                raise ValueError("checkpoint holds dense replay actions; this ring stores sparse rows")
+            self.actions[:n].copy_(sd["actions"].to(self.device))
+        else:
+            self.actions[:n, :self.action_dim].copy_(sd["actions"].to(self.device))
         self.pos, self.full = int(sd["pos"]), bool(sd["full"])
         self.state[0] = self.pos
         self.state[1] = int(self.full)
+
+
+def decompress_actions(rec: torch.Tensor, n_pad: int) -> torch.Tensor:
+    """Dense bf16 [..., R * n_pad] actions from sparse row records [..., R, 12] (int32): every destination takes
+    the row's base value, listed exceptions their own (the reference for ``csrc/ops/sparse_act.hip``)."""
+    rec = rec.to(torch.int64) & 0xffffffff
+    head = rec[..., 0]
+    base = (head & 0xffff).to(torch.int32)
+    cnt = (head >> 16) & 0xffff
+    bits = base.unsqueeze(-1).expand(*base.shape, n_pad + 1).clone()   # column n_pad: sink of unused slots
+    slots = rec[..., 1:]
+    k = torch.arange(slots.shape[-1], device=rec.device)
+    valid = k < cnt.unsqueeze(-1)
+    idx = torch.where(valid, (slots & 0xffff).clamp(max=n_pad - 1), torch.full_like(slots, n_pad))
+    val = ((slots >> 16) & 0xffff).to(torch.int32)
+    bits.scatter_(-1, idx, val)
+    f = (bits[..., :n_pad].to(torch.int32) << 16).view(torch.float32)
+    return f.reshape(*f.shape[:-2], -1).to(torch.bfloat16)
 
 
 class GraphReplayBuffer:

@@ -60,9 +60,11 @@ def explore_postprocess_reference(mu: torch.Tensor, mask: torch.Tensor, n_pad: i
 
 def explore_postprocess(mu: torch.Tensor, mask: torch.Tensor, n_pad: int, warmup: bool, rand_mu: float,
                         rand_sigma: float, seed: int, step: int, threshold: float = 0.1, passes: int = 2,
-                        out: Optional[torch.Tensor] = None, topo: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        out: Optional[torch.Tensor] = None, topo: Optional[torch.Tensor] = None,
+                        pmask: Optional[tuple] = None) -> torch.Tensor:
     """mu [E, A] actor output -> post-processed actions [E, A] (float32).  ``mask``: [E, A] per-env
-    masks, or with ``topo`` [E] the per-topology table [T, A] (row ``topo[e]`` masks env e)."""
+    masks, or with ``topo`` [E] the per-topology table [T, A] (row ``topo[e]`` masks env e).  ``pmask``
+    (device, ``BatchedSimulator.pmask_target()``): also write the simulator's destination bitsets."""
     if mu.is_cuda:
         from gsc_amd.native import load
         nat = load()
@@ -78,7 +80,7 @@ def explore_postprocess(mu: torch.Tensor, mask: torch.Tensor, n_pad: int, warmup
         nat.explore_postprocess(mu.data_ptr(), mask.data_ptr(), topo.data_ptr() if topo is not None else 0,
                                 out.data_ptr(), E, A, n_pad, int(warmup), float(rand_mu), float(rand_sigma),
                                 int(seed) & 0xffffffff, int(step), float(threshold), int(passes),
-                                torch.cuda.current_stream(mu.device).cuda_stream)
+                                torch.cuda.current_stream(mu.device).cuda_stream, pmask)
         return out
     if topo is not None:
         mask = mask.index_select(0, topo.to(torch.int64))

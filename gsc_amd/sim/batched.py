@@ -281,9 +281,20 @@ class BatchedSimulator:
         then [E, 64, 2] handler cycles / dispatches per (process type, resume state)."""
         self.prof = torch.zeros(self.E * 4 + self.E * 128, dtype=torch.int64, device=self.device) if on else None
 
-    def step(self, actions: torch.Tensor, buffer_set: int = 0, obs_out: Optional[torch.Tensor] = None) -> SimStepOut:
+    def pmask_target(self) -> Optional[tuple]:
+        """(base, stride, C, F, Cd, Sd) for the exploration kernel to write the step kernel's destination bitsets
+        (topologies beyond 64 nodes with HBM-resident tables), or None when the kernel does not read them."""
+        lay = self.ctx.pmask_layout if self.is_device else None
+        if lay is None:
+            return None
+        off, Cd, Sd = lay
+        return (self.states.data_ptr() + int(off), self.state_bytes, self.C, self.F, int(Cd), int(Sd))
+
+    def step(self, actions: torch.Tensor, buffer_set: int = 0, obs_out: Optional[torch.Tensor] = None,
+             pmask_ready: bool = False) -> SimStepOut:
         """One lockstep step of every env.  ``obs_out``: write the next action's observations there
-        instead of the buffer set's own ``obs`` (the trainer's rotating observation buffers)."""
+        instead of the buffer set's own ``obs`` (the trainer's rotating observation buffers).  ``pmask_ready``:
+        the producer of ``actions`` already wrote the destination bitsets (``pmask_target``)."""
         if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
             actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
         if actions.dim() != 2 or actions.shape[0] != self.E or actions.shape[1] < self.action_dim:
@@ -298,7 +309,7 @@ class BatchedSimulator:
                       actions.shape[1], obs.data_ptr(), next_obs.data_ptr(), reward.data_ptr(),
                       done_u8.data_ptr(), stats.data_ptr(), ep_return.data_ptr(), self.E, self._stream(),
                       self.prof.data_ptr() if (self.prof is not None and self.is_device) else 0,
-                      self.topo_cur.data_ptr())
+                      self.topo_cur.data_ptr(), bool(pmask_ready))
         done = done_u8.view(torch.bool)  # 0/1 bytes: zero-copy
         return SimStepOut(obs, next_obs, reward, done, stats, ep_return)
 
