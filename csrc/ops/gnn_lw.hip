@@ -384,7 +384,7 @@ __device__ __forceinline__ void lw_store_row(float* dst, const float (&v)[HV], i
 // graph's x_l rows sit in LDS with a padded row stride HV (16-byte reads), the raw scores in an LDS
 // slot per message (each message has one target), and the next conv's node linears read W
 // broadcast from LDS.  Same arithmetic as lw_attn_fwd_kernel.
-template <int HV, bool MF = false>
+template <int HV>
 __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const float* __restrict__ xl,
                                                                const float* __restrict__ xr,
                                                                const float* __restrict__ att,
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
   const int b = blockIdx.x, t = g.topo[b];
   float* s_xl = lw_g;
   float* s_w = s_xl + P * HV;
-  float* s_sc = s_w + (nx.wl && !MF ? 2 * H * HV : 0);  // MF: no staged W (fragments from L2)
+  float* s_sc = s_w + (nx.wl ? 2 * H * HV : 0);
   float* s_deg = s_sc + M;
   int32_t* iptr = reinterpret_cast<int32_t*>(s_deg + P);
   int32_t* src = iptr + P + 1;
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
     const int r = k / HV, c = k - r * HV;
     s_xl[k] = c < H ? xl[base + (long)r * H + c] : 0.f;
   }
-  if (nx.wl && !MF) {
+  if (nx.wl) {
     for (int k = threadIdx.x; k < H * HV; k += 256) {
       const int r = k / HV, c = k - r * HV;
       s_w[k] = c < H ? nx.wl[r * H + c] : 0.f;
@@ -429,9 +429,9 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
   }
   const int n = g.nnodes[t];
   float* al = alpha + (long)b * M;
-  float ys[HV], ykeep[HV];
+  float ys[HV];
 #pragma unroll
-  for (int c = 0; c < HV; ++c) ys[c] = ykeep[c] = 0.f;
+  for (int c = 0; c < HV; ++c) ys[c] = 0.f;
   for (int i = threadIdx.x; i < P; i += 256) {
     const long node = (long)b * P + i;
     float y[HV];
@@ -486,10 +486,7 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
       for (int c = 0; c < HV; ++c) y[c] = 0.f;
     }
     lw_store_row<HV>(h_out + node * H, y, H);
-    if constexpr (MF) {  // P <= 256: this thread's only node -- its row feeds the MFMA epilogue below
-#pragma unroll
-      for (int c = 0; c < HV; ++c) ykeep[c] = y[c];
-    } else if (nx.wl) {  // x_l'[co] = b_l'[co] + W_l'[co] . y  (W rows broadcast from LDS)
+    if (nx.wl) {  // x_l'[co] = b_l'[co] + W_l'[co] . y  (W rows broadcast from LDS)
       float ol[HV], orr[HV];
 #pragma unroll
       for (int co = 0; co < HV; ++co) {
@@ -511,15 +508,6 @@ __global__ __launch_bounds__(256) void lw_lane_attn_fwd_kernel(LwGraph g, const 
       }
       lw_store_row<HV>(nx.xl + node * H, ol, H);
       lw_store_row<HV>(nx.xr + node * H, orr, H);
-    }
-  }
-  if constexpr (MF) {
-    if (nx.wl) {  // the next conv's node linears on the matrix cores
-      __syncthreads();  // every lane is done with the x_l rows: the bf16 image reuses their LDS
-      __bf16* s_y = reinterpret_cast<__bf16*>(s_xl);
-      if ((int)threadIdx.x < ((P + 31) & ~31)) lw_put_bf16_row<HV>(s_y, threadIdx.x, ykeep, H);
-      __syncthreads();
-      lw_mfma_rows<false>(s_y, nx.wl, nx.bl, nx.xl, nullptr, nx.wr, nx.br, nx.xr, P, H, (long)b * P);
     }
   }
   if (emb) {
@@ -779,208 +767,6 @@ __global__ __launch_bounds__(256, HV <= 24 ? 4 : 2) void lw_stage_attn_fwd_kerne
     __syncthreads();
     lw_mfma_rows<false>(s_y, nx.wl, nx.bl, nx.xl, nullptr, nx.wr, nx.br, nx.xr, P, H, (long)b * P);
   }
-}
-
-// One conv's parameters (device pointers into the flat embedder parameters)
-struct LwConvP {
-  const float *wl, *bl, *wr, *br, *att, *bias;
-};
-constexpr int kLwMaxConvs = 8;
-struct LwEmbedArgs {
-  LwConvP c[kLwMaxConvs];
-  int L;
-  const float* x;  // [B*P][Fi]
-  int Fi;
-  float* emb;      // [B][H]
-};
-
-// Whole embedding per graph in one workgroup (forwards without a backward: target / act / actor-loss
-// embedders at P <= 256, H <= 32, Fi <= 8): the graph's rows never leave LDS between convs -- per conv
-// the staged attention of lw_stage_attn_fwd_kernel, then the output rows as a bf16 image and the next
-// conv's node linears on the matrix cores straight into LDS (x_l rows in region A, x_r rows in region B
-// over the consumed image).  HBM traffic per graph: its input rows and topology in, the pooled embedding
-// out (the per-conv kernels moved ~1.8 GB of x_l / x_r rows per conv at B = 25,600).
-template <int HV>
-__global__ __launch_bounds__(256, HV <= 24 ? 3 : 2) void lw_embed_fwd_kernel(LwGraph g, LwEmbedArgs e) {
-  constexpr int RS = HV + 4;
-  __shared__ float red[4][HV];
-  extern __shared__ __attribute__((aligned(16))) float lw_g[];
-  const int H = g.H, P = g.P, M = g.M;
-  const int b = blockIdx.x, t = g.topo[b];
-  float* s_xl = lw_g;                  // region A: x_l rows [P][RS]
-  float* s_b = s_xl + P * RS;          // region B: bf16 image of the rows, then x_r rows [P][RS]
-  float* s_sc = s_b + P * RS;          // [M]
-  float* s_deg = s_sc + M;             // [P]
-  int32_t* iptr = reinterpret_cast<int32_t*>(s_deg + P);
-  int32_t* src = iptr + P + 1;
-  const int i = threadIdx.x, lane = i & 63, wave = i >> 6, r = lane & 31, hh = lane >> 5;
-  const int n = g.nnodes[t];
-  // ---- loads in flight together: the lane's input row, the topology
-  float xin[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) xin[k] = (i < P && k < e.Fi) ? e.x[((long)b * P + i) * e.Fi + k] : 0.f;
-  for (int k = i; k <= P; k += 256) {
-    iptr[k] = g.in_ptr[(long)t * (P + 1) + k];
-    if (k < P) s_deg[k] = g.deg[(long)t * P + k];
-  }
-  for (int k = i; k < M; k += 256) src[k] = g.in_src[(long)t * M + k];
-  float y[HV], xri[HV];
-  // ---- conv 0's node linears from the input row (uniform weights: scalar loads)
-  if (i < P) {
-#pragma unroll
-    for (int v = 0; v < HV / 4; ++v) {
-      float xl4[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = 4 * v + q;
-        float al = 0.f, ar = 0.f;
-        if (c < H) {
-          al = e.c[0].bl[c];
-          ar = e.c[0].br[c];
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if (k < e.Fi) {
-              al = fmaf(e.c[0].wl[c * e.Fi + k], xin[k], al);
-              ar = fmaf(e.c[0].wr[c * e.Fi + k], xin[k], ar);
-            }
-        }
-        xl4[q] = al;
-        xri[c] = ar;
-      }
-      reinterpret_cast<float4*>(s_xl + i * RS)[v] = make_float4(xl4[0], xl4[1], xl4[2], xl4[3]);
-    }
-  }
-  __syncthreads();
-  for (int l = 0; l < e.L; ++l) {
-    const LwConvP cp = e.c[l];
-    const bool relu = l + 1 < e.L || e.L == 1;
-    if (l > 0) {
-      // previous conv's rows -> bf16 image in region B, once every lane is done with the previous conv (its
-      // x_r row read out of region B, its x_l row gathers out of region A)
-      __syncthreads();
-      __bf16* img = reinterpret_cast<__bf16*>(s_b);
-      if (i < ((P + 31) & ~31)) lw_put_bf16_row<HV>(img, i, y, H);
-      __syncthreads();  // image complete
-      // x_l, x_r = rows W^T + b: up to two 32-row tiles per wave, results held until the image is consumed
-      bf16x8 fa[2], fb[2];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        fa[ks] = mf_wfrag(cp.wl, H, H, r, 16 * ks + 8 * hh, false);
-        fb[ks] = mf_wfrag(cp.wr, H, H, r, 16 * ks + 8 * hh, false);
-      }
-      const float bca = r < H ? cp.bl[r] : 0.f, bcb = r < H ? cp.br[r] : 0.f;
-      // x_l rows go straight to region A (free: the previous conv is done with it); x_r is held until
-      // every wave has read the image out of region B
-      f32x16 xb[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int tt = wave + 4 * u;
-        f32x16 xa;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          xa[q] = bca;
-          xb[u][q] = bcb;
-        }
-        if (32 * tt < P) {
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            const bf16x8 a = *reinterpret_cast<const bf16x8*>(img + (32 * tt + r) * kMfRS + 16 * ks + 8 * hh);
-            xa = mf_mma(a, fa[ks], xa);
-            xb[u] = mf_mma(a, fb[ks], xb[u]);
-          }
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int row = 32 * tt + mf_row(q, hh);
-            if (row < P && r < HV) s_xl[row * RS + r] = r < H ? xa[q] : 0.f;  // channels H..HV-1 read: zero
-          }
-        }
-      }
-      __syncthreads();  // every wave is done reading the image: region B takes the x_r rows
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int tt = wave + 4 * u;
-        if (32 * tt < P) {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int row = 32 * tt + mf_row(q, hh);
-            if (row < P && r < HV) s_b[row * RS + r] = r < H ? xb[u][q] : 0.f;
-          }
-        }
-      }
-      __syncthreads();
-      if (i < P) {
-        const float4* rr = reinterpret_cast<const float4*>(s_b + i * RS);
-#pragma unroll
-        for (int v = 0; v < HV / 4; ++v) {
-          const float4 f = rr[v];
-          xri[4 * v] = f.x;
-          xri[4 * v + 1] = f.y;
-          xri[4 * v + 2] = f.z;
-          xri[4 * v + 3] = f.w;
-        }
-      }
-    }
-    // ---- attention: lane = target node (as lw_stage_attn_fwd_kernel)
-    float acc[HV];
-#pragma unroll
-    for (int c = 0; c < HV; ++c) acc[c] = 0.f;
-    float scl = 0.f;
-    if (i < n) {
-      float a_[HV];
-#pragma unroll
-      for (int c = 0; c < HV; ++c) a_[c] = c < H ? cp.att[c] : 0.f;
-      const int q0 = iptr[i], q1 = iptr[i + 1];
-      float mx = -__builtin_inff(), den = 0.f;
-      for (int q = q0; q < q1; ++q) {
-        const float4* row = reinterpret_cast<const float4*>(s_xl + src[q] * RS);
-        float xj[HV];
-#pragma unroll
-        for (int v = 0; v < HV / 4; ++v) {
-          const float4 f = row[v];
-          xj[4 * v] = f.x;
-          xj[4 * v + 1] = f.y;
-          xj[4 * v + 2] = f.z;
-          xj[4 * v + 3] = f.w;
-        }
-        float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-        for (int c = 0; c < HV; ++c) {
-          const float z = xj[c] + xri[c];
-          s0 = fmaf(a_[c], z, s0);
-          s1 = fmaf(a_[c], fabsf(z), s1);
-        }
-        const float sc = 0.5f * (1.f + kLwSlope) * s0 + 0.5f * (1.f - kLwSlope) * s1;
-        if (sc > mx) {
-          const float rs = __expf(mx - sc);
-          den *= rs;
-#pragma unroll
-          for (int c = 0; c < HV; ++c) acc[c] *= rs;
-          mx = sc;
-        }
-        const float ex = __expf(sc - mx);
-        den += ex;
-#pragma unroll
-        for (int c = 0; c < HV; ++c) acc[c] = fmaf(ex, xj[c], acc[c]);
-      }
-      scl = 1.f / (den + 1e-16f) / s_deg[i];
-    }
-#pragma unroll
-    for (int c = 0; c < HV; ++c) {
-      float v = acc[c] * scl + (c < H ? cp.bias[c] : 0.f);
-      if (relu) v = v > 0.f ? v : 0.f;
-      y[c] = (c < H && i < n) ? v : 0.f;
-    }
-  }
-  // mean pool of the last conv: lane partial sums reduced in a fixed shuffle / wave order
-#pragma unroll
-  for (int c = 0; c < HV; ++c) {
-    float v = i < n ? y[c] : 0.f;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if (lane == 0) red[wave][c] = v;
-  }
-  __syncthreads();
-  if (i < H) e.emb[(long)b * H + i] = ((red[0][i] + red[1][i]) + (red[2][i] + red[3][i])) / (float)n;
 }
 
 // emb[b,:] = mean over the graph's real nodes of h[b,:,:]
@@ -2207,9 +1993,8 @@ void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
   }
   if (H <= 32) {  // lane per node
     const int hv = H <= 8 ? 8 : H <= 16 ? 16 : H <= 24 ? 24 : 32;
-    // MFMA node linears (no staged W) when the graph's rows fit the bf16 image (GSC_LW_MFMA=0: VALU)
+    // GSC_LW_MFMA=0: the lane kernels (VALU node linears) even where the staged kernel applies
     static const bool mf_env = getenv("GSC_LW_MFMA") == nullptr || atoi(getenv("GSC_LW_MFMA")) != 0;
-    const bool mf = mf_env && nx.wl && lw_mfma_fits(P, hv);
     // staged variant: both row blocks in LDS, coalesced output / alpha stores, MFMA linears
     const size_t lds_st = sizeof(float) * ((size_t)P * (hv + 4) + 2 * g.M + 2 * P + 1);
     if (mf_env && P <= 256 && hv >= 16 && (!nx.wl || lw_mfma_fits(P, hv + 4)) && lds_st <= 80 * 1024) {
@@ -2228,13 +2013,13 @@ void lw_attn_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t
       return;
     }
     materialise_first();
-    const size_t lds = sizeof(float) * ((size_t)P * hv + (nx.wl && !mf ? 2 * H * hv : 0) + 2 * g.M + 2 * P + 1);
+    // lane kernel: H < 16 channels, graphs whose rows do not tile the staged kernel's MFMA image (P % 32 != 0
+    // at H = 16), GSC_LW_MFMA=0, n_pad > 256
+    const size_t lds = sizeof(float) * ((size_t)P * hv + (nx.wl ? 2 * H * hv : 0) + 2 * g.M + 2 * P + 1);
     if (lds <= 64 * 1024) {
-      auto kl = mf ? (hv == 16 ? lw_lane_attn_fwd_kernel<16, true> : hv == 24 ? lw_lane_attn_fwd_kernel<24, true>
-                                                                    : lw_lane_attn_fwd_kernel<32, true>)
-                   : hv == 8 ? lw_lane_attn_fwd_kernel<8>
-                   : hv == 16 ? lw_lane_attn_fwd_kernel<16> : hv == 24 ? lw_lane_attn_fwd_kernel<24>
-                                                              : lw_lane_attn_fwd_kernel<32>;
+      auto kl = hv == 8 ? lw_lane_attn_fwd_kernel<8>
+                : hv == 16 ? lw_lane_attn_fwd_kernel<16> : hv == 24 ? lw_lane_attn_fwd_kernel<24>
+                                                           : lw_lane_attn_fwd_kernel<32>;
       hipLaunchKernelGGL(kl, dim3(B), dim3(256), lds, stream_of(stream), g, ptr<const float>(xl), ptr<const float>(xr),
                          ptr<const float>(att), ptr<const float>(bias), relu, ptr<float>(h_out), ptr<float>(alpha), nx,
                          ptr<float>(emb));
@@ -2371,41 +2156,6 @@ bool lw_attn_bwd_gather(py::dict tables, uintptr_t topo, int B, int P, int H, ui
   return false;
 }
 
-// The whole embedding of a forward without a backward in one launch; convs = ((wl, bl, wr, br, att, bias), ...)
-// returns False (nothing launched) when the shape is outside the kernel's range
-bool lw_embed_fwd(py::dict tables, uintptr_t topo, int B, int P, int H, uintptr_t x, int Fi, py::list convs,
-                  uintptr_t emb, uintptr_t stream) {
-  const LwGraph g = lw_graph(tables, topo, B, P, H);
-  const int L = (int)convs.size();
-  // off by default: measured slower than the per-conv kernels (config 5: 4.85k vs 5.05k env-steps/s, one
-  // embedding 2.12 vs 1.64 ms at 25,600 graphs) -- three graphs per CU and four barriers per conv serialise
-  // the phases that separate launches overlap across workgroups.  GSC_LW_EMBED=1 enables it.
-  static const bool on = getenv("GSC_LW_EMBED") != nullptr && atoi(getenv("GSC_LW_EMBED")) != 0;
-  const int hv = H <= 16 ? 16 : H <= 24 ? 24 : 32;
-  const size_t lds = sizeof(float) * (2 * (size_t)P * (hv + 4) + 2 * g.M + 2 * P + 1);
-  if (!on || H > 32 || P > 256 || Fi < 1 || Fi > 8 || L < 1 || L > kLwMaxConvs || lds > 80 * 1024 ||
-      !lw_mfma_fits(P, hv + 4))
-    return false;
-  LwEmbedArgs e{};
-  for (int l = 0; l < L; ++l) {
-    py::tuple c = convs[l].cast<py::tuple>();
-    e.c[l] = LwConvP{ptr<const float>(c[0].cast<uintptr_t>()), ptr<const float>(c[1].cast<uintptr_t>()),
-                     ptr<const float>(c[2].cast<uintptr_t>()), ptr<const float>(c[3].cast<uintptr_t>()),
-                     ptr<const float>(c[4].cast<uintptr_t>()), ptr<const float>(c[5].cast<uintptr_t>())};
-  }
-  e.L = L;
-  e.x = ptr<const float>(x);
-  e.Fi = Fi;
-  e.emb = ptr<float>(emb);
-  auto k = hv == 16 ? lw_embed_fwd_kernel<16> : hv == 24 ? lw_embed_fwd_kernel<24> : lw_embed_fwd_kernel<32>;
-  if (lds > 65536)
-    GSC_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds));
-  hipLaunchKernelGGL(k, dim3(B), dim3(256), lds, stream_of(stream), g, e);
-  check_launch();
-  return true;
-}
-
 void lw_relu_mask(uintptr_t dh, uintptr_t h, long n, uintptr_t stream) {
   hipLaunchKernelGGL(lw_relu_mask_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream_of(stream),
                      ptr<float>(dh), ptr<const float>(h), n);
@@ -2501,8 +2251,6 @@ void register_gnn_lw(py::module_& m) {
   m.def("lw_conv_grads_v", &lw_conv_grads_v, "layer-wise GATv2: conv parameter gradients, streamed (MFMA dW with "
         "a ones column for the bias sums), d att from per-graph sums");
   m.def("lw_colsum", &lw_colsum, "deterministic column sums (two phases)");
-  m.def("lw_embed_fwd", &lw_embed_fwd, "layer-wise GATv2: a whole embedding without a backward in one launch "
-        "(rows stay in LDS between convs); False when the shape is outside its range");
 }
 
 }  // namespace gsc

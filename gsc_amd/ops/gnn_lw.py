@@ -95,11 +95,6 @@ class LayerwiseGAT:
         assert topo32.dtype == torch.int32 and topo32.numel() == B
         nat, s, t = self.nat, self._stream(), self.tables
         self.x, self.topo32 = x, topo32
-        if not save:   # the whole embedding in one launch when the shape allows (rows stay in LDS)
-            convs = [self._params(flat, blk)[1:] for blk in self.layer_of]
-            ptrs = [tuple(p.data_ptr() for p in c) for c in convs]
-            if nat.lw_embed_fwd(t, topo32.data_ptr(), B, P, H, x.data_ptr(), self.Fin, ptrs, emb.data_ptr(), s):
-                return
         h = x.view(B * P, self.Fin)
         for l, blk in enumerate(self.layer_of):
             Fi, Wl, bl, Wr, br, att, bias = self._params(flat, blk)

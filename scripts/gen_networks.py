@@ -11,8 +11,8 @@ paths hard-coded).  Here as a CLI, plus what BASELINE configs (4) and (5) need:
   reads it like any shipped network;
 * ``trace`` — a ``time,node,inter_arrival_mean`` trace (reference format,
   ``configs/traces/*.csv``) with per-node random-walk rates for every ingress node;
-* ``suite`` — regenerate the shipped ``configs/networks/synthetic`` set (50-node + traces and
-  four 200-node variants for the scheduler-driven generalisation config).
+* ``suite`` — regenerate the shipped ``configs/networks/synthetic`` set (50-node + traces, three more
+  50-node variants and four 200-node variants for the scheduler-driven generalisation configs).
 
     python scripts/gen_networks.py caps IN OUT --min-cap 1 --max-cap 2 [--seed S]
     python scripts/gen_networks.py ingress IN OUT --node 3
@@ -109,6 +109,9 @@ def suite() -> None:
     n50 = os.path.join(out, "syn50-in8-cap1-3.graphml")
     nx.write_graphml(synthetic_topology(50, 8, degree=3, seed=50), n50)
     make_trace(n50, os.path.join(ROOT, "configs", "traces", "trace_syn50_in8.csv"), seed=50)
+    for s in range(1, 4):  # 50-node variants for the scheduler / held-out generalisation runs (scripts/generalize.py)
+        nx.write_graphml(synthetic_topology(50, 8, degree=3, seed=100 + s),
+                         os.path.join(out, f"syn50-in8-cap1-3-s{s}.graphml"))
     for s in range(4):
         nx.write_graphml(synthetic_topology(200, 16, degree=3, seed=200 + s, ms_per_unit=6.0),
                          os.path.join(out, f"syn200-in16-cap1-3-s{s}.graphml"))

@@ -105,9 +105,8 @@ def test_layerwise_200_nodes_wide_hidden_per_node_kernel():
 
 @pytest.mark.parametrize("layers,iters,hidden", [(2, 2, 22), (1, 1, 22), (3, 1, 16), (2, 2, 32)])
 def test_layerwise_forward_without_backward(layers, iters, hidden):
-    """No-grad forwards (target / act embedders): the per-conv kernels without stored rows / alpha, and the
-    whole-embedding kernel (lw_embed_fwd, opt-in: GSC_LW_EMBED=1, read once per process -- covered by the
-    GPU run of scripts/gpurun/r4_check13.sh); same tolerance as the saved path."""
+    """No-grad forwards (target / act embedders): the per-conv kernels without stored rows / alpha; same
+    tolerance as the saved path."""
     from gsc_amd.ops.gnn import gnn_embed_layerwise
     gs = GraphSet([load_topology(p) for p in SYN200], 200, DEV)
     torch.manual_seed(1)
