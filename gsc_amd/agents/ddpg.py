@@ -599,12 +599,10 @@ class BatchedTrainer:
         lds = max(int(sim.ctx.lds_per_env), 1)
         per_cu = max(1, min(4 if os.environ.get("GSC_SIM_CU_LAYOUT", "auto") != "contig" else 3, (160 * 1024) // lds))
         need = -(-sim.E // per_cu)
-        # Mid-size topologies (33..64 nodes: two envs per CU by LDS, the learner's two-tile GATv2 kernels
-        # need 52-81 KB of LDS and cannot share those CUs) are learner-bound: half a round's CUs, so the
-        # simulator runs two rounds while the learner keeps three quarters of the device.  Measured, 256
-        # syn50 envs (73 KB each): 64 CUs 16.4k env-steps/s, 128 CUs (one round) 13.5k, 96 13.3k, 32 13.8k.
-        if per_cu == 2 and max(t.n for t in sim.topologies) <= 64:
-            need = -(-need // 2)
+        # Mid-size topologies (33..64 nodes, two envs per CU by LDS) take one full round as well since round 5
+        # (profiles/syn50_partition.txt, 256 syn50 envs at HEAD: 64 CUs 23.2k env-steps/s, 80 23.4k, 96 23.8k,
+        # 128 24.0k, 160 23.5k, 192 22.9k).  In round 4, with a ~2x slower learner, half a round (64 CUs,
+        # two simulator rounds) was best (16.4k vs 13.5k at 128).
         k = xcd * -(-need // xcd)
         return int(min(max(k, xcd), n // 2))
 
