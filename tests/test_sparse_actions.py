@@ -59,3 +59,20 @@ def test_decompress_actions_reference():
     want[3], want[17] = 0.25, 0.75
     assert torch.equal(d[0, 1], want)
     assert torch.all(d[1, 2] == 0.5) and torch.all(d[1, :2] == 0)
+
+
+def test_sparse_fwd_splits_fill_whole_rounds():
+    """The forward's row-block split count: within [1, min(R, max, 64)], and ceil(B / 256) x S workgroups fill
+    at least 95 % of whole 256-CU rounds when such an S exists (B = 25,600: 100 row blocks -> S = 5, 500 of
+    512 slots)."""
+    from gsc_amd.agents.native_update import sparse_fwd_splits
+    assert sparse_fwd_splits(25600, 1800, 64) == 5
+    for B, R, mx in [(25600, 1800, 64), (8192, 1800, 64), (4096, 250, 16), (512, 3, 64), (300, 1, 8)]:
+        S = sparse_fwd_splits(B, R, mx)
+        assert 1 <= S <= max(1, min(R, mx, 64))
+        wgs = -(-B // 256) * S
+        rounds = -(-wgs // 256)
+        if rounds >= 2 and wgs / (rounds * 256) < 0.95:   # no S reaches 95 %: the best one is taken
+            best = max(-(-B // 256) * s / (max(2, -(-(-(-B // 256) * s) // 256)) * 256)
+                       for s in range(1, max(1, min(R, mx, 64)) + 1))
+            assert abs(wgs / (max(2, rounds) * 256) - best) < 1e-9
