@@ -6,8 +6,8 @@ The reference trains with the network scheduler swapping the training network be
 (``/root/reference/src/rlsp/envs/gym_env.py:103-128``) and tests the trained actor on an unseen
 ``inference_network`` (``/root/reference/main.py:61-76``).  Here:
 
-* train: ``BatchedTrainer`` on the preset's training topologies, every env switched to the next topology at
-  every episode end (scheduler period 1), bounded actor (``actor_output_activation: sigmoid``,
+* train: ``BatchedTrainer`` on the preset's training topologies, every env switched to the next topology every
+  ``period`` episodes (1 for syn50 / syn200, the reference's 10 for its scheduler_type presets), bounded actor (``actor_output_activation: sigmoid``,
   docs/DEVIATIONS.md Q6), ``--train-steps`` lockstep steps of ``--envs`` envs;
 * test: ``--eval-envs`` envs on the held-out topology, one episode each (``--eval-envs`` episodes), for three
   schedules post-processed exactly like the reference's actions (simple_ddpg.py:374-395):
@@ -36,6 +36,24 @@ PRESETS = {
                   test=f"{NET}/syn50-in8-cap1-3-s3.graphml", agent="configs/config/agent/agent_syn50.yaml",
                   service="configs/service_functions/abc-3sfc.yaml",
                   sim="configs/config/simulator/sample_config.yaml", episode_steps=50),
+    # the reference's own generalisation schedulers (configs/config/scheduler_type{1,2,4}.yaml): their training
+    # networks (period 10 episodes) and inference network, Abilene-scale (n_pad 24), abc service, 200-step episodes
+    "type1": dict(train=["configs/networks/abilene/abilene-in4-rand-cap0-2.graphml",
+                         "configs/networks/abilene/abilene-in4-cap1.graphml"],
+                  test="configs/networks/abilene/abilene-in4-rand-cap1-2.graphml",
+                  agent="configs/config/agent/sample_agent.yaml", service="configs/service_functions/abc.yaml",
+                  sim="configs/config/simulator/sample_config.yaml", episode_steps=200, period=10),
+    "type2": dict(train=["configs/networks/abilene/abilene-in4-rand-cap.graphml",
+                         "configs/networks/abilene/abilene-in4-rand-cap0-2.graphml"],
+                  test="configs/networks/abilene/abilene-in4-rand-cap1-2-perm1.graphml",
+                  agent="configs/config/agent/sample_agent.yaml", service="configs/service_functions/abc.yaml",
+                  sim="configs/config/simulator/sample_config.yaml", episode_steps=200, period=10),
+    "type4": dict(train=["configs/networks/Compuserve_n14_e17/Compuserve-in4-cap1.graphml",
+                         "configs/networks/node6/node6-in2-cap1-delay10.graphml",
+                         "configs/networks/Claranet_n15_e18/Claranet-in4-cap1.graphml"],
+                  test="configs/networks/abilene/abilene-in4-rand-cap1-2.graphml",
+                  agent="configs/config/agent/sample_agent.yaml", service="configs/service_functions/abc.yaml",
+                  sim="configs/config/simulator/sample_config.yaml", episode_steps=200, period=10),
     # 200-node: s0 / s1 for training (as bench config 5), s2 held out
     "syn200": dict(train=[f"{NET}/syn200-in16-cap1-3-s0.graphml", f"{NET}/syn200-in16-cap1-3-s1.graphml"],
                    test=f"{NET}/syn200-in16-cap1-3-s2.graphml", agent="configs/config/agent/agent_syn200.yaml",
@@ -126,7 +144,7 @@ def main():
     sim = load_batched_from_paths(pre["train"], pre["service"], pre["sim"], cfg, a.envs, device=dev, seed=a.seed)
     T = len(pre["train"])
     tr = BatchedTrainer(cfg, sim, TrainerConfig(num_envs=a.envs, seed=a.seed, check_every=0),
-                        network_schedule=list(range(T)), period=1)
+                        network_schedule=list(range(T)), period=int(pre.get("period", 1)))
     t0 = time.time()
     curve = []
     uni = []
