@@ -439,6 +439,24 @@ class TrainerConfig:
                                             # hop; the learner waits for the act (it reads the actor weights)
 
 
+def replay_plan(cap: int, n_pad: int, n_obs: int, action_dim: int, action_bytes: int, hbm: float, eligible: bool,
+                mode: str = "auto"):
+    """(sparse, bytes per transition, byte budget) of the replay ring for ``cap`` requested transitions.
+
+    Dense rows take ``action_bytes`` per action entry within 60 % of HBM; sparse row records (48 B per n_pad-wide
+    destination row, ``csrc/ops/sparse_act.hip``) within 65 % (syn200: 2M x 91 KB = 182 GB of 288 GB; the learner
+    needs < 40 GB).  ``mode`` auto: sparse only when ``eligible`` (native GPU learner, n_pad <= 240, critic
+    first layer 64 wide) and the dense ring cannot hold ``cap`` transitions; "1" forces sparse where eligible,
+    "0" dense.  Without HBM (CPU) the budget is 4 GB, dense."""
+    obs_bytes = 4 * (2 * n_pad * n_obs + 4)
+    dense_per = obs_bytes + action_bytes * action_dim
+    sparse_per = obs_bytes + 48 * (action_dim // n_pad)
+    if hbm <= 0:
+        return False, dense_per, 4e9
+    sparse = bool(eligible and mode != "0" and (mode == "1" or cap * dense_per > 0.6 * hbm))
+    return (True, sparse_per, 0.65 * hbm) if sparse else (False, dense_per, 0.6 * hbm)
+
+
 class BatchedTrainer:
     """E lockstep environments on the device simulator + DDPG learner (one process per GPU)."""
 
@@ -462,21 +480,13 @@ class BatchedTrainer:
         # 2M x 720 KB; config 4's 2M x 45 KB fits dense, whose GEMMs are faster at small A); 1 forces it where
         # the native kernels apply (n_pad <= 240, critic first layer 64 wide), 0 disables it.
         R_rows = sim.action_dim // sim.n_pad
-        obs_bytes = 4 * (2 * sim.n_pad * sim.n_obs + 4)
-        dense_per = obs_bytes + torch.empty((), dtype=adt).element_size() * sim.action_dim
-        sparse_per = obs_bytes + 48 * R_rows
         hbm = torch.cuda.get_device_properties(self.device).total_memory if self.device.type == "cuda" else 0
-        mode = os.environ.get("GSC_SPARSE_REPLAY", "auto")
         eligible = bool(self.learner.native_ok and self.device.type == "cuda" and sim.n_pad <= 240
-                        and self.learner.critic.mlp.layers[0].weight.shape[0] == 64 and mode != "0")
-        self.sparse_replay = eligible and (mode == "1" or cap * dense_per > 0.6 * hbm)
-        if self.sparse_replay:
-            per, frac = sparse_per, 0.65  # syn200: 2M x 91 KB = 182 GB of 288 GB; the learner needs < 40 GB
-        else:
-            per, frac = dense_per, 0.6
-        # byte budget of the ring (the dense [A]-wide rows of large action spaces bound its size)
-        budget = tcfg.replay_bytes_max or (frac * torch.cuda.get_device_properties(self.device).total_memory
-                                           if self.device.type == "cuda" else 4e9)
+                        and self.learner.critic.mlp.layers[0].weight.shape[0] == 64)
+        self.sparse_replay, per, budget = replay_plan(
+            cap, sim.n_pad, sim.n_obs, sim.action_dim, torch.empty((), dtype=adt).element_size(), hbm, eligible,
+            os.environ.get("GSC_SPARSE_REPLAY", "auto"))
+        budget = tcfg.replay_bytes_max or budget
         cap = int(min(cap, budget // per))
         # on the GPU actions are stored in bf16: the critic consumes them as bf16 GEMM operands
         # (bf16 rows padded to 8 columns: 16-byte aligned operand rows for the native learner's GEMMs)

@@ -76,3 +76,21 @@ def test_sparse_fwd_splits_fill_whole_rounds():
             best = max(-(-B // 256) * s / (max(2, -(-(-(-B // 256) * s) // 256)) * 256)
                        for s in range(1, max(1, min(R, mx, 64)) + 1))
             assert abs(wgs / (max(2, rounds) * 256) - best) < 1e-9
+
+
+def test_replay_plan_per_config():
+    """Ring representation and capacity of the three headline configs on a 288 GB MI355X (E = 256 envs,
+    mem_limit 10,000 -> 2M requested): Abilene and syn50 dense at full capacity, syn200 sparse at full capacity
+    (the dense ring would hold ~107k); forcing and disabling; no HBM -> dense within 4 GB."""
+    from gsc_amd.agents.ddpg import replay_plan
+    hbm = 288e9
+    cases = {"abilene": (24, 3, 24 * 3 * 24), "syn50": (50, 3, 50 * 9 * 50), "syn200": (200, 3, 200 * 9 * 200)}
+    for name, (P, F, A) in cases.items():
+        sparse, per, budget = replay_plan(2_000_000, P, F, A, 2, hbm, True)
+        assert sparse == (name == "syn200"), name
+        assert min(2_000_000, budget // per) == 2_000_000, name
+    sparse, per, budget = replay_plan(2_000_000, 200, 3, 360_000, 2, hbm, True, mode="0")
+    assert not sparse and budget // per < 250_000   # dense syn200 rows: ~238k transitions in 60 % of HBM
+    assert replay_plan(2_000_000, 24, 3, 1728, 2, hbm, True, mode="1")[0]
+    assert not replay_plan(2_000_000, 200, 3, 360_000, 2, hbm, False, mode="1")[0]
+    assert replay_plan(2_000_000, 200, 3, 360_000, 2, 0, True)[0] is False
