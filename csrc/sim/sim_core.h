@@ -1238,13 +1238,12 @@ GSC_HD_CALL void env_init(Env& S, const SimConst& K, const TopoDev& T, int topo,
                           int l0 = 0, int ls = 1) {
   Header* h = S.h;
   const int N = S.d.N, Sd = S.d.S, C = S.d.C, n = T.n;
-  const double ewma = S.st->ewma_flows, ep_ret = S.st->episode_return;
+  const double ewma = S.st->ewma_flows;
   lanes_sync(ls);  // every lane has read the values kept across the reset
   *h = Header{};
   if (l0 == 0) {
-    *S.st = Stats{};
+    *S.st = Stats{};  // episode_return restarts at 0 (gym's per-episode return, simple_ddpg.py:254)
     S.st->ewma_flows = episode <= 1 ? 1.0 : ewma;
-    S.st->episode_return = ep_ret;
   }
   lanes_sync(ls);
   h->topo = topo;

@@ -78,12 +78,19 @@ def test_episode_reset_and_done():
     am = sim.action_mask().view(24, 1, 3, 24)
     u = (am / 3.0).reshape(-1)
     a[:] = u
-    dones = []
+    dones, rets, run = [], [], torch.zeros(3, dtype=torch.float64)
     for _ in range(11):
         out = sim.step(a)
         dones.append(bool(out.done[0]))
+        run += out.reward.double()
+        if out.done[0]:
+            # the finished episode's return is that episode's reward sum, not a running total
+            assert torch.allclose(out.ep_return.double(), run, atol=1e-4), (out.ep_return, run)
+            rets.append(run.clone())
+            run.zero_()
     assert dones == [False] * 4 + [True] + [False] * 4 + [True] + [False]
     assert out.stats[0, 6] > 0
+    assert len(rets) == 2
 
 
 @pytest.mark.parametrize("simcfg", ["rand-arrival10_det-size001_duration100", "rand-mmp-arrival12-8_det-size001_dur100",
