@@ -7,7 +7,11 @@
 // shape.  The two
 // threshold/normalise passes run in fp64 (cross-lane sums; the reference sums Python floats left to
 // right, so results agree to float32 rounding) with the residual of the rounded sum added to the
-// first weight that can absorb it, found by a ballot.
+// first weight that can absorb it, found by a ballot.  Above 32 destinations most rows skip them: when
+// the second pass provably zeroes the whole row (FastExit), the kernel writes the uniform row directly.
+// At 200 nodes x 256 envs (92M weights): 565 -> 255 us noisy, 441 -> 169 us warm-up, against a 137 us
+// copy of the same bytes (profiles/explore_r5.txt); the remaining time is VALU issue (Philox-10 +
+// Box-Muller per weight quad).
 #include <pybind11/pybind11.h>
 
 #include "../common.h"
@@ -25,8 +29,33 @@ __device__ __forceinline__ double round10(double x) { return rint(x * 1e10) * 1e
 // its four uniforms -> warm-up: the uniforms; else two fp32 Box-Muller pairs (v0, v1) -> weights 0, 1 and
 // (v2, v3) -> weights 2, 3.  The value of a weight depends only on (seed, step, flat index).
 struct Quad { float x[4]; };
-__device__ __forceinline__ Quad explore_quad(uint64_t f4, int warmup, uint32_t seed, uint32_t step) {
-  const Philox4 r = philox4x32_10(seed, step, f4);
+
+// Philox4x32-10 round keys of (seed, step) computed once on the host: the wave kernel reads them from its
+// arguments instead of bumping the key pair in every draw (20 scalar adds per wave).  Same bits as philox4x32_10.
+struct RoundKeys {
+  uint32_t k0[10], k1[10];
+};
+static RoundKeys round_keys(uint32_t k0, uint32_t k1) {
+  RoundKeys rk;
+  for (int r = 0; r < 10; ++r) {
+    rk.k0[r] = k0;
+    rk.k1[r] = k1;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return rk;
+}
+__device__ __forceinline__ Philox4 philox_keyed(const RoundKeys& K, uint64_t ctr) {
+  uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0x9E3779B9u, c3 = 0x243F6A88u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) philox_round(c0, c1, c2, c3, K.k0[r], K.k1[r]);
+  Philox4 o;
+  o.v[0] = c0; o.v[1] = c1; o.v[2] = c2; o.v[3] = c3;
+  return o;
+}
+
+__device__ __forceinline__ Quad explore_quad(uint64_t f4, int warmup, const RoundKeys& rk) {
+  const Philox4 r = philox_keyed(rk, f4);
   Quad q;
 #pragma unroll
   for (int j = 0; j < 4; ++j) q.x[j] = (float)(r.v[j] >> 8) * (1.0f / 16777216.0f);  // [0, 1)
@@ -122,6 +151,18 @@ __device__ __forceinline__ double wave_sum(double v) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63), __builtin_amdgcn_readlane(__double2loint(v), 63));
 }
 
+// Max over the wave of non-negative floats (lanes outside a DPP source read 0), same shift tree as wave_sum;
+// compared as signed integers (order-preserving for non-negative floats, -0 counts as below 0), which folds
+// the DPP into the max
+__device__ __forceinline__ float wave_max_nonneg(float f) {
+  int v = __float_as_int(f);
+#define GSC_DPP_MAXI(ctrl, rm) v = max(v, __builtin_amdgcn_update_dpp(0, v, ctrl, rm, 0xF, false));
+  GSC_DPP_MAXI(0x111, 0xF) GSC_DPP_MAXI(0x112, 0xF) GSC_DPP_MAXI(0x114, 0xF) GSC_DPP_MAXI(0x118, 0xF)
+  GSC_DPP_MAXI(0x142, 0xA) GSC_DPP_MAXI(0x143, 0xC)
+#undef GSC_DPP_MAXI
+  return __int_as_float(max(__builtin_amdgcn_readlane(v, 63), 0));
+}
+
 // 32 < n_pad <= 256: one slice per wave, K <= 4 consecutive weights per lane (lane l holds weights
 // K l .. K l + K - 1, so "the first weight that can absorb the residual" is the first lane of a
 // ballot, then the first of its K).
@@ -133,50 +174,89 @@ struct PMask {
   char* base;
   long stride;
   int C, F, Cd, Sd;
+  int ident;  // C == Cd and F == Sd: the bitset of action row r sits at 32 r bytes (no index split)
 };
 
+// Host-side constants of the early uniform exit (passes == 2, thr > 0): the rows whose second pass zeroes
+// every weight -- at n_pad 50-200 nearly all of them (profiles/learning_curves.md, round 5) -- get the
+// reference's all-zero answer, the uniform row, without the fp64 passes.  Pass 1's output is w / s rounded
+// to 10 decimals plus a residual below 2e-8, so its largest entry is below thr - 1e-7 whenever the largest
+// thresholded w is below (thr - 2e-7) s; the test runs on an fp32 sum of the same thresholded weights, with
+// a 2^-11 relative margin that covers the fp32 sum's error (< 2e-5 for 256 terms).  Rows near the margin take
+// the general fp64 loop.
+struct FastExit {
+  int on;         // passes == 2 and thr > 0
+  float thr_f;    // smallest float f with (double) f >= thr: the fp32 threshold test selects the fp64 one's set
+  double bound;   // (thr - 2e-7) (1 - 2^-11)
+  int zero_ok;    // round10(1 / P) + 1e-7 < thr: an all-zero pass 1 (uniform row) is also zeroed by pass 2
+  float uni, uni0;  // the uniform row: (float) round10(1 / P) and weight 0 with the residual
+                    // 1 - (left-to-right sum of P copies), as normalize_scheduling_probabilities adds it
+};
+
+// Sum / max over the wave in fp32 (DPP folded into the add / max), same shift tree as wave_sum
+__device__ __forceinline__ float wave_sum_f32(float v) {
+#define GSC_DPP_ADDF(ctrl, rm) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, rm, 0xF, false));
+  GSC_DPP_ADDF(0x111, 0xF) GSC_DPP_ADDF(0x112, 0xF) GSC_DPP_ADDF(0x114, 0xF) GSC_DPP_ADDF(0x118, 0xF)
+  GSC_DPP_ADDF(0x142, 0xA) GSC_DPP_ADDF(0x143, 0xC)
+#undef GSC_DPP_ADDF
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// Lane's K raw noisy weights of one slice (undefined at and beyond P) from its K inputs v (mu, or the mask row in
+// warm-up): flat indices f0 .. f0 + K - 1, within one or two Philox quads (one when vec: K = 4, 4-aligned rows)
 template <int K>
-__global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const float* __restrict__ mu,
-                                                                      const float* __restrict__ mask,
-                                                                      const long long* __restrict__ topo,
-                                                                      float* __restrict__ out, int E, int A, int P,
-                                                                      int warmup, float rand_mu, float rand_sigma,
-                                                                      uint32_t seed, uint32_t step, double thr,
-                                                                      int passes, PMask pm) {
-  const int R = A / P;
-  const long slice = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (slice >= (long)E * R) return;  // whole waves exit together
-  const long base = slice * P;
-  const float* mrow = topo ? mask + topo[slice / R] * (long)A + (slice % R) * P : mask + base;
-  // lane's weights: flat indices f0 .. f0 + K - 1, within one or two Philox quads
-  double w[K];
-  {
-    const int i0 = K * lane;
-    const uint64_t f0 = (uint64_t)(base + i0);
-    const bool any = i0 < P;
-    Quad qa{}, qb{};
-    if (any) {
-      qa = explore_quad(f0 & ~3ull, warmup, seed, step);
-      const uint64_t fl = f0 + K - 1;
-      if ((fl >> 2) != (f0 >> 2) && i0 + (int)(((f0 & ~3ull) + 4) - f0) < P)
-        qb = explore_quad(fl & ~3ull, warmup, seed, step);
-    }
+__device__ __forceinline__ void explore_raw(float (&wf)[K], const float (&v)[K], long base, int i0, int P, bool vec,
+                                            int warmup, float rand_mu, float rand_sigma, const RoundKeys& rk) {
+  const uint64_t f0 = (uint64_t)(base + i0);
+  const Quad qa = explore_quad(f0 & ~3ull, warmup, rk);  // lanes past P compute it too (no branch)
+  Quad qb{};
+  if (!vec) {
+    const uint64_t fl = f0 + K - 1;
+    if ((fl >> 2) != (f0 >> 2) && i0 + (int)(((f0 & ~3ull) + 4) - f0) < P) qb = explore_quad(fl & ~3ull, warmup, rk);
+  }
+  float z[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int i = i0 + k;
-      const int j = (int)((f0 & 3) + k);  // 0..6: quad a below 4, quad b from 4
-      float z = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const int j = (int)((f0 & 3) + k);  // 0..6: quad a below 4, quad b from 4
+    z[k] = 0.f;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (j == t) z = qa.x[t];
-        if (j == t + 4) z = qb.x[t];
-      }
-      w[k] = i < P ? (double)explore_apply(z, warmup ? 0.f : mu[base + i], warmup ? mrow[i] : 0.f, warmup, rand_mu,
-                                           rand_sigma)
-                   : 0.0;
+    for (int t = 0; t < 4; ++t) {
+      if (j == t) z[k] = qa.x[t];
+      if (j == t + 4) z[k] = qb.x[t];
     }
   }
+  // one wave-uniform branch on warmup around the whole loop; weights past P are computed from the clamped
+  // inputs and left in place (every consumer tests i < P), so there is no per-weight exec branch
+  if (warmup) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) wf[k] = explore_apply(z[k], 0.f, v[k], 1, rand_mu, rand_sigma);
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) wf[k] = explore_apply(z[k], v[k], 0.f, 0, rand_mu, rand_sigma);
+  }
+}
+
+// Bitset word offset (in u64) of action row `row` in the simulator's pmask block of env `env`
+__device__ __forceinline__ uint64_t* pmask_dst(const PMask& pm, int env, int row) {
+  long prow = row;
+  if (!pm.ident) {
+    const int sf = row % pm.F, c = (row / pm.F) % pm.C, sn = row / (pm.F * pm.C);
+    prow = (long)(sn * pm.Cd + c) * pm.Sd + sf;
+  }
+  return reinterpret_cast<uint64_t*>(pm.base + env * pm.stride) + 4L * prow;
+}
+
+// General path of one slice: the reference's two fp64 threshold / normalise passes on the raw weights wf, the
+// store, and the bitset from the final weights (rows the early exit does not decide; out of line, rare at
+// 50-200 nodes)
+template <int K>
+__device__ __forceinline__ void explore_general(const float* __restrict__ mrow, float* __restrict__ out, long base,
+                                             int P, int env, int row, int lane, double thr, int passes, PMask pm,
+                                             float wf0, float wf1, float wf2, float wf3) {
+  const float wf[4] = {wf0, wf1, wf2, wf3};
+  double w[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) w[k] = (double)wf[k];
   const double acc = 1.4901161193847656e-08;  // sqrt(float64 eps)
   const double uni = round10(1.0 / P);
   for (int pass = 0; pass < passes; ++pass) {
@@ -236,11 +316,119 @@ __global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const flo
       const uint64_t wq = (uint64_t)__ballot(d < P && ((b >> (l & 63)) & 1ull) && l < 64);
       if (lane == q) word = wq;
     }
-    const int row = (int)(slice % R);
-    const int sf = row % pm.F, c = (row / pm.F) % pm.C, src = row / (pm.F * pm.C);
-    uint64_t* dst = reinterpret_cast<uint64_t*>(pm.base + (slice / R) * pm.stride) + 4L * ((src * pm.Cd + c) * pm.Sd + sf);
+    uint64_t* dst = pmask_dst(pm, env, row);
     if (lane < 4) dst[lane] = word;
   }
+}
+
+// S slices per wave (rows row0 .. row0 + S - 1 of env blockIdx.y), four waves per block: every input load of
+// the S slices is issued up front (mu or mask row, and the mask words of the bitsets), the S Philox / reduction
+// chains are independent (latency of one overlaps the other's), then each slice takes the early uniform exit or
+// the general path.  env and rows come from the block index (scalar), no division.
+template <int K, int S, bool VEC>
+__global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const float* __restrict__ mu,
+                                                                      const float* __restrict__ mask,
+                                                                      const long long* __restrict__ topo,
+                                                                      float* __restrict__ out, int E, int A, int P,
+                                                                      int warmup, float rand_mu, float rand_sigma,
+                                                                      uint32_t seed, uint32_t step, double thr,
+                                                                      int passes, PMask pm, FastExit fx,
+                                                                      RoundKeys rk) {
+  const int R = A / P;
+  const int row0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 * S + (threadIdx.x >> 6) * S));
+  if (row0 >= R) return;  // whole waves exit together
+  const int env = blockIdx.y, lane = threadIdx.x & 63, i0 = K * lane;
+  constexpr bool vec = VEC;  // K = 4, 4-aligned rows, 16-byte aligned buffers: one 16-byte load / store per lane
+  const float* mtab = topo ? mask + topo[env] * (long)A : mask + (long)env * A;  // [R, P] mask rows of this env
+  float v[S][K], pmv[S][4], wf[S][K];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int row = min(row0 + s, R - 1);
+    const long base = ((long)env * R + row) * P;
+    const float* mrow = mtab + (long)row * P;
+    const float* src = warmup ? mrow : mu + base;
+    // loads from clamped (in-bounds) addresses, no exec-mask branch around them, and no use before the Philox
+    // rounds (explore_raw zeroes the weights past P), so nothing waits for them early
+    if (pm.base) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pmv[s][q] = mrow[min(64 * q + lane, P - 1)];
+    }
+    if constexpr (VEC) {
+      const float4 t = *reinterpret_cast<const float4*>(src + min(i0, P - 4));
+      v[s][0] = t.x; v[s][K > 1 ? 1 : 0] = t.y; v[s][K > 2 ? 2 : 0] = t.z; v[s][K > 3 ? 3 : 0] = t.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) v[s][k] = src[min(i0 + k, P - 1)];
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const long base = ((long)env * R + min(row0 + s, R - 1)) * P;
+    explore_raw<K>(wf[s], v[s], base, i0, P, vec, warmup, rand_mu, rand_sigma, rk);
+  }
+  bool fast[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    fast[s] = false;
+    if (fx.on) {
+      float ps = 0.f, mx = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const bool keep = (i0 + k < P) & (wf[s][k] >= fx.thr_f);  // non-short-circuit: a select, not a branch
+        const float t = keep ? wf[s][k] : 0.f;
+        ps += t;
+        mx = fmaxf(mx, t);
+      }
+      const float sum = wave_sum_f32(ps), M = wave_max_nonneg(mx);
+      fast[s] = sum == 0.f ? fx.zero_ok != 0 : (double)M < fx.bound * (double)sum;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int row = row0 + s;
+    if (row >= R) break;
+    const long base = ((long)env * R + row) * P;
+    if (fast[s]) {
+      if (vec) {
+        if (i0 < P) *reinterpret_cast<float4*>(out + base + i0) = float4{lane == 0 ? fx.uni0 : fx.uni, fx.uni, fx.uni, fx.uni};
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (i0 + k < P) out[base + i0 + k] = lane == 0 && k == 0 ? fx.uni0 : fx.uni;
+      }
+      if (pm.base) {  // every weight is positive: the bitset is the topology's real destinations
+        uint64_t word = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint64_t b = (uint64_t)__ballot(64 * q + lane < P && pmv[s][q] > 0.f);
+          if (lane == q) word = b;
+        }
+        if (lane < 4) pmask_dst(pm, env, row)[lane] = word;
+      }
+    } else {
+      explore_general<K>(mtab + (long)row * P, out, base, P, env, row, lane, thr, passes, pm, wf[s][0],
+                         wf[s][K > 1 ? 1 : 0], wf[s][K > 2 ? 2 : 0], wf[s][K > 3 ? 3 : 0]);
+    }
+  }
+}
+
+// Host constants of the early uniform exit (see FastExit)
+static FastExit fast_exit(int P, double thr, int passes) {
+  FastExit fx{};
+  fx.on = passes == 2 && thr > 0.0;
+  float f = (float)thr;
+  if ((double)f < thr) f = nextafterf(f, INFINITY);
+  while ((double)nextafterf(f, -INFINITY) >= thr) f = nextafterf(f, -INFINITY);
+  fx.thr_f = f;
+  fx.bound = (thr - 2e-7) * (1.0 - 1.0 / 2048.0);
+  const double uni = std::nearbyint((1.0 / P) * 1e10) * 1e-10;  // round10, as on the device
+  double sum = 0.0;
+  for (int i = 0; i < P; ++i) sum += uni;  // left to right, as Python's sum()
+  const double r = 1.0 - sum;
+  fx.zero_ok = uni + 1e-7 < thr;
+  fx.uni = (float)uni;
+  fx.uni0 = (float)(uni + r);  // weight 0 absorbs the residual (uni + r >= 0)
+  return fx;
 }
 
 void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t out, int E, int A, int P, int warmup, float rand_mu,
@@ -248,7 +436,7 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t
                          py::object pmask) {
   GSC_CHECK(A % P == 0, "action dim must be a multiple of n_pad");
   GSC_CHECK(P <= 256, "n_pad > 256 not supported by the exploration kernel");
-  PMask pm{nullptr, 0, 1, 1, 1, 1};
+  PMask pm{nullptr, 0, 1, 1, 1, 1, 1};
   if (!pmask.is_none()) {  // (base, stride, C, F, Cd, Sd)
     py::tuple t = pmask.cast<py::tuple>();
     pm.base = ptr<char>(t[0].cast<uintptr_t>());
@@ -259,24 +447,32 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t
     pm.Sd = t[5].cast<int>();
     GSC_CHECK(P > 32 && (long)P * P * pm.C * pm.F == A && pm.C <= pm.Cd && pm.F <= pm.Sd,
               "explore pmask hand-off: n_pad > 32 and A = n_pad^2 C F within the simulator dims");
+    pm.ident = pm.C == pm.Cd && pm.F == pm.Sd;
   }
   const long slices = (long)E * (A / P);
+  GSC_CHECK(slices < (1L << 31) - 4, "exploration: E * A / n_pad must fit in int32");
   if (P <= 32) {
     const int sl_per_block = 8;
     hipLaunchKernelGGL(explore_postprocess_lanes_kernel, dim3((int)((slices + sl_per_block - 1) / sl_per_block)), dim3(256), 0,
                        stream_of(stream), ptr<const float>(mu), ptr<const float>(mask), ptr<const long long>(topo),
                        ptr<float>(out), E, A, P, warmup, rand_mu, rand_sigma, seed, step, thr, passes);
   } else {
-    const int grid = (int)((slices + 3) / 4);  // four slices (waves) per block
+    GSC_CHECK(E < 65536, "exploration: at most 65535 envs per launch");
+    const FastExit fx = fast_exit(P, thr, passes);
+    const RoundKeys rk = round_keys(seed, step);
+    constexpr int S = 1;  // slices per wave (2 measured slower at 200 nodes: 278 vs 255 us, profiles/explore_r5.txt)
+    const dim3 grid((unsigned)((A / P + 4 * S - 1) / (4 * S)), (unsigned)E);  // four waves per block
     auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, stream_of(stream), ptr<const float>(mu), ptr<const float>(mask),
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream_of(stream), ptr<const float>(mu), ptr<const float>(mask),
                          ptr<const long long>(topo), ptr<float>(out), E, A, P, warmup, rand_mu, rand_sigma, seed, step, thr,
-                         passes, pm);
+                         passes, pm, fx, rk);
     };
-    if (P <= 64) go(explore_postprocess_wave_kernel<1>);
-    else if (P <= 128) go(explore_postprocess_wave_kernel<2>);
-    else if (P <= 192 && P % 2 == 1) go(explore_postprocess_wave_kernel<3>);
-    else go(explore_postprocess_wave_kernel<4>);
+    const bool vec = P % 4 == 0 && mu % 16 == 0 && mask % 16 == 0 && out % 16 == 0;
+    if (P <= 64) go(explore_postprocess_wave_kernel<1, S, false>);
+    else if (P <= 128) go(explore_postprocess_wave_kernel<2, S, false>);
+    else if (P <= 192 && P % 2 == 1) go(explore_postprocess_wave_kernel<3, S, false>);
+    else if (vec) go(explore_postprocess_wave_kernel<4, S, true>);
+    else go(explore_postprocess_wave_kernel<4, S, false>);
   }
   check_launch();
 }

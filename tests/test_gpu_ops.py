@@ -211,6 +211,32 @@ def test_explore_noise_independent_of_slice_shape():
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("P,n", [(50, 50), (200, 200), (200, 131), (64, 7)])
+def test_explore_noisy_rows_match_reference_postprocess(P, n):
+    """Noisy rows against the reference post-processing (fp64, simple_ddpg.py:338-395) of the same raw noisy
+    weights (the passes=0 output).  mu mixes flat rows (pass 2 zeroes them: the kernel's early uniform exit)
+    with one-hot rows (a weight stays >= 0.1 through pass 2: the general loop), so both paths are compared
+    (noise sigma 0.1: at 0.3 the noise alone spreads a one-hot row at 200 destinations below the threshold)."""
+    torch.manual_seed(4)
+    E, A = 8, P * 3 * P
+    mask = torch.zeros(E, P, 3, P, device=DEV)
+    mask[:, :n, :, :n] = 1
+    mask = mask.view(E, A)
+    mu = (torch.rand(E, A // P, P, device=DEV) * 0.6).view(E, A)
+    hot = torch.zeros(E, A // P, P, device=DEV)
+    hot[:, ::2, 0] = 1.0  # every other row: one destination near 1, the rest at 0
+    mu = torch.where(hot.view(E, A).bool() | (torch.arange(A // P, device=DEV) % 2 == 1).repeat_interleave(P)[None],
+                     torch.where(hot.view(E, A).bool(), torch.ones_like(mu), torch.zeros_like(mu)), mu) * mask
+    for warm in (True, False):
+        raw = explore_postprocess(mu, mask, P, warm, 0.0, 0.1, seed=11, step=3, threshold=0.0, passes=0)
+        out = explore_postprocess(mu, mask, P, warm, 0.0, 0.1, seed=11, step=3)
+        ref = normalize_slices_reference(raw.view(E, -1, P).cpu().double(), 0.1, 2).float()
+        torch.testing.assert_close(out.cpu().view(E, -1, P), ref, rtol=1e-6, atol=1e-6)
+        uniform = (ref.amax(-1) - ref.amin(-1)).abs() < 1e-6
+        if not warm and n > 100:
+            assert uniform.any() and (~uniform).any(), "both kernel paths exercised"
+
+
 def test_splitk_linear_matches_linear():
     """Split-K weight gradient == plain GEMM gradient (fp32 reference, bf16 autocast tolerance)."""
     from gsc_amd.ops.linear import linear
