@@ -53,7 +53,40 @@ static void cu_probe(uintptr_t out, int blocks, int spin, uintptr_t stream) {
   check_launch();
 }
 
+// Cross-stream hand-off by stream memory operations: the command processor of the producing stream writes a
+// 32-bit sequence number once the stream's preceding work is done, and the consuming stream's processor polls
+// for it (>=) before its next packet.  Replaces an event record + barrier-packet wait on the act <-> simulator
+// chain between two simulator kernels.  The word lives in signal memory (hipMallocSignalMemory), as the API
+// requires; kernels keep their own acquire / release fences, so data written before the value is visible to
+// the consumer's kernels.
+static bool stream_values_supported() {
+  int dev = 0, v = 0;
+  GSC_HIP_CHECK(hipGetDevice(&dev));
+  GSC_HIP_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, dev));
+  return v != 0;
+}
+static uintptr_t alloc_signal_words(int n) {
+  void* p = nullptr;
+  GSC_HIP_CHECK(hipExtMallocWithFlags(&p, sizeof(uint32_t) * (size_t)n, hipMallocSignalMemory));
+  GSC_HIP_CHECK(hipMemset(p, 0, sizeof(uint32_t) * (size_t)n));
+  GSC_HIP_CHECK(hipDeviceSynchronize());
+  return reinterpret_cast<uintptr_t>(p);
+}
+static void free_signal_words(uintptr_t p) { GSC_HIP_CHECK(hipFree(reinterpret_cast<void*>(p))); }
+static void stream_write_value(uintptr_t stream, uintptr_t word, uint32_t value) {
+  GSC_HIP_CHECK(hipStreamWriteValue32(stream_of(stream), reinterpret_cast<void*>(word), value, 0));
+}
+static void stream_wait_value(uintptr_t stream, uintptr_t word, uint32_t value) {
+  GSC_HIP_CHECK(hipStreamWaitValue32(stream_of(stream), reinterpret_cast<void*>(word), value, hipStreamWaitValueGte,
+                                     0xFFFFFFFFu));
+}
+
 void register_streams(py::module_& m) {
+  m.def("stream_values_supported", &stream_values_supported);
+  m.def("alloc_signal_words", &alloc_signal_words, "n zeroed 32-bit words of signal memory (device pointer)");
+  m.def("free_signal_words", &free_signal_words);
+  m.def("stream_write_value", &stream_write_value, "stream writes value to word after its preceding work");
+  m.def("stream_wait_value", &stream_wait_value, "stream waits until word >= value");
   m.def("cu_probe", &cu_probe, "record the hardware CU of each workgroup");
   m.def("create_cu_masked_stream", &create_cu_masked_stream, "HIP stream restricted to the given CUs");
   m.def("destroy_stream", &destroy_stream);

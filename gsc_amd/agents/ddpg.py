@@ -19,9 +19,10 @@ act (actor forward) -> exploration + post-processing kernel -> simulator kernel 
 from __future__ import annotations
 
 import copy
-import os
 import math
+import os
 import time
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -531,6 +532,7 @@ class BatchedTrainer:
         self._handoff = True
         self.sim_stream = self.learn_stream = None
         self.act_stream = None  # GSC_ACT_STREAM=1: the act path on an unmasked stream (every CU)
+        self._words = 0         # signal words of the act <-> simulator hand-off (0: events)
         self.sim_cus = 0
         if self.device.type == "cuda" and tcfg.overlap_sim:
             sim_cus = tcfg.sim_cus if tcfg.sim_cus >= 0 else self.auto_sim_cus(sim)
@@ -568,6 +570,11 @@ class BatchedTrainer:
                 act_env = os.environ.get("GSC_ACT_STREAM", "auto")
                 if act_env != "0":
                     self.act_stream = torch.cuda.Stream(self.device)
+                    # simulator <-> act hand-offs by stream memory operations (GSC_STREAM_VALUES=0: events)
+                    if os.environ.get("GSC_STREAM_VALUES", "1") != "0" and nat.stream_values_supported():
+                        self._words = nat.alloc_signal_words(2)  # [simulator step done, act done]
+                        self._seq = 0
+                        weakref.finalize(self, nat.free_signal_words, self._words)
                 # persistent GNN grids sized to the CUs free while the simulator runs (one full round)
                 budget = int(os.environ.get("GSC_GNN_CU_BUDGET", str(n - k)))
                 nat.gnn_set_cu_budget(budget)
@@ -717,7 +724,21 @@ class BatchedTrainer:
             # buffers this step reuses).  The learner's replay insert of step t-1 and update t wait for the
             # act only (the update rewrites the actor weights), so they run concurrently with simulator(t).
             self.sim_stream.wait_stream(main)
-            if self.act_stream is not None:
+            if self.act_stream is not None and self._words:
+                # sequence words instead of events on the chain simulator(t-1) -> act(t) -> simulator(t): the
+                # act waits for the learner's stream (actor weights, by event: that work finished long before)
+                # and for the simulator's word; the simulator for the act's word (scripts/gpurun/handoff_ab.sh)
+                nat, seq, sim_word, act_word = self.sim.native, self._seq, self._words, self._words + 4
+                self.act_stream.wait_stream(main)
+                if seq > 0:
+                    nat.stream_wait_value(self.act_stream.cuda_stream, sim_word, seq)
+                with torch.cuda.stream(self.act_stream):
+                    act = self._act(obs, topo, warm, k)
+                    ev_act = self._event()
+                    ev_act.record(self.act_stream)
+                nat.stream_write_value(self.act_stream.cuda_stream, act_word, seq + 1)
+                nat.stream_wait_value(self.sim_stream.cuda_stream, act_word, seq + 1)
+            elif self.act_stream is not None:
                 self.act_stream.wait_stream(self.sim_stream)
                 with torch.cuda.stream(self.act_stream):
                     act = self._act(obs, topo, warm, k)
@@ -733,6 +754,9 @@ class BatchedTrainer:
                 out = self.sim.step(act, buffer_set=k, obs_out=obs_next, pmask_ready=self._pmask_ready)
                 ev_sim = self._event()
                 ev_sim.record(self.sim_stream)
+            if self.act_stream is not None and self._words:
+                self.sim.native.stream_write_value(self.sim_stream.cuda_stream, self._words, self._seq + 1)
+                self._seq += 1
                 if episode_end:
                     new_topo = self.sim.topo_next.to(torch.int64).clone()
             main.wait_event(ev_act)

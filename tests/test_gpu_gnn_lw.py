@@ -56,8 +56,10 @@ def test_layerwise_matches_reference_small_graphs(case):
     _check(gs, P, 300, direct=True)
 
 
-@pytest.mark.parametrize("layers,iters,hidden", [(1, 1, 22), (3, 1, 16), (2, 2, 32)])
+@pytest.mark.parametrize("layers,iters,hidden", [(1, 1, 22), (3, 1, 16), (2, 2, 32), (2, 1, 8)])
 def test_layerwise_shapes(layers, iters, hidden):
+    """hidden 22 / 32: the staged MFMA kernels; 16 with a next conv (its fused linears' MFMA image does not
+    fit at n_pad 200) and 8: the lane-per-node kernels."""
     gs = GraphSet([load_topology(p) for p in SYN200[:2]], 200, DEV)
     _check(gs, 200, 40, layers, iters, hidden, direct=True)
 
