@@ -53,12 +53,14 @@ static void cu_probe(uintptr_t out, int blocks, int spin, uintptr_t stream) {
   check_launch();
 }
 
-// Cross-stream hand-off by stream memory operations: the command processor of the producing stream writes a
-// 32-bit sequence number once the stream's preceding work is done, and the consuming stream's processor polls
-// for it (>=) before its next packet.  Replaces an event record + barrier-packet wait on the act <-> simulator
-// chain between two simulator kernels.  The word lives in signal memory (hipMallocSignalMemory), as the API
-// requires; kernels keep their own acquire / release fences, so data written before the value is visible to
-// the consumer's kernels.
+// Cross-stream hand-off by sequence words in fine-grained device memory (system-scope atomics: visible across
+// XCDs and queues).  The producing stream runs signal_word_kernel after its work (an ordinary dispatch, back-to-back with
+// the kernel before it in its queue); the consuming stream runs wait_word_kernel, one lane polling the word
+// (>=, wrap-safe) with s_sleep between reads, before its next kernel.  Replaces an event record + barrier-packet
+// wait on the act <-> simulator chain (and HIP's stream memory operations, whose write is a separately
+// scheduled kernel ~10 us after the producer's last one: profiles/handoff_ab.txt).  Kernel boundaries keep
+// their acquire / release fences, so data written before the word is visible to the consumer's kernels.  Every
+// wait ends: after timeout_ticks of the 100 MHz constant clock it sets err and exits (the trainer checks err).
 static bool stream_values_supported() {
   int dev = 0, v = 0;
   GSC_HIP_CHECK(hipGetDevice(&dev));
@@ -67,26 +69,49 @@ static bool stream_values_supported() {
 }
 static uintptr_t alloc_signal_words(int n) {
   void* p = nullptr;
-  GSC_HIP_CHECK(hipExtMallocWithFlags(&p, sizeof(uint32_t) * (size_t)n, hipMallocSignalMemory));
+  GSC_HIP_CHECK(hipExtMallocWithFlags(&p, sizeof(uint32_t) * (size_t)n, hipDeviceMallocFinegrained));
   GSC_HIP_CHECK(hipMemset(p, 0, sizeof(uint32_t) * (size_t)n));
   GSC_HIP_CHECK(hipDeviceSynchronize());
   return reinterpret_cast<uintptr_t>(p);
 }
 static void free_signal_words(uintptr_t p) { GSC_HIP_CHECK(hipFree(reinterpret_cast<void*>(p))); }
-static void stream_write_value(uintptr_t stream, uintptr_t word, uint32_t value) {
-  GSC_HIP_CHECK(hipStreamWriteValue32(stream_of(stream), reinterpret_cast<void*>(word), value, 0));
+
+__global__ void signal_word_kernel(uint32_t* word, uint32_t value) {
+  if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-static void stream_wait_value(uintptr_t stream, uintptr_t word, uint32_t value) {
-  GSC_HIP_CHECK(hipStreamWaitValue32(stream_of(stream), reinterpret_cast<void*>(word), value, hipStreamWaitValueGte,
-                                     0xFFFFFFFFu));
+__global__ void wait_word_kernel(uint32_t* word, uint32_t value, uint32_t* err, long long timeout_ticks) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = wall_clock64();
+  while ((int)(__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > timeout_ticks) {
+      __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
+}
+static void signal_word(uintptr_t stream, uintptr_t word, uint32_t value) {
+  hipLaunchKernelGGL(signal_word_kernel, dim3(1), dim3(64), 0, stream_of(stream), ptr<uint32_t>(word), value);
+  check_launch();
+}
+static void wait_word(uintptr_t stream, uintptr_t word, uint32_t value, uintptr_t err, double timeout_s) {
+  hipLaunchKernelGGL(wait_word_kernel, dim3(1), dim3(64), 0, stream_of(stream), ptr<uint32_t>(word), value,
+                     ptr<uint32_t>(err), (long long)(timeout_s * 1e8));
+  check_launch();
+}
+static uint32_t read_word(uintptr_t word) {
+  uint32_t v = 0;
+  GSC_HIP_CHECK(hipMemcpy(&v, reinterpret_cast<void*>(word), sizeof(v), hipMemcpyDeviceToHost));
+  return v;
 }
 
 void register_streams(py::module_& m) {
   m.def("stream_values_supported", &stream_values_supported);
-  m.def("alloc_signal_words", &alloc_signal_words, "n zeroed 32-bit words of signal memory (device pointer)");
+  m.def("alloc_signal_words", &alloc_signal_words, "n zeroed 32-bit words of fine-grained device memory");
   m.def("free_signal_words", &free_signal_words);
-  m.def("stream_write_value", &stream_write_value, "stream writes value to word after its preceding work");
-  m.def("stream_wait_value", &stream_wait_value, "stream waits until word >= value");
+  m.def("signal_word", &signal_word, "stream stores value to word after its preceding work");
+  m.def("wait_word", &wait_word, "stream waits until word >= value (err |= 1 after timeout_s)");
+  m.def("read_word", &read_word);
   m.def("cu_probe", &cu_probe, "record the hardware CU of each workgroup");
   m.def("create_cu_masked_stream", &create_cu_masked_stream, "HIP stream restricted to the given CUs");
   m.def("destroy_stream", &destroy_stream);

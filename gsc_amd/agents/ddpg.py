@@ -572,7 +572,7 @@ class BatchedTrainer:
                     self.act_stream = torch.cuda.Stream(self.device)
                     # simulator <-> act hand-offs by stream memory operations (GSC_STREAM_VALUES=0: events)
                     if os.environ.get("GSC_STREAM_VALUES", "1") != "0" and nat.stream_values_supported():
-                        self._words = nat.alloc_signal_words(2)  # [simulator step done, act done]
+                        self._words = nat.alloc_signal_words(3)  # [simulator step done, act done, wait timed out]
                         self._seq = 0
                         weakref.finalize(self, nat.free_signal_words, self._words)
                 # persistent GNN grids sized to the CUs free while the simulator runs (one full round)
@@ -727,17 +727,19 @@ class BatchedTrainer:
             if self.act_stream is not None and self._words:
                 # sequence words instead of events on the chain simulator(t-1) -> act(t) -> simulator(t): the
                 # act waits for the learner's stream (actor weights, by event: that work finished long before)
-                # and for the simulator's word; the simulator for the act's word (scripts/gpurun/handoff_ab.sh)
+                # and for the simulator's word; the simulator for the act's word (csrc/ops/streams.hip,
+                # profiles/handoff_ab.txt)
                 nat, seq, sim_word, act_word = self.sim.native, self._seq, self._words, self._words + 4
+                err = self._words + 8
                 self.act_stream.wait_stream(main)
                 if seq > 0:
-                    nat.stream_wait_value(self.act_stream.cuda_stream, sim_word, seq)
+                    nat.wait_word(self.act_stream.cuda_stream, sim_word, seq, err, 10.0)
                 with torch.cuda.stream(self.act_stream):
                     act = self._act(obs, topo, warm, k)
                     ev_act = self._event()
                     ev_act.record(self.act_stream)
-                nat.stream_write_value(self.act_stream.cuda_stream, act_word, seq + 1)
-                nat.stream_wait_value(self.sim_stream.cuda_stream, act_word, seq + 1)
+                nat.signal_word(self.act_stream.cuda_stream, act_word, seq + 1)
+                nat.wait_word(self.sim_stream.cuda_stream, act_word, seq + 1, err, 10.0)
             elif self.act_stream is not None:
                 self.act_stream.wait_stream(self.sim_stream)
                 with torch.cuda.stream(self.act_stream):
@@ -755,7 +757,7 @@ class BatchedTrainer:
                 ev_sim = self._event()
                 ev_sim.record(self.sim_stream)
             if self.act_stream is not None and self._words:
-                self.sim.native.stream_write_value(self.sim_stream.cuda_stream, self._words, self._seq + 1)
+                self.sim.native.signal_word(self.sim_stream.cuda_stream, self._words, self._seq + 1)
                 self._seq += 1
                 if episode_end:
                     new_topo = self.sim.topo_next.to(torch.int64).clone()
@@ -799,6 +801,8 @@ class BatchedTrainer:
                 main.wait_stream(self.sim_stream)
             self.sim.check_flags()
             self.replay.check_sparse()
+            if self._words and self.sim.native.read_word(self._words + 8):
+                raise RuntimeError("act / simulator hand-off: a stream waited 10 s for its sequence word")
 
     def _learn(self) -> None:
         if _DIAG_NO_LEARN:  # diagnostics only (never in bench numbers): measures the act + sim chain alone

@@ -1,5 +1,5 @@
 #!/bin/bash
-# act <-> simulator hand-off: signal words (GSC_STREAM_VALUES=1, default) vs events, the equivalence test, then
+# act <-> simulator hand-off: sequence words (GSC_STREAM_VALUES=1, default) vs events, the equivalence test, then
 # the headline bench interleaved (two rounds each)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,5 +1,5 @@
 """Overlapped trainer (simulator on its CU-masked stream, act path on its own stream): the act <-> simulator
-hand-off by stream memory operations (signal words, the default) gives bit-identical training to the event
+hand-off by sequence words (signal / wait kernels, the default) gives bit-identical training to the event
 hand-off (GSC_STREAM_VALUES=0) -- the same transitions, metrics and learner parameters."""
 import os
 
