@@ -19,12 +19,14 @@ def _run(words: str):
     try:
         cfg = yaml.safe_load(open(cfg_path("config", "agent", "sample_agent.yaml")))
         cfg["episode_steps"] = 12
-        sim = load_batched_from_paths([cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml")],
-                                      cfg_path("service_functions", "abc.yaml"),
+        nets = [cfg_path("networks", "abilene", f) for f in ("abilene-in4-rand-cap1-2.graphml",
+                                                             "abilene-in4-rand-cap0-2.graphml")]
+        sim = load_batched_from_paths(nets, cfg_path("service_functions", "abc.yaml"),
                                       cfg_path("config", "simulator", "sample_config.yaml"), cfg, 64,
                                       device="cuda", seed=5)
         tr = BatchedTrainer(cfg, sim, TrainerConfig(num_envs=64, batch_size=512, learning_starts=4, seed=2,
-                                                    check_every=0, replay_capacity=256))
+                                                    check_every=0, replay_capacity=256),
+                            network_schedule=[0, 1], period=1)  # topology switches at every episode end
         assert tr.sim_stream is not None and tr.act_stream is not None, "overlapped act / simulator streams"
         assert bool(tr._words) == (words == "1")
         for _ in range(30):
@@ -32,7 +34,7 @@ def _run(words: str):
         m = tr.metrics()
         torch.cuda.synchronize()
         n = len(tr.replay)
-        return (m["succ"], m["drop"], tr.learner.updates, tr.learner.actor_flat.view().clone(),
+        return (m["succ"], m["drop"], tr.learner.updates, tr.learner.actor_flat.view().clone(), tr.topo.clone(),
                 tr.learner.critic_flat.view().clone(), tr.replay.obs[:n].clone(), tr.replay.rewards[:n].clone())
     finally:
         os.environ.pop("GSC_STREAM_VALUES", None)
@@ -42,5 +44,6 @@ def test_word_handoff_matches_event_handoff():
     a, b = _run("1"), _run("0")
     assert a[2] == b[2] >= 20
     assert a[0] == b[0] and a[1] == b[1] and a[0] + a[1] > 0
+    assert torch.equal(a[4], b[4]) and int(a[4][0]) == 0  # two switches: back on topology 0
     for x, y in zip(a[3:], b[3:]):
         assert torch.equal(x, y)
