@@ -570,8 +570,11 @@ class BatchedTrainer:
                 act_env = os.environ.get("GSC_ACT_STREAM", "auto")
                 if act_env != "0":
                     self.act_stream = torch.cuda.Stream(self.device)
-                    # simulator <-> act hand-offs by stream memory operations (GSC_STREAM_VALUES=0: events)
-                    if os.environ.get("GSC_STREAM_VALUES", "1") != "0" and nat.stream_values_supported():
+                    # simulator <-> act hand-offs by sequence words (GSC_STREAM_VALUES=0: events).  Not under
+                    # rocprofv3 counter collection: it serializes kernels, so a wait kernel would spin while its
+                    # producer waits behind it (until the 10 s timeout)
+                    counters = os.environ.get("ROCPROF_COUNTER_COLLECTION", "") not in ("", "0", "False", "false")
+                    if os.environ.get("GSC_STREAM_VALUES", "1") != "0" and not counters and nat.stream_values_supported():
                         self._words = nat.alloc_signal_words(3)  # [simulator step done, act done, wait timed out]
                         self._seq = 0
                         weakref.finalize(self, nat.free_signal_words, self._words)
