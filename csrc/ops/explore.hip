@@ -9,7 +9,7 @@
 // right, so results agree to float32 rounding) with the residual of the rounded sum added to the
 // first weight that can absorb it, found by a ballot.  Above 32 destinations most rows skip them: when
 // the second pass provably zeroes the whole row (FastExit), the kernel writes the uniform row directly.
-// At 200 nodes x 256 envs (92M weights): 565 -> 255 us noisy, 441 -> 169 us warm-up, against a 137 us
+// At 200 nodes x 256 envs (92M weights): 565 -> 244 us noisy, 441 -> 159 us warm-up, against a 137 us
 // copy of the same bytes (profiles/explore_r5.txt); the remaining time is VALU issue (Philox-10 +
 // Box-Muller per weight quad).
 #include <pybind11/pybind11.h>
@@ -217,6 +217,10 @@ __device__ __forceinline__ void explore_raw(float (&wf)[K], const float (&v)[K],
   float z[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
+    if (vec) {  // f0 is 4-aligned (4-aligned rows, 4 weights per lane): weight k is quad entry k
+      z[k] = qa.x[k & 3];
+      continue;
+    }
     const int j = (int)((f0 & 3) + k);  // 0..6: quad a below 4, quad b from 4
     z[k] = 0.f;
 #pragma unroll
