@@ -175,6 +175,8 @@ struct PMask {
   long stride;
   int C, F, Cd, Sd;
   int ident;  // C == Cd and F == Sd: the bitset of action row r sits at 32 r bytes (no index split)
+  int rows;   // action rows the simulator's block holds (N C F of its largest topology): rows past it (sources
+              // >= N when n_pad > N) have no bitset and are skipped -- they would land in the next env's state
 };
 
 // Host-side constants of the early uniform exit (passes == 2, thr > 0): the rows whose second pass zeroes
@@ -240,8 +242,10 @@ __device__ __forceinline__ void explore_raw(float (&wf)[K], const float (&v)[K],
   }
 }
 
-// Bitset word offset (in u64) of action row `row` in the simulator's pmask block of env `env`
+// Bitset word offset (in u64) of action row `row` in the simulator's pmask block of env `env`, or null for a
+// row whose source node the simulator's block does not hold
 __device__ __forceinline__ uint64_t* pmask_dst(const PMask& pm, int env, int row) {
+  if (row >= pm.rows) return nullptr;  // rows are source-major: row >= N C F <=> source >= N
   long prow = row;
   if (!pm.ident) {
     const int sf = row % pm.F, c = (row / pm.F) % pm.C, sn = row / (pm.F * pm.C);
@@ -321,7 +325,7 @@ __device__ __forceinline__ void explore_general(const float* __restrict__ mrow, 
       if (lane == q) word = wq;
     }
     uint64_t* dst = pmask_dst(pm, env, row);
-    if (lane < 4) dst[lane] = word;
+    if (dst && lane < 4) dst[lane] = word;
   }
 }
 
@@ -407,7 +411,8 @@ __global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const flo
           const uint64_t b = (uint64_t)__ballot(64 * q + lane < P && pmv[s][q] > 0.f);
           if (lane == q) word = b;
         }
-        if (lane < 4) pmask_dst(pm, env, row)[lane] = word;
+        uint64_t* dst = pmask_dst(pm, env, row);
+        if (dst && lane < 4) dst[lane] = word;
       }
     } else {
       explore_general<K>(mtab + (long)row * P, out, base, P, env, row, lane, thr, passes, pm, wf[s][0],
@@ -440,8 +445,8 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t
                          py::object pmask) {
   GSC_CHECK(A % P == 0, "action dim must be a multiple of n_pad");
   GSC_CHECK(P <= 256, "n_pad > 256 not supported by the exploration kernel");
-  PMask pm{nullptr, 0, 1, 1, 1, 1, 1};
-  if (!pmask.is_none()) {  // (base, stride, C, F, Cd, Sd)
+  PMask pm{nullptr, 0, 1, 1, 1, 1, 1, 0};
+  if (!pmask.is_none()) {  // (base, stride, C, F, Cd, Sd, N): N = source nodes of the simulator's pmask block
     py::tuple t = pmask.cast<py::tuple>();
     pm.base = ptr<char>(t[0].cast<uintptr_t>());
     pm.stride = t[1].cast<long>();
@@ -449,8 +454,11 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t
     pm.F = t[3].cast<int>();
     pm.Cd = t[4].cast<int>();
     pm.Sd = t[5].cast<int>();
-    GSC_CHECK(P > 32 && (long)P * P * pm.C * pm.F == A && pm.C <= pm.Cd && pm.F <= pm.Sd,
-              "explore pmask hand-off: n_pad > 32 and A = n_pad^2 C F within the simulator dims");
+    GSC_CHECK(t.size() == 7, "explore pmask hand-off: (base, stride, C, F, Cd, Sd, N)");
+    const int N = t[6].cast<int>();
+    GSC_CHECK(P > 32 && (long)P * P * pm.C * pm.F == A && pm.C <= pm.Cd && pm.F <= pm.Sd && N >= 1 && N <= P,
+              "explore pmask hand-off: n_pad > 32, A = n_pad^2 C F and N <= n_pad within the simulator dims");
+    pm.rows = N * pm.C * pm.F;
     pm.ident = pm.C == pm.Cd && pm.F == pm.Sd;
   }
   const long slices = (long)E * (A / P);

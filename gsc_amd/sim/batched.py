@@ -282,13 +282,16 @@ class BatchedSimulator:
         self.prof = torch.zeros(self.E * 4 + self.E * 128, dtype=torch.int64, device=self.device) if on else None
 
     def pmask_target(self) -> Optional[tuple]:
-        """(base, stride, C, F, Cd, Sd) for the exploration kernel to write the step kernel's destination bitsets
-        (topologies beyond 64 nodes with HBM-resident tables), or None when the kernel does not read them."""
+        """(base, stride, C, F, Cd, Sd, N) for the exploration kernel to write the step kernel's destination bitsets
+        (topologies beyond 64 nodes with HBM-resident tables), or None when the kernel does not read them.  The
+        block holds rows for the N source nodes of the largest topology only; the kernel skips action rows of
+        sources >= N (n_pad > N)."""
         lay = self.ctx.pmask_layout if self.is_device else None
         if lay is None:
             return None
         off, Cd, Sd = lay
-        return (self.states.data_ptr() + int(off), self.state_bytes, self.C, self.F, int(Cd), int(Sd))
+        return (self.states.data_ptr() + int(off), self.state_bytes, self.C, self.F, int(Cd), int(Sd),
+                int(self.dims["N"]))
 
     def step(self, actions: torch.Tensor, buffer_set: int = 0, obs_out: Optional[torch.Tensor] = None,
              pmask_ready: bool = False) -> SimStepOut:

@@ -39,7 +39,7 @@ def main():
     if a.pmask:
         stride = P * a.C * a.F * 32
         buf = torch.zeros(E * stride, dtype=torch.uint8, device="cuda")
-        pm = (buf.data_ptr(), stride, a.C, a.F, a.C, a.F)
+        pm = (buf.data_ptr(), stride, a.C, a.F, a.C, a.F, P)
     gbytes = 2 * E * A * 4 / 1e9
 
     def timed(fn):
