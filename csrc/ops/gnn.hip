@@ -1,13 +1,15 @@
 // GATv2 embedder entry points (reference models.py:10-53 on PyG GATv2Conv, aggr='mean'): dispatch to
 // the fused per-graph MFMA kernels and the column-sum reduction of their per-workgroup gradients.
 //
-//   <= 32 nodes   gnn_mf.hip  one wave per graph (Abilene, BtEurope: the headline configs)
-//   33..64 nodes  gnn_mt.hip  one graph per workgroup, one wave per 32-node tile (50-node configs)
+//   <= 32 nodes    gnn_mf.hip  one wave per graph (Abilene, BtEurope: the headline configs)
+//   33..64 nodes   gnn_mt.hip  one graph per workgroup, one wave per 32-node tile (50-node configs)
+//   65..256 nodes  gnn_lg.hip  one graph per 512-thread workgroup, all convs in LDS, recomputing backward
+//                              (200-node configs; H < 24 at 200 nodes, LDS-bound)
 //
-// Both need H <= 32, F_in <= 16, an encoder + ONE shared process block (GSC's num_layers = 2) and
-// unique (source, target) messages.  Every other shape -- larger graphs (200-node topologies),
-// wider embedders, other layer counts -- runs the layer-wise kernels (gsc_amd/ops/gnn_lw.py:
-// MFMA GEMM node linears + per-node attention kernels); gsc_amd/ops/gnn.py routes by gnn_fused_fits.
+// All need F_in <= 16, an encoder + ONE shared process block (GSC's num_layers = 2) and unique
+// (source, target) messages (mf / mt: H <= 32; lg: H <= 31 and the LDS budget).  Every other shape --
+// wider embedders, other layer counts -- runs the layer-wise kernels (gsc_amd/ops/gnn_lw.py: MFMA GEMM
+// node linears + per-node attention kernels); gsc_amd/ops/gnn.py routes by gnn_fused_fits.
 //
 // The backward writes one partial gradient row per workgroup (each element owned by one lane or
 // summed over the workgroup's waves in a fixed order: no atomics, bitwise reproducible); a column
@@ -33,6 +35,10 @@ bool gnn_mt_supported(int Fin, int H, int NM, int M, int L, int n_blocks, const 
 void gnn_mt_forward(const void* args, uintptr_t stream, int cus);
 int gnn_mt_backward(const void* args, uintptr_t stream, int cus, int max_rows);
 int gnn_mt_saved_bytes(const void* args);
+bool gnn_lg_supported(int Fin, int H, int NM, int P, int M, int L, int n_blocks, const int* layer_of);
+void gnn_lg_forward(const void* args, uintptr_t stream, int cus);
+int gnn_lg_backward(const void* args, uintptr_t stream, int cus, int max_rows);
+std::vector<unsigned long long> gnn_lg_prof();
 
 __global__ __launch_bounds__(256) void column_sum_kernel(const float* __restrict__ partials, float* __restrict__ out,
                                                          int rows, int cols) {
@@ -57,13 +63,20 @@ static int n_blocks_of(const std::vector<int>& layer_of) {
   return maxb + 1;
 }
 
-enum GnnPath { kPathNone = 0, kPathMf = 1, kPathMt = 2 };
+enum GnnPath { kPathNone = 0, kPathMf = 1, kPathMt = 2, kPathLg = 3 };
 
-static GnnPath fused_path(int M, int NM, int Fin, int H, const std::vector<int>& layer_of, bool uniq) {
+// GSC_GNN_LG=0: large graphs on the layer-wise kernels instead (A/B)
+static bool lg_enabled() {
+  const char* e = getenv("GSC_GNN_LG");
+  return !(e && e[0] == '0');
+}
+
+static GnnPath fused_path(int M, int NM, int P, int Fin, int H, const std::vector<int>& layer_of, bool uniq) {
   if (!uniq || layer_of.empty() || (int)layer_of.size() > kClMaxLayers) return kPathNone;
   const int L = (int)layer_of.size(), nb = n_blocks_of(layer_of);
   if (gnn_mf_supported(Fin, H, NM, L, nb, layer_of.data())) return kPathMf;
   if (gnn_mt_supported(Fin, H, NM, M, L, nb, layer_of.data())) return kPathMt;
+  if (lg_enabled() && gnn_lg_supported(Fin, H, NM, P, M, L, nb, layer_of.data())) return kPathLg;
   return kPathNone;
 }
 
@@ -86,6 +99,7 @@ static ClArgs make_args(py::dict t, uintptr_t params, uintptr_t x, uintptr_t top
   c.s_dst = reinterpret_cast<const void*>(t["s_dst"].cast<uintptr_t>());
   c.s_src = reinterpret_cast<const void*>(t["s_src"].cast<uintptr_t>());
   c.MP = t["MP"].cast<int>();
+  c.deg_order = t.contains("deg_order") ? ptr<const int32_t>(t["deg_order"].cast<uintptr_t>()) : nullptr;
   c.M = t["M"].cast<int>();
   c.NM = t["NM"].cast<int>();
   c.B = B;
@@ -97,7 +111,7 @@ static ClArgs make_args(py::dict t, uintptr_t params, uintptr_t x, uintptr_t top
   c.n_blocks = n_blocks_of(layer_of);
   c.n_params = cl_block_offset(c.n_blocks - 1, Fin, H) + cl_block_size(c.n_blocks == 1 ? Fin : H, H);
   c.waves = 4;
-  *path = fused_path(c.M, c.NM, Fin, H, layer_of, t["uniq"].cast<bool>());
+  *path = fused_path(c.M, c.NM, P, Fin, H, layer_of, t["uniq"].cast<bool>());
   GSC_CHECK(*path != kPathNone,
             "GNN shape not covered by the fused MFMA kernels (route it to the layer-wise kernels, gnn_lw.py)");
   return c;
@@ -177,6 +191,7 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
   c.emb = ptr<float>(emb);
   c.blob = reinterpret_cast<void*>(blob);
   if (path == kPathMf) gnn_mf_forward(&c, stream, num_cus());
+  else if (path == kPathLg) gnn_lg_forward(&c, stream, num_cus());
   else mt_forward_queued(c, stream);
 }
 
@@ -193,6 +208,13 @@ void gnn_forward2(py::dict tables, uintptr_t params, uintptr_t params2, uintptr_
     c.params2 = ptr<const float>(params2);
     c.emb2 = ptr<float>(emb2);
     gnn_mf_forward(&c, stream, num_cus());
+    return;
+  }
+  if (path == kPathLg) {
+    gnn_lg_forward(&c, stream, num_cus());
+    c.params = ptr<const float>(params2);
+    c.emb = ptr<float>(emb2);
+    gnn_lg_forward(&c, stream, num_cus());
     return;
   }
   mt_forward_queued(c, stream);
@@ -212,6 +234,8 @@ void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo
   int rows;
   if (path == kPathMf) {
     rows = gnn_mf_backward(&c, stream, num_cus(), max_rows);
+  } else if (path == kPathLg) {
+    rows = gnn_lg_backward(&c, stream, num_cus(), max_rows);  // recomputes the forward: no saved state
   } else if ((c.work = work_slot(stream_of(stream))) != nullptr) {
     // CU-masked partner stream (overlap mode): the grid spans every CU and claims graphs from a counter,
     // so the CUs the simulator releases mid-kernel join in (a fixed-stride grid sized to the budget left
@@ -227,13 +251,14 @@ void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo
 
 // Whether the fused MFMA kernels cover this shape (else: layer-wise kernels).
 bool gnn_fused_fits(int M, int NM, int P, int Fin, int H, std::vector<int> layer_of, bool uniq) {
-  return P >= NM && fused_path(M, NM, Fin, H, layer_of, uniq) != kPathNone;
+  return P >= NM && fused_path(M, NM, P, Fin, H, layer_of, uniq) != kPathNone;
 }
 
 // Bytes per graph the grad-requiring forward saves for the backward.
 int gnn_saved_bytes(py::dict tables, int P, int Fin, int H, std::vector<int> layer_of) {
   GnnPath path;
   const ClArgs c = make_args(tables, 0, 0, 0, 1, P, Fin, H, layer_of, &path);
+  if (path == kPathLg) return 0;
   return path == kPathMf ? gnn_mf_saved_bytes(&c) : gnn_mt_saved_bytes(&c);
 }
 
@@ -256,6 +281,7 @@ void register_gnn(py::module_& m) {
   m.def("gnn_fused_fits", &gnn_fused_fits, py::arg("M"), py::arg("NM"), py::arg("P"), py::arg("Fin"), py::arg("H"),
         py::arg("layer_of"), py::arg("uniq"));
   m.def("gnn_set_cu_budget", &gnn_set_cu_budget, "CUs available to GNN launches (0 = whole device)");
+  m.def("gnn_lg_prof", &gnn_lg_prof, "large-graph kernels' phase cycles (GSC_LG_PROF=1), read and cleared");
 }
 
 }  // namespace gsc

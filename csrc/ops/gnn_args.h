@@ -52,6 +52,7 @@ struct ClArgs {
   const float* params2;      // forward only: a second parameter set on the same graphs (or null) ...
   float* emb2;               // ... and its embeddings [B, H] (target actor + target critic in one launch)
   int* work;                 // multi-tile backward: zeroed work-queue counter (graphs claimed by atomics), or null
+  const int32_t* deg_order;  // [T, 2, P] nodes by in-degree / by out-degree, descending (large-graph kernels)
 };
 
 __device__ __forceinline__ void cl_wave_sync() {

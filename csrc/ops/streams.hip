@@ -60,7 +60,11 @@ static void cu_probe(uintptr_t out, int blocks, int spin, uintptr_t stream) {
 // wait on the act <-> simulator chain (and HIP's stream memory operations, whose write is a separately
 // scheduled kernel ~10 us after the producer's last one: profiles/handoff_ab.txt).  Kernel boundaries keep
 // their acquire / release fences, so data written before the word is visible to the consumer's kernels.  Every
-// wait ends: after timeout_ticks of the 100 MHz constant clock it sets err and exits (the trainer checks err).
+// wait ends: after timeout_ticks of the 100 MHz constant clock it sets err and exits.  err is a mapped host word
+// the trainer reads at every step, with at most a few steps enqueued ahead of the GPU, so a timed-out hand-off
+// fails the run within those steps; the replay data written after the timeout is invalid (the run is aborted).
+// Streams sharing a hardware queue (GPU_MAX_HW_QUEUES = 4, more streams under RCCL) cannot deadlock here: each
+// wait is submitted after its producer's signal in submission order, so a shared queue only serialises them.
 static bool stream_values_supported() {
   int dev = 0, v = 0;
   GSC_HIP_CHECK(hipGetDevice(&dev));
@@ -75,6 +79,17 @@ static uintptr_t alloc_signal_words(int n) {
   return reinterpret_cast<uintptr_t>(p);
 }
 static void free_signal_words(uintptr_t p) { GSC_HIP_CHECK(hipFree(reinterpret_cast<void*>(p))); }
+// One zeroed 32-bit word of coherent, mapped host memory: (host pointer, device pointer).  The wait kernel's
+// timeout flag lives here, so the trainer reads it every step with a plain load (no copy, no stream sync).
+static py::tuple alloc_host_word() {
+  void* h = nullptr;
+  void* d = nullptr;
+  GSC_HIP_CHECK(hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+  *reinterpret_cast<volatile uint32_t*>(h) = 0u;
+  GSC_HIP_CHECK(hipHostGetDevicePointer(&d, h, 0));
+  return py::make_tuple(reinterpret_cast<uintptr_t>(h), reinterpret_cast<uintptr_t>(d));
+}
+static void free_host_word(uintptr_t h) { GSC_HIP_CHECK(hipHostFree(reinterpret_cast<void*>(h))); }
 
 __global__ void signal_word_kernel(uint32_t* word, uint32_t value) {
   if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -109,6 +124,8 @@ void register_streams(py::module_& m) {
   m.def("stream_values_supported", &stream_values_supported);
   m.def("alloc_signal_words", &alloc_signal_words, "n zeroed 32-bit words of fine-grained device memory");
   m.def("free_signal_words", &free_signal_words);
+  m.def("alloc_host_word", &alloc_host_word, "(host ptr, device ptr) of a zeroed coherent mapped host word");
+  m.def("free_host_word", &free_host_word);
   m.def("signal_word", &signal_word, "stream stores value to word after its preceding work");
   m.def("wait_word", &wait_word, "stream waits until word >= value (err |= 1 after timeout_s)");
   m.def("read_word", &read_word);

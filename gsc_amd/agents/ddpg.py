@@ -18,7 +18,9 @@ act (actor forward) -> exploration + post-processing kernel -> simulator kernel 
 """
 from __future__ import annotations
 
+import collections
 import copy
+import ctypes
 import math
 import os
 import time
@@ -419,7 +421,9 @@ class TrainerConfig:
     learning_starts: Optional[int] = None   # iterations; default: nb_steps_warmup_critic
     replay_capacity: Optional[int] = None   # default: mem_limit * num_envs (capped)
     replay_cap_max: int = 2_000_000
-    replay_bytes_max: Optional[float] = None  # default: 25 % of HBM (4 GB on CPU)
+    replay_bytes_max: Optional[float] = None  # default: 60 % (dense) / 65 % (sparse rows) of this process's
+                                            # share of the device memory (_replay_hbm); 4 GB on CPU
+    handoff_timeout_s: float = 10.0         # act <-> simulator sequence-word wait limit (then the run fails)
     seed: int = 0
     check_every: int = 50
     overlap_sim: bool = True                # run the simulator kernel on its own stream, concurrent with updates
@@ -458,8 +462,23 @@ def replay_plan(cap: int, n_pad: int, n_obs: int, action_dim: int, action_bytes:
     return (True, sparse_per, 0.65 * hbm) if sparse else (False, dense_per, 0.6 * hbm)
 
 
+def _replay_hbm(device) -> float:
+    """Device bytes the replay budget is a share of: this process's part of the GPU -- the total divided by the
+    local ranks that share the device (a multi-process-per-GPU rehearsal), and never more than is free right now
+    (another job on the card, or this rank's learner already allocated)."""
+    if device.type != "cuda":
+        return 0.0
+    total = torch.cuda.get_device_properties(device).total_memory
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1)
+    per_dev = max(1, lw // max(1, torch.cuda.device_count()))
+    free, _ = torch.cuda.mem_get_info(device)
+    return float(min(total / per_dev, free))
+
+
 class BatchedTrainer:
     """E lockstep environments on the device simulator + DDPG learner (one process per GPU)."""
+
+    _AHEAD = 4  # steps the host may enqueue ahead of the simulator when hand-offs use sequence words
 
     def __init__(self, cfg: dict, sim: BatchedSimulator, tcfg: TrainerConfig, dist_info: Optional[DistInfo] = None,
                  network_schedule: Optional[Sequence[int]] = None, period: int = 0):
@@ -481,7 +500,7 @@ class BatchedTrainer:
         # 2M x 720 KB; config 4's 2M x 45 KB fits dense, whose GEMMs are faster at small A); 1 forces it where
         # the native kernels apply (n_pad <= 240, critic first layer 64 wide), 0 disables it.
         R_rows = sim.action_dim // sim.n_pad
-        hbm = torch.cuda.get_device_properties(self.device).total_memory if self.device.type == "cuda" else 0
+        hbm = _replay_hbm(self.device)
         eligible = bool(self.learner.native_ok and self.device.type == "cuda" and sim.n_pad <= 240
                         and self.learner.critic.mlp.layers[0].weight.shape[0] == 64)
         self.sparse_replay, per, budget = replay_plan(
@@ -533,6 +552,8 @@ class BatchedTrainer:
         self.sim_stream = self.learn_stream = None
         self.act_stream = None  # GSC_ACT_STREAM=1: the act path on an unmasked stream (every CU)
         self._words = 0         # signal words of the act <-> simulator hand-off (0: events)
+        self._err_host = None   # the hand-off's wait-timed-out flag (mapped host word)
+        self._ahead = collections.deque()  # simulator-done events of the last steps (run-ahead bound)
         self.sim_cus = 0
         if self.device.type == "cuda" and tcfg.overlap_sim:
             sim_cus = tcfg.sim_cus if tcfg.sim_cus >= 0 else self.auto_sim_cus(sim)
@@ -575,9 +596,14 @@ class BatchedTrainer:
                     # producer waits behind it (until the 10 s timeout)
                     counters = os.environ.get("ROCPROF_COUNTER_COLLECTION", "") not in ("", "0", "False", "false")
                     if os.environ.get("GSC_STREAM_VALUES", "1") != "0" and not counters and nat.stream_values_supported():
-                        self._words = nat.alloc_signal_words(3)  # [simulator step done, act done, wait timed out]
+                        self._words = nat.alloc_signal_words(3)  # [simulator step done, act done, -]
                         self._seq = 0
                         weakref.finalize(self, nat.free_signal_words, self._words)
+                        # wait-timed-out flag in mapped host memory: read every step without a sync; the host
+                        # stays at most _AHEAD steps ahead of the simulator so a timeout fails the run promptly
+                        hptr, self._err_dev = nat.alloc_host_word()
+                        self._err_host = ctypes.c_uint32.from_address(hptr)
+                        weakref.finalize(self, nat.free_host_word, hptr)
                 # persistent GNN grids sized to the CUs free while the simulator runs (one full round)
                 budget = int(os.environ.get("GSC_GNN_CU_BUDGET", str(n - k)))
                 nat.gnn_set_cu_budget(budget)
@@ -711,7 +737,19 @@ class BatchedTrainer:
                                        seed=self.t.seed * 131 + self.dist.rank, step=self.global_step,
                                        out=self._act_bufs[k], topo=topo, pmask=pm)
 
+    def _check_handoff(self) -> None:
+        """Fail the run if a sequence-word wait timed out: wait for the simulator of _AHEAD steps ago (already done
+        in steady state: the GPU has that many steps queued), then read the mapped host flag."""
+        while len(self._ahead) >= self._AHEAD:
+            self._ahead.popleft().synchronize()
+        if self._err_host is not None and self._err_host.value:
+            raise RuntimeError(f"act / simulator hand-off: a stream waited {self.t.handoff_timeout_s:g} s for its "
+                               f"sequence word (step {self.global_step}); the run is aborted, its replay data after "
+                               "the timeout is invalid")
+
     def _step(self) -> None:
+        if self._words:
+            self._check_handoff()
         warm = self.global_step < self.learning_starts
         k = self.global_step & 1
         obs, topo = self._obs_bufs[self.global_step % 3], self.topo
@@ -733,10 +771,10 @@ class BatchedTrainer:
                 # and for the simulator's word; the simulator for the act's word (csrc/ops/streams.hip,
                 # profiles/handoff_ab.txt)
                 nat, seq, sim_word, act_word = self.sim.native, self._seq, self._words, self._words + 4
-                err = self._words + 8
+                err, tmo = self._err_dev, float(self.t.handoff_timeout_s)
                 self.act_stream.wait_stream(main)
                 if seq > 0:
-                    nat.wait_word(self.act_stream.cuda_stream, sim_word, seq, err, 10.0)
+                    nat.wait_word(self.act_stream.cuda_stream, sim_word, seq, err, tmo)
                 with torch.cuda.stream(self.act_stream):
                     act = self._act(obs, topo, warm, k)
                     # the signal right behind the last act kernel: an event record between them costs the
@@ -744,7 +782,7 @@ class BatchedTrainer:
                     nat.signal_word(self.act_stream.cuda_stream, act_word, seq + 1)
                     ev_act = self._event()
                     ev_act.record(self.act_stream)
-                nat.wait_word(self.sim_stream.cuda_stream, act_word, seq + 1, err, 10.0)
+                nat.wait_word(self.sim_stream.cuda_stream, act_word, seq + 1, err, tmo)
             elif self.act_stream is not None:
                 self.act_stream.wait_stream(self.sim_stream)
                 with torch.cuda.stream(self.act_stream):
@@ -762,6 +800,9 @@ class BatchedTrainer:
                 if self.act_stream is not None and self._words:  # right behind the simulator kernel
                     self.sim.native.signal_word(self.sim_stream.cuda_stream, self._words, self._seq + 1)
                     self._seq += 1
+                    ahead = torch.cuda.Event()
+                    ahead.record(self.sim_stream)
+                    self._ahead.append(ahead)
                 ev_sim = self._event()
                 ev_sim.record(self.sim_stream)
                 if episode_end:
@@ -806,8 +847,6 @@ class BatchedTrainer:
                 main.wait_stream(self.sim_stream)
             self.sim.check_flags()
             self.replay.check_sparse()
-            if self._words and self.sim.native.read_word(self._words + 8):
-                raise RuntimeError("act / simulator hand-off: a stream waited 10 s for its sequence word")
 
     def _learn(self) -> None:
         if _DIAG_NO_LEARN:  # diagnostics only (never in bench numbers): measures the act + sim chain alone

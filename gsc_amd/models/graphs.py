@@ -88,6 +88,15 @@ class GraphSet:
         self.in_dst = torch.from_numpy(in_dst).to(dev)
         self.out_q = torch.from_numpy(out_q).to(dev)
         self.out_dst = torch.from_numpy(out_dst).to(dev)
+        # lane -> node maps of the large-graph kernels (csrc/ops/gnn_lg.hip): nodes by in-degree (row 0) and by
+        # out-degree (row 1), descending (stable; padded nodes last), so each wave's 32 nodes have similar
+        # degrees and the per-node message loops waste few lane-iterations on shorter segments
+        order = np.zeros((T, 2, self.n_pad), np.int32)
+        for i in range(T):
+            for r, ptr in enumerate((in_ptr, out_ptr)):
+                d = np.diff(ptr[i])
+                order[i, r] = np.argsort(-d, kind="stable")
+        self.deg_order = torch.from_numpy(order).to(dev)
         self.in_ptr = torch.from_numpy(in_ptr).to(dev)
         self.in_msg = torch.from_numpy(in_msg).to(dev)
         self.out_ptr = torch.from_numpy(out_ptr).to(dev)

@@ -20,7 +20,8 @@ def _tables(graphs) -> dict:
                  nmsgs=graphs.num_msgs.data_ptr(), M=int(graphs.M), NM=int(graphs.max_nodes),
                  in_src=graphs.in_src.data_ptr(), in_dst=graphs.in_dst.data_ptr(), out_q=graphs.out_q.data_ptr(),
                  out_dst=graphs.out_dst.data_ptr(), uniq=bool(graphs.unique_messages),
-                 s_dst=graphs.s_dst.data_ptr(), s_src=graphs.s_src.data_ptr(), MP=int(graphs.mf_mp))
+                 s_dst=graphs.s_dst.data_ptr(), s_src=graphs.s_src.data_ptr(), MP=int(graphs.mf_mp),
+                 deg_order=graphs.deg_order.data_ptr())
         graphs._kernel_tables = t
     return t
 

@@ -142,9 +142,17 @@ class FlatParams:
             total += p.numel()
         return out
 
-    def pack_legacy(self, t: torch.Tensor) -> torch.Tensor:
-        """Packed form of a tensor stored in the unsharded layout (pre-packed checkpoints)."""
-        return torch.cat([t[o:o + p.numel()].reshape(-1) for p, o in zip(self.params, self.legacy_offsets())])
+    def pack_legacy(self, t: torch.Tensor, align: int = 4) -> torch.Tensor:
+        """Packed form of a tensor stored in the unsharded layout (pre-packed checkpoints).  Only the unsharded
+        lengths are accepted -- the parameter run itself or the padded flat buffer (Adam moments): a checkpoint
+        written with a sharded (bucket-aligned) layout is longer and shifted and would load wrong weights."""
+        offs = self.legacy_offsets()
+        end = offs[-1] + self.params[-1].numel()
+        if t.numel() not in (end, end + (-end) % align):
+            raise ValueError(f"legacy (unpacked) checkpoint tensor has {t.numel()} elements; the unsharded layout of "
+                             f"this network has {end} (padded {end + (-end) % align}) -- a sharded-layout checkpoint "
+                             "cannot be read: re-save it with this build (packed layout)")
+        return torch.cat([t[o:o + p.numel()].reshape(-1) for p, o in zip(self.params, offs)])
 
 
 class FusedAdamPolyak:

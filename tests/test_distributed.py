@@ -241,6 +241,11 @@ def test_learner_loads_legacy_flat_checkpoint():
     b.load_state_dict(legacy)
     assert torch.equal(b.actor_flat.flat, a.actor_flat.flat)
     assert torch.equal(b.critic_opt.v, a.critic_opt.v)
+    # a bucket-aligned (ZeRO) flat buffer is longer and shifted: refused instead of loading wrong weights
+    bad = dict(legacy)
+    bad["actor_opt"] = dict(legacy["actor_opt"], m=torch.cat([legacy["actor_opt"]["m"], torch.zeros(64)]))
+    with pytest.raises(ValueError, match="sharded-layout"):
+        b.load_state_dict(bad)
 
 
 def test_dp_batched_trainer_replicas_identical():

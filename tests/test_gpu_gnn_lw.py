@@ -36,8 +36,11 @@ def _check(gs, P, B, layers=2, iters=2, hidden=22, direct=False):
     return out
 
 
-def test_layerwise_200_nodes_is_the_native_path():
+def test_layerwise_200_nodes_is_the_native_path_without_lg(monkeypatch):
+    """GSC_GNN_LG=0 routes 200-node graphs back to the layer-wise kernels (the large-graph fused kernels'
+    A/B partner)."""
     from gsc_amd.ops.gnn import gnn_fits
+    monkeypatch.setenv("GSC_GNN_LG", "0")
     gs = GraphSet([load_topology(p) for p in SYN200], 200, DEV)
     emb = GNNEmbedder(3, 22, 2, "mean", 2)
     assert not gnn_fits(emb, gs, 200, 3)
@@ -64,9 +67,10 @@ def test_layerwise_shapes(layers, iters, hidden):
     _check(gs, 200, 40, layers, iters, hidden, direct=True)
 
 
-def test_native_update_uses_layerwise_for_200_nodes():
-    """The native DDPG update runs the layer-wise embedder (no PyTorch GNN) on 200-node graphs."""
+def test_native_update_uses_layerwise_for_200_nodes(monkeypatch):
+    """With GSC_GNN_LG=0 the native DDPG update runs the layer-wise embedder (no PyTorch GNN) on 200-node graphs."""
     import yaml
+    monkeypatch.setenv("GSC_GNN_LG", "0")
     from gsc_amd.agents import Batch, DDPGLearner
     cfg = yaml.safe_load(open(cfg_path("config", "agent", "agent_syn200.yaml")))
     gs = GraphSet([load_topology(p) for p in SYN200], 200, DEV)

@@ -47,3 +47,41 @@ def test_word_handoff_matches_event_handoff():
     assert torch.equal(a[4], b[4]) and int(a[4][0]) == 0  # two switches: back on topology 0
     for x, y in zip(a[3:], b[3:]):
         assert torch.equal(x, y)
+
+
+def test_handoff_timeout_fails_at_that_step():
+    """A simulator signal that never comes: the act's wait times out (0.2 s here), sets the mapped host flag, and
+    the trainer raises within its run-ahead bound of that step -- not at the episode end (200 steps)."""
+    from gsc_amd.agents import BatchedTrainer, TrainerConfig
+    from gsc_amd.sim.batched import load_batched_from_paths
+    cfg = yaml.safe_load(open(cfg_path("config", "agent", "sample_agent.yaml")))
+    sim = load_batched_from_paths([cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml")],
+                                  cfg_path("service_functions", "abc.yaml"),
+                                  cfg_path("config", "simulator", "sample_config.yaml"), cfg, 64, device="cuda", seed=5)
+    tr = BatchedTrainer(cfg, sim, TrainerConfig(num_envs=64, batch_size=512, learning_starts=2, seed=2, check_every=0,
+                                                replay_capacity=256, handoff_timeout_s=0.2))
+    if not tr._words:
+        pytest.skip("sequence-word hand-off not in use on this device")
+    for _ in range(6):
+        tr.step()
+    nat = tr.sim.native
+    real = nat.signal_word
+    dropped = []
+
+    def drop_once(stream, word, value):
+        if word == tr._words and not dropped:
+            dropped.append(tr.global_step)
+            return None
+        return real(stream, word, value)
+
+    lost = tr.global_step
+    tr.sim.native.signal_word = drop_once
+    try:
+        with pytest.raises(RuntimeError, match="hand-off"):
+            for _ in range(60):
+                tr.step()
+    finally:
+        tr.sim.native.signal_word = real
+        torch.cuda.synchronize()
+    assert dropped == [lost]
+    assert tr.global_step - lost <= tr._AHEAD + 3, (lost, tr.global_step)

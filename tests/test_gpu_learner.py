@@ -250,11 +250,14 @@ def test_native_update_reads_replay_rows_in_place():
 SYN200 = [cfg_path("networks", "synthetic", f"syn200-in16-cap1-3-s{i}.graphml") for i in range(3)]
 
 
-def test_native_update_matches_fp32_reference_200_nodes():
+@pytest.mark.parametrize("lg", ["1", "0"], ids=["fused-lg", "layer-wise"])
+def test_native_update_matches_fp32_reference_200_nodes(lg, monkeypatch):
     """Config-5 shapes: n_pad 200, 3 SFCs x 3 SFs (A = 360,000), three 200-node topologies (different
-    action masks), batch 256: the layer-wise GNN kernels, the composed multi-topology actor loss
+    action masks), batch 256: the large-graph fused GNN kernels (GSC_GNN_LG=0: the layer-wise ones), the
+    composed multi-topology actor loss
     (T c1 = 192 <= B), split-K action projections and the fused TD-target projection, against the fp32
     CPU autograd learner (first-update gradients per tensor, losses)."""
+    monkeypatch.setenv("GSC_GNN_LG", lg)
     cfg = yaml.safe_load(open(cfg_path("config", "agent", "agent_syn200.yaml")))
     P, C, T, B = 200, 3, 3, 256
     ref, gpu = _learners(cfg, T, P, nets=SYN200, C=C)
@@ -263,7 +266,7 @@ def test_native_update_matches_fp32_reference_200_nodes():
     for l in (ref, gpu, auto):
         l.critic_opt.lr = 0.0  # frozen critic (see the three_topologies case)
     nu = gpu.native_update(B)
-    assert nu.compose and nu.fuse_target and nu.layerwise
+    assert nu.compose and nu.fuse_target and nu.layerwise == (lg == "0")
     from gsc_amd.agents import Batch
     g = torch.Generator().manual_seed(5)
     topo = torch.arange(B) % T

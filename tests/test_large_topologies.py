@@ -68,14 +68,17 @@ def test_syn200_sim_and_scheduler():
 
 
 def test_gnn_native_path_for_graphs_beyond_lds():
-    """50-node graphs fit the fused per-graph kernels; 200-node graphs do not and run the layer-wise
-    native kernels (gsc_amd/ops/gnn_lw.py) -- no PyTorch GNN on the GPU (GPU numerics:
-    tests/test_gpu_gnn_lw.py)."""
+    """50-node graphs run the two-tile fused kernels, 200-node graphs the large-graph fused kernels (gnn_lg.hip:
+    one graph per workgroup, all convs in LDS) at GSC's width; shapes beyond their LDS budget (H = 32 at 200
+    nodes) run the layer-wise native kernels (gsc_amd/ops/gnn_lw.py) -- no PyTorch GNN on the GPU (GPU numerics:
+    tests/test_gpu_gnn_lg.py, tests/test_gpu_gnn_lw.py)."""
     import inspect
     from gsc_amd.models import gnn as gnn_mod
     from gsc_amd.ops.gnn import gnn_fits
     e = GNNEmbedder(3, 22, 2, "mean", 2)
     assert gnn_fits(e, GraphSet([load_topology(SYN50)], 50, "cpu"), 50, 3)
-    assert not gnn_fits(e, GraphSet([load_topology(SYN200[0])], 200, "cpu"), 200, 3)
+    assert gnn_fits(e, GraphSet([load_topology(SYN200[0])], 200, "cpu"), 200, 3)
+    assert not gnn_fits(GNNEmbedder(3, 32, 2, "mean", 2), GraphSet([load_topology(SYN200[0])], 200, "cpu"), 200, 3)
+    assert not gnn_fits(GNNEmbedder(3, 22, 3, "mean", 1), GraphSet([load_topology(SYN200[0])], 200, "cpu"), 200, 3)
     src = inspect.getsource(gnn_mod.GNNEmbedder.forward)
     assert "gnn_embed_layerwise" in src
