@@ -43,7 +43,7 @@ namespace gsc {
 
 constexpr int kLgThreads = 512;  // 8 waves: 256 lane pairs = up to 256 nodes, 8 MFMA row tiles
 constexpr int kLgMaxNodes = 256;
-constexpr int kLgRows = kLgThreads / 16;  // 16-lane DPP rows of the workgroup (partial sums of the reductions)
+constexpr int kLgBwdThreads = 1024;  // backward: 16 waves, 4 lanes per node
 constexpr float kLgSlope = 0.2f;
 constexpr int kLgUf = 2;
 constexpr int kLgUb = 2;  // ... in the backward's row-reading loops  // messages per chunk in the forward attention loop (registers: 4 waves / SIMD)
@@ -51,7 +51,7 @@ constexpr int kLgUb = 2;  // ... in the backward's row-reading loops  // message
 struct LgLayout {
   int P, P32, PK, RS, TS, L, nslots, xs;
   int frag, vec, ord, iptr, deg, isrc, optr, oq, odst, sc, ds, zb, slot[kClMaxLayers], R, xl, xr, dy, dtl, dtr, dnl, dnr, ht,
-      red, acc0, total;
+      red, acc0, wacc, total;
 };
 
 // thread id through an opaque asm: the LDS addresses derived from it are recomputed at their use instead of
@@ -77,49 +77,100 @@ struct LgClock {
     }                                                          \
   } while (0)
 static unsigned long long* g_lg_prof = nullptr;
+// PROF variants only (debug): count non-finite fp32 words of an LDS region into prof[slot]
+__device__ __forceinline__ void lg_nanchk(const float* p, int n, unsigned long long* prof, int slot) {
+  unsigned c = 0;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) c += !isfinite(p[k]);
+  if (c) atomicAdd(prof + slot, (unsigned long long)c);
+}
 
-// sum of v over the 8 lanes of this lane's parity in its 16-lane row (node lanes holding the same channels),
-// complete in lanes 14 (even) and 15 (odd): three DPP row shifts, no LDS
-__device__ __forceinline__ float lg_row_parity_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xF, 0xF, false));  // row_shr:2
+// Lane groups: NL consecutive lanes (2 or 4) hold one node, HV / NL channels each.
+// Sum over the node's NL lanes (the score's / dalpha's channel sum): DPP quad permutations, no LDS
+template <int NL>
+__device__ __forceinline__ float lg_node_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+  if (NL == 4) v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  return v;
+}
+// Sum over the wave's nodes of one channel slot (lanes of the same position within their group): DPP row
+// shifts within each 16-lane row, then the four rows; complete in the wave's last NL lanes (lanes 64-NL .. 63)
+template <int NL>
+__device__ __forceinline__ float lg_wave_sum(float v) {
+  if (NL <= 2) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xF, 0xF, false));  // row_shr:2
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xF, 0xF, false));  // row_shr:4
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xF, 0xF, false));  // row_shr:8
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
   return v;
 }
 
-// lane value of the pair partner (lanes 2i <-> 2i+1): DPP quad_perm [1, 0, 3, 2]
-__device__ __forceinline__ float lg_pair(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-}
-
 template <int HC>
-__device__ __forceinline__ void lg_load_f(float (&v)[HC], const float* src) {
+__device__ __forceinline__ void lg_load_f(float (&v)[HC], const float* src) {  // 16-B (HC % 4 == 0) or 8-B runs
+  if constexpr (HC % 4 == 0) {
 #pragma unroll
-  for (int u = 0; u < HC / 4; ++u) {
-    const float4 f = reinterpret_cast<const float4*>(src)[u];
-    v[4 * u] = f.x;
-    v[4 * u + 1] = f.y;
-    v[4 * u + 2] = f.z;
-    v[4 * u + 3] = f.w;
+    for (int u = 0; u < HC / 4; ++u) {
+      const float4 f = reinterpret_cast<const float4*>(src)[u];
+      v[4 * u] = f.x;
+      v[4 * u + 1] = f.y;
+      v[4 * u + 2] = f.z;
+      v[4 * u + 3] = f.w;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < HC / 2; ++u) {
+      const float2 f = reinterpret_cast<const float2*>(src)[u];
+      v[2 * u] = f.x;
+      v[2 * u + 1] = f.y;
+    }
   }
 }
 template <int HC>
-__device__ __forceinline__ void lg_store_bf16(__bf16* dst, const float (&v)[HC]) {  // HC / 4 8-byte stores
+__device__ __forceinline__ void lg_store_f(float* dst, const float (&v)[HC]) {
+  if constexpr (HC % 4 == 0) {
 #pragma unroll
-  for (int u = 0; u < HC / 4; ++u) {
-    bf16x4 b;
+    for (int u = 0; u < HC / 4; ++u)
+      reinterpret_cast<float4*>(dst)[u] = float4{v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]};
+  } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[4 * u + e];
-    reinterpret_cast<bf16x4*>(dst)[u] = b;
+    for (int u = 0; u < HC / 2; ++u) reinterpret_cast<float2*>(dst)[u] = float2{v[2 * u], v[2 * u + 1]};
+  }
+}
+template <int HC>
+__device__ __forceinline__ void lg_store_bf16(__bf16* dst, const float (&v)[HC]) {  // 8-B or 4-B stores
+  if constexpr (HC % 4 == 0) {
+#pragma unroll
+    for (int u = 0; u < HC / 4; ++u) {
+      bf16x4 b;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[4 * u + e];
+      reinterpret_cast<bf16x4*>(dst)[u] = b;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < HC / 2; ++u) {
+      __attribute__((ext_vector_type(2))) __bf16 b;
+      b[0] = (__bf16)v[2 * u];
+      b[1] = (__bf16)v[2 * u + 1];
+      reinterpret_cast<decltype(b)*>(dst)[u] = b;
+    }
   }
 }
 template <int HC>
 __device__ __forceinline__ void lg_load_bf16(float (&v)[HC], const __bf16* src) {
+  if constexpr (HC % 4 == 0) {
 #pragma unroll
-  for (int u = 0; u < HC / 4; ++u) {
-    const bf16x4 b = reinterpret_cast<const bf16x4*>(src)[u];
+    for (int u = 0; u < HC / 4; ++u) {
+      const bf16x4 b = reinterpret_cast<const bf16x4*>(src)[u];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[4 * u + e] = (float)b[e];
+      for (int e = 0; e < 4; ++e) v[4 * u + e] = (float)b[e];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < HC / 2; ++u) {
+      const __attribute__((ext_vector_type(2))) __bf16 b = reinterpret_cast<const __attribute__((ext_vector_type(2))) __bf16*>(src)[u];
+      v[2 * u] = (float)b[0];
+      v[2 * u + 1] = (float)b[1];
+    }
   }
 }
 
@@ -127,7 +178,7 @@ __device__ __forceinline__ void lg_load_bf16(float (&v)[HC], const __bf16* src) 
 // 2: block 1 transposed, B operand of dX W), lane-linear in LDS: [set][Wl k-step 0, 1, Wr k-step 0, 1][lane]
 __device__ __forceinline__ void lg_stage_frags(const ClArgs& a, bf16x8* img, int nsets) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int f = wave; f < nsets; f += kLgThreads / 64) {
+  for (int f = wave; f < nsets; f += blockDim.x / 64) {
     MfW w;
     mf_load_w(w, a, a.params, f == 0 ? 0 : 1, f == 2, lane);
     img[(f * 4 + 0) * 64 + lane] = w.l[0];
@@ -199,16 +250,15 @@ __device__ __forceinline__ void lg_linear(const bf16x8* frag, int set, bool k2, 
 // rescale per chunk) and mean aggregation; returns the conv output half-row (bias, optional ReLU; zero for i >= n).
 // Messages go U at a time: the U source ids, then the U rows are loaded before any of them is used (clamped to
 // the segment's last message), so one LDS round trip serves U messages.
-template <int HC, int U>
-__device__ __forceinline__ void lg_attend(float (&y)[HC], int i, int n, int c0, const float* vec, bool relu,
+template <int HC, int U, int NL>
+__device__ __forceinline__ void lg_attend(float (&y)[HC], int i, int n, int c0, bool hi, const float* vec, bool relu,
                                           const float* XL, const float* XR, const int32_t* iptr,
                                           const uint16_t* isrc, const float* deg, const LgLayout& m) {
 #pragma unroll
   for (int k = 0; k < HC; ++k) y[k] = 0.f;
   if (i >= n) return;
   // score = att . LeakyReLU(z) = 0.6 (u_j + v_i) + 0.4 att . |z|: one FMA per channel with the |z| source
-  // modifier; the half holding channel HV - 1 (u + v) adds the linear part
-  const bool hi = c0 != 0;
+  // modifier; the lane holding channel HV - 1 (u + v; hi) adds the linear part
   float xr[HC], a4[HC], acc[HC];
   lg_load_f<HC>(xr, XR + i * m.RS + c0);
   lg_load_f<HC>(a4, vec + 64 + c0);
@@ -237,7 +287,7 @@ __device__ __forceinline__ void lg_attend(float (&y)[HC], int i, int n, int c0, 
       float v = lin * z[HC - 1];
 #pragma unroll
       for (int k = 0; k < HC; ++k) v = fmaf(a4[k], fabsf(z[k]), v);
-      v += lg_pair(v);
+      v = lg_node_sum<NL>(v);
       sc[u] = q + u < q1 ? v : -__builtin_inff();
       cm = fmaxf(cm, sc[u]);
     }
@@ -266,20 +316,20 @@ __device__ __forceinline__ void lg_attend(float (&y)[HC], int i, int n, int c0, 
 }
 
 // Topology rows of graph type t into LDS (u16 message arrays; the backward also the source-sorted CSR)
-template <bool BWD>
+template <bool BWD, int NT>
 __device__ __forceinline__ void lg_stage_topo(const ClArgs& a, int t, char* lds, const LgLayout& m) {
   int32_t* iptr = reinterpret_cast<int32_t*>(lds + m.iptr);
   float* deg = reinterpret_cast<float*>(lds + m.deg);
   uint16_t* isrc = reinterpret_cast<uint16_t*>(lds + m.isrc);
   const int P = m.P, M = a.M;
   uint16_t* ord = reinterpret_cast<uint16_t*>(lds + m.ord);
-  for (int k = threadIdx.x; k < 2 * P; k += kLgThreads) ord[k] = (uint16_t)a.deg_order[(long)t * 2 * P + k];
-  for (int k = threadIdx.x; k <= P; k += kLgThreads) {
+  for (int k = threadIdx.x; k < 2 * P; k += NT) ord[k] = (uint16_t)a.deg_order[(long)t * 2 * P + k];
+  for (int k = threadIdx.x; k <= P; k += NT) {
     iptr[k] = a.in_ptr[(long)t * (P + 1) + k];
     if (k < P) deg[k] = a.deg[(long)t * P + k];
     if (BWD) reinterpret_cast<int32_t*>(lds + m.optr)[k] = a.out_ptr[(long)t * (P + 1) + k];
   }
-  for (int k = threadIdx.x; k < M; k += kLgThreads) {
+  for (int k = threadIdx.x; k < M; k += NT) {
     isrc[k] = (uint16_t)a.in_src[(long)t * M + k];
     if (BWD) {
       reinterpret_cast<uint16_t*>(lds + m.oq)[k] = (uint16_t)a.out_q[(long)t * M + k];
@@ -289,15 +339,16 @@ __device__ __forceinline__ void lg_stage_topo(const ClArgs& a, int t, char* lds,
 }
 
 // input rows of graph b as the bf16 image (channels 0..15: F_in <= 16, zero past F_in and for rows >= P)
-__device__ __forceinline__ void lg_load_x(float (&xv)[8], const ClArgs& a, long b, int i, int hf) {
+// (g = the lane's position in its node group: lanes 0 / 1 of the group take channels 0..7 / 8..15)
+__device__ __forceinline__ void lg_load_x(float (&xv)[8], const ClArgs& a, long b, int i, int g) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int c = 8 * hf + k;
-    xv[k] = (i < a.P && c < a.Fin) ? a.x[(b * a.P + i) * a.Fin + c] : 0.f;
+    const int c = 8 * g + k;
+    xv[k] = (i < a.P && g < 2 && c < a.Fin) ? a.x[(b * a.P + i) * a.Fin + c] : 0.f;
   }
 }
 __device__ __forceinline__ void lg_put_x(__bf16* S, const float (&xv)[8], int i, int hf, const LgLayout& m) {
-  if (i < m.P32) {
+  if (i < m.P32 && hf < 2) {
     bf16x8 v;
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = (__bf16)xv[k];
@@ -306,7 +357,7 @@ __device__ __forceinline__ void lg_put_x(__bf16* S, const float (&xv)[8], int i,
 }
 
 __device__ __forceinline__ void lg_zero(char* p, int bytes) {
-  for (int k = 16 * threadIdx.x; k < bytes; k += 16 * kLgThreads) *reinterpret_cast<float4*>(p + k) = float4{0, 0, 0, 0};
+  for (int k = 16 * threadIdx.x; k < bytes; k += 16 * blockDim.x) *reinterpret_cast<float4*>(p + k) = float4{0, 0, 0, 0};
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -314,7 +365,7 @@ __device__ __forceinline__ void lg_zero(char* p, int bytes) {
 // ---------------------------------------------------------------------------------------------
 template <int HV, bool PROF>
 __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void gnn_lg_fwd_kernel(ClArgs a, LgLayout m, unsigned long long* prof) {
-  constexpr int HC = HV / 2;
+  constexpr int NL = 2, HC = HV / NL;  // lane pairs: 2 workgroups of 8 waves per CU
   extern __shared__ __attribute__((aligned(16))) char lds[];
   bf16x8* frag = reinterpret_cast<bf16x8*>(lds + m.frag);
   float* vec = reinterpret_cast<float*>(lds + m.vec);
@@ -334,11 +385,11 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
     {
       const int tq = lg_tid();
       float xv[8];
-      lg_load_x(xv, a, b, tq >> 1, tq & 1);
+      lg_load_x(xv, a, b, tq / NL, tq % NL);
       __syncthreads();  // the previous graph is done with every LDS image
       LG_MARK(PROF, clk, 0);
-      lg_stage_topo<false>(a, t, lds, m);
-      lg_put_x(S, xv, tq >> 1, tq & 1, m);
+      lg_stage_topo<false, kLgThreads>(a, t, lds, m);
+      lg_put_x(S, xv, tq / NL, tq % NL, m);
       __syncthreads();
       LG_MARK(PROF, clk, 1);
     }
@@ -352,11 +403,11 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
       __syncthreads();
       LG_MARK(PROF, clk, 2);
       // lane pair p = the node of in-degree rank p (similar segment lengths per wave); p >= P: idle (zero rows)
-      const int tq = lg_tid(), pq = tq >> 1, cq = (tq & 1) * HC, lane = tq & 63;
+      const int tq = lg_tid(), pq = tq / NL, cq = (tq % NL) * HC, lane = tq & 63;
       const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
       float y[HC];
       const bool last = l + 1 == a.L;
-      lg_attend<HC, kLgUf>(y, iq, n, cq, vb, !last, XL, XR, iptr, isrc, deg, m);
+      lg_attend<HC, kLgUf, NL>(y, iq, n, cq, cq + HC == HV, vb, !last, XL, XR, iptr, isrc, deg, m);
       if (!last) {
         __syncthreads();  // S (this conv's input) was read by the node linears before the previous barrier;
                           // the barrier orders this conv's XL reads before the next node linears' XL writes
@@ -364,17 +415,17 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
         if (iq < m.P32) lg_store_bf16<HC>(S + iq * kMfRS + cq, y);
         __syncthreads();
         LG_MARK(PROF, clk, 4);
-      } else {  // mean pool over the real nodes: DPP row sums, then the 32 row partials in a fixed order
+      } else {  // mean pool over the real nodes: wave sums (DPP + two swaps), then the waves in a fixed order
 #pragma unroll
         for (int k = 0; k < HC; ++k) {
-          const float v = lg_row_parity_sum(y[k]);  // y is zero for i >= n
-          if ((lane & 14) == 14) red[(tq >> 4) * 32 + cq + k] = v;
+          const float v = lg_wave_sum<NL>(y[k]);  // y is zero for i >= n
+          if (lane >= 64 - NL) red[wave * 32 + cq + k] = v;
         }
         __syncthreads();
         if (tq < a.H) {
           float s = 0.f;
-#pragma unroll 8
-          for (int w = 0; w < kLgRows; ++w) s += red[w * 32 + tq];
+#pragma unroll
+          for (int w = 0; w < kLgThreads / 64; ++w) s += red[w * 32 + tq];
           a.emb[b * a.H + tq] = s / (float)n;
         }
         LG_MARK(PROF, clk, 5);
@@ -388,11 +439,15 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
 // ---------------------------------------------------------------------------------------------
 // backward (recompute): per-workgroup gradient rows (module layout) into a.partials[blockIdx.x]
 // ---------------------------------------------------------------------------------------------
-// step 2: per target node i -- softmax backward and d x_r[i]; alpha / d score per message into SC / DS.  One pass
-// over the source rows (U at a time): score, z signs and d alpha = dY_i . x_l[j] / deg_i together; then two
-// row-free passes over the per-message scalars.
-template <int HC, int U>
-__device__ __forceinline__ void lg_bwd_targets(float (&dxr)[HC], float (&gbias)[HC], int i, int n, int c0, int hf,
+// step 2: per target node i -- softmax backward and d x_r[i]; alpha / d score per message into SC / DS.
+//   d x_r[i] = att * sum_q ds_q LeakyReLU'(z_q),  ds_q = alpha_q (dalpha_q - c),  c = sum_q alpha_q dalpha_q
+// With LeakyReLU'(z) = 0.2 + 0.8 [z > 0] and sum_q ds_q = 0 this is 0.8 att * (T1 - c T2) / den, where
+// T1 = sum_q e_q dalpha_q [z_q > 0] and T2 = sum_q e_q [z_q > 0] accumulate (online-rescaled, like the forward's
+// aggregation) in the same pass over the source rows that forms the scores and dalpha = dY_i . x_l[j] / deg_i --
+// no per-message sign bits, no second row pass.  A row-free pass then writes alpha and ds for step 3.
+// [z > 0] is saturate(z * 2^126): exact except for denormal z.
+template <int HC, int U, int NL>
+__device__ __forceinline__ void lg_bwd_targets(float (&dxr)[HC], float (&gbias)[HC], int i, int n, int c0, bool hi,
                                                const float* vec, char* lds, const LgLayout& m) {
 #pragma unroll
   for (int k = 0; k < HC; ++k) dxr[k] = 0.f;
@@ -405,17 +460,21 @@ __device__ __forceinline__ void lg_bwd_targets(float (&dxr)[HC], float (&gbias)[
   const float* deg = reinterpret_cast<const float*>(lds + m.deg);
   float* SC = reinterpret_cast<float*>(lds + m.sc);
   float* DS = reinterpret_cast<float*>(lds + m.ds);
-  uint16_t* ZB = reinterpret_cast<uint16_t*>(lds + m.zb);
-  float xr[HC], at[HC], dy[HC];
+  float xr[HC], a4[HC], dy[HC], t1[HC], t2[HC];
   lg_load_f<HC>(xr, XR + i * m.RS + c0);
-  lg_load_f<HC>(at, vec + 64 + c0);
+  lg_load_f<HC>(a4, vec + 64 + c0);
   lg_load_f<HC>(dy, DY + i * m.RS + c0);
 #pragma unroll
-  for (int k = 0; k < HC; ++k) gbias[k] += dy[k];
+  for (int k = 0; k < HC; ++k) {
+    gbias[k] += dy[k];
+    a4[k] *= 0.5f * (1.f - kLgSlope);
+    t1[k] = t2[k] = 0.f;
+  }
   const int q0 = iptr[i], q1 = iptr[i + 1];
   const float rdeg = 1.f / deg[i];
-  const float lin = hf ? 0.5f * (1.f + kLgSlope) : 0.f;  // the half holding channel HV - 1 (u + v): linear part
-  float mx = -__builtin_inff(), den = 0.f;
+  const float lin = hi ? 0.5f * (1.f + kLgSlope) : 0.f;  // the lane holding channel HV - 1 (u + v): linear part
+  const bool lead = c0 == 0;  // the group's first lane writes the per-message scalars
+  float mx = -__builtin_inff(), den = 0.f, ced = 0.f;  // ced = sum e dalpha
   for (int q = q0; q < q1; q += U) {
     int j[U];
 #pragma unroll
@@ -424,47 +483,54 @@ __device__ __forceinline__ void lg_bwd_targets(float (&dxr)[HC], float (&gbias)[
 #pragma unroll
     for (int u = 0; u < U; ++u) lg_load_f<HC>(xj[u], XL + j[u] * m.RS + c0);
     float sc[U], da[U];
-    uint32_t bits[U];
     float cm = -__builtin_inff();
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      float z[HC];
-#pragma unroll
-      for (int k = 0; k < HC; ++k) z[k] = xj[u][k] + xr[k];
-      float v = lin * z[HC - 1], d = 0.f;
-      bits[u] = 0;
+      float v = lin * (xj[u][HC - 1] + xr[HC - 1]), d = 0.f;
 #pragma unroll
       for (int k = 0; k < HC; ++k) {
-        v = fmaf(0.5f * (1.f - kLgSlope) * at[k], fabsf(z[k]), v);
+        v = fmaf(a4[k], fabsf(xj[u][k] + xr[k]), v);
         d = fmaf(dy[k], xj[u][k], d);
-        bits[u] |= (z[k] > 0.f ? 1u : 0u) << k;
       }
-      v += lg_pair(v);
-      d += lg_pair(d);
+      v = lg_node_sum<NL>(v);
+      d = lg_node_sum<NL>(d);
       sc[u] = q + u < q1 ? v : -__builtin_inff();
       da[u] = d * rdeg;
       cm = fmaxf(cm, sc[u]);
     }
     if (cm > mx) {
-      den *= __expf(mx - cm);
+      const float rs = __expf(mx - cm);  // 0 for the first chunk
+      den *= rs;
+      ced *= rs;
+#pragma unroll
+      for (int k = 0; k < HC; ++k) {
+        t1[k] *= rs;
+        t2[k] *= rs;
+      }
       mx = cm;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      den += __expf(sc[u] - mx);
-      if (q + u < q1) {
-        if (hf == 0) {
-          SC[q + u] = sc[u];
-          DS[q + u] = da[u];
-        }
-        ZB[2 * (q + u) + hf] = (uint16_t)bits[u];
+      const float e = __expf(sc[u] - mx), ed = e * da[u];  // 0 past the segment
+      den += e;
+      ced += ed;
+#pragma unroll
+      for (int k = 0; k < HC; ++k) {
+        const float st = __saturatef((xj[u][k] + xr[k]) * 0x1p126f);
+        t1[k] = fmaf(ed, st, t1[k]);
+        t2[k] = fmaf(e, st, t2[k]);
+      }
+      if (q + u < q1 && lead) {
+        SC[q + u] = sc[u];
+        DS[q + u] = da[u];
       }
     }
   }
-  // alpha = softmax; c = sum alpha d alpha (row-free: the lane's own SC / DS entries, written by the pair's
-  // lane 0 in this wave, read back in program order)
-  const float inv = 1.f / (den + 1e-16f);
-  float cs = 0.f;
+  const float inv = 1.f / (den + 1e-16f), cs = ced * inv;
+#pragma unroll
+  for (int k = 0; k < HC; ++k)  // 0.8 att = 2 a4 (a4 = 0.4 att)
+    dxr[k] = 2.f * a4[k] * (t1[k] - cs * t2[k]) * inv;
+  // alpha and ds per message (the group's lead lane wrote this wave's SC / DS entries: program order)
   for (int q = q0; q < q1; q += 4) {
     float sv[4], dv[4];
 #pragma unroll
@@ -475,31 +541,9 @@ __device__ __forceinline__ void lg_bwd_targets(float (&dxr)[HC], float (&gbias)[
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const float al = __expf(sv[u] - mx) * inv;
-      if (q + u < q1) {
-        cs = fmaf(al, dv[u], cs);
-        if (hf == 0) SC[q + u] = al;
-      }
-    }
-  }
-  // d score = alpha (d alpha - c);  d x_r[i] += d score * att * LeakyReLU'(z)
-  for (int q = q0; q < q1; q += 4) {
-    float av[4], dv[4];
-    uint32_t bv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int qq = min(q + u, q1 - 1);
-      av[u] = SC[qq];
-      dv[u] = DS[qq];
-      bv[u] = ZB[2 * qq + hf];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (q + u < q1) {
-        const float ds = av[u] * (dv[u] - cs);
-#pragma unroll
-        for (int k = 0; k < HC; ++k)
-          dxr[k] = fmaf(ds * at[k], __builtin_amdgcn_ubfe(bv[u], k, 1) ? 1.f : kLgSlope, dxr[k]);
-        if (hf == 0) DS[q + u] = ds;
+      if (q + u < q1 && lead) {
+        SC[q + u] = al;
+        DS[q + u] = al * (dv[u] - cs);
       }
     }
   }
@@ -522,9 +566,12 @@ __device__ __forceinline__ void lg_bwd_sources(float (&dxl)[HC], float (&gatt)[H
   const float* deg = reinterpret_cast<const float*>(lds + m.deg);
   const float* SC = reinterpret_cast<const float*>(lds + m.sc);
   const float* DS = reinterpret_cast<const float*>(lds + m.ds);
-  float xl[HC], at[HC];
+  // d x_l[j] = sum_p w_p dY_i + att * sum_p ds_p LeakyReLU'(z_p) = sum_p w_p dY_i + att * (0.2 S + 0.8 T),
+  // S = sum_p ds_p, T = sum_p ds_p [z_p > 0];  d att += sum_p ds_p LeakyReLU(z_p) = 0.6 ds z + 0.4 ds |z|
+  float xl[HC], tt[HC], sds = 0.f;
   lg_load_f<HC>(xl, XL + j * m.RS + c0);
-  lg_load_f<HC>(at, vec + 64 + c0);
+#pragma unroll
+  for (int k = 0; k < HC; ++k) tt[k] = 0.f;
   const int p0 = optr[j], p1 = optr[j + 1];
   for (int p = p0; p < p1; p += U) {
     int q[U], ti[U];
@@ -539,27 +586,45 @@ __device__ __forceinline__ void lg_bwd_sources(float (&dxl)[HC], float (&gatt)[H
     for (int u = 0; u < U; ++u) {
       lg_load_f<HC>(xr[u], XR + ti[u] * m.RS + c0);
       lg_load_f<HC>(dy[u], DY + ti[u] * m.RS + c0);
-      w[u] = SC[q[u]] / deg[ti[u]];
-      ds[u] = DS[q[u]];
+      const bool ok = p + u < p1;
+      w[u] = ok ? SC[q[u]] / deg[ti[u]] : 0.f;
+      ds[u] = ok ? DS[q[u]] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (p + u < p1) {
+      const float d6 = 0.5f * (1.f + kLgSlope) * ds[u], d4 = 0.5f * (1.f - kLgSlope) * ds[u];
+      sds += ds[u];
 #pragma unroll
-        for (int k = 0; k < HC; ++k) {
-          const float z = xl[k] + xr[u][k];
-          const bool pos = z > 0.f;
-          gatt[k] = fmaf(ds[u], pos ? z : kLgSlope * z, gatt[k]);
-          dxl[k] = fmaf(w[u], dy[u][k], fmaf(ds[u] * at[k], pos ? 1.f : kLgSlope, dxl[k]));
-        }
+      for (int k = 0; k < HC; ++k) {
+        const float z = xl[k] + xr[u][k];
+        gatt[k] = fmaf(d6, z, fmaf(d4, fabsf(z), gatt[k]));
+        tt[k] = fmaf(ds[u], __saturatef(z * 0x1p126f), tt[k]);
+        dxl[k] = fmaf(w[u], dy[u][k], dxl[k]);
       }
     }
+  }
+  float at[HC];
+  lg_load_f<HC>(at, vec + 64 + c0);
+#pragma unroll
+  for (int k = 0; k < HC; ++k) dxl[k] = fmaf(at[k], fmaf(1.f - kLgSlope, tt[k], kLgSlope * sds), dxl[k]);
+}
+
+// dst[k] += sum over the wave's nodes of v[k] (this lane's HC channels; dst points at the lane's first channel in
+// the wave's own slot): wave sums, then the wave's last node group adds -- one writer per slot, fixed order
+template <int HC, int NL>
+__device__ __forceinline__ void lg_wave_accum(float* dst, const float (&v)[HC], int lane) {
+  float s[HC];
+#pragma unroll
+  for (int k = 0; k < HC; ++k) s[k] = lg_wave_sum<NL>(v[k]);
+  if (lane >= 64 - NL) {
+#pragma unroll
+    for (int k = 0; k < HC; ++k) dst[k] += s[k];
   }
 }
 
 // HT [k][node] (bf16, row stride TS) of the conv input image S: channels < Fi, a ones row at k = Fi (bias
 // gradients from the same product), zero rows in between up to HV; zero columns for nodes >= P
-template <int HC>
+template <int HC, int HV>
 __device__ __forceinline__ void lg_put_ht(__bf16* HT, const __bf16* S, int i, int c0, int Fi, const LgLayout& m) {
   if (i >= m.PK) return;
   float v[HC];
@@ -570,12 +635,14 @@ __device__ __forceinline__ void lg_put_ht(__bf16* HT, const __bf16* S, int i, in
     const float e = i >= m.P ? 0.f : (c < Fi ? v[k] : (c == Fi ? 1.f : 0.f));
     HT[c * m.TS + i] = (__bf16)e;
   }
-  if (Fi >= 2 * HC && c0 == HC) HT[Fi * m.TS + i] = (__bf16)(i < m.P ? 1.f : 0.f);  // ones row past the channels
+  if (Fi >= HV && c0 + HC == HV) HT[Fi * m.TS + i] = (__bf16)(i < m.P ? 1.f : 0.f);  // ones row past the channels
 }
 
-template <int HV, bool PROF>
-__global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgLayout m, unsigned long long* prof) {
-  constexpr int HC = HV / 2;
+template <int HV, int NL, bool PROF>
+__global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout m, unsigned long long* prof) {
+  // node groups of NL lanes (HV / NL channels each).  NL = 4: 16 waves, so the one workgroup an LDS-full CU holds
+  // still has 4 waves per SIMD to hide the message loops' LDS latency
+  constexpr int HC = HV / NL, NT = 256 * NL;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   bf16x8* frag = reinterpret_cast<bf16x8*>(lds + m.frag);
   float* vec = reinterpret_cast<float*>(lds + m.vec);
@@ -590,15 +657,12 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
   for (int s = 0; s < m.nslots; ++s) lg_zero(lds + m.slot[s], m.P32 * kMfRS * 2);
   lg_zero(lds + m.ht, 32 * m.TS * 2);
   const bool k2b = a.H > 16;
-  // gradient accumulators over all the graphs of this workgroup: per lane (attention vector, output bias; lane
-  // pair = node, 12 channels) and, in waves 0..3, the augmented weight gradients [dW | db] of (block, side)
+  // gradient accumulators over all the graphs of this workgroup: per lane (attention vector, output bias; HC
+  // channels of a node) and, in waves 0..3, the augmented weight gradients [dW | db] of (block, side)
   // (block 1, convs 1 .. L-1: registers for the workgroup's whole run; block 0, conv 0 only: per graph, then
   // summed over the wave's nodes into the wave's own LDS slot -- 24 fewer live registers)
-  float gatt1[HC], gbias1[HC];
-#pragma unroll
-  for (int k = 0; k < HC; ++k) gatt1[k] = gbias1[k] = 0.f;
-  // block 0's [att | bias][32] sums over the workgroup's graphs (thread c owns entry c of each)
-  if (threadIdx.x < 64) reinterpret_cast<float*>(lds + m.acc0)[threadIdx.x] = 0.f;
+  // per-wave [block][att | bias][32] sums over the workgroup's graphs (each wave owns its slots: no barrier)
+  for (int k = threadIdx.x; k < NT / 64 * 128; k += NT) reinterpret_cast<float*>(lds + m.wacc)[k] = 0.f;
   f32x16 accW;
   mf_zero(accW);
   const int wblk = wave >> 1, wside = wave & 1;  // waves 0..3: (block, l | r) of accW
@@ -606,26 +670,20 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
   if (PROF) clk.last = __builtin_amdgcn_s_memtime();
   for (long b = blockIdx.x; b < a.B; b += gridDim.x) {
     const int t = a.topo[b], n = a.nnodes[t];
-    float gatt0[HC], gbias0[HC];
-#pragma unroll
-    for (int k = 0; k < HC; ++k) gatt0[k] = gbias0[k] = 0.f;
     {
-      const int tq = lg_tid(), iq = tq >> 1, hq = tq & 1, cq = hq * HC;
+      const int tq = lg_tid(), iq = tq / NL, hq = tq % NL, cq = hq * HC;
       float xv[8], dy0[HC];
       lg_load_x(xv, a, b, iq, hq);
 #pragma unroll
       for (int k = 0; k < HC; ++k) dy0[k] = (iq < n && cq + k < a.H) ? a.demb[b * a.H + cq + k] / (float)n : 0.f;
       __syncthreads();  // the previous graph is done with every LDS image
       LG_MARK(PROF, clk, 0);
-      lg_stage_topo<true>(a, t, lds, m);
+      lg_stage_topo<true, NT>(a, t, lds, m);
       lg_put_x(reinterpret_cast<__bf16*>(lds + m.slot[m.xs]), xv, iq, hq, m);
-      if (iq < m.P) {  // d emb / n on every real node (no ReLU after the last conv: L >= 2)
-#pragma unroll
-        for (int u = 0; u < HC / 4; ++u)
-          reinterpret_cast<float4*>(DY + iq * m.RS + cq)[u] = float4{dy0[4 * u], dy0[4 * u + 1], dy0[4 * u + 2], dy0[4 * u + 3]};
-      }
+      if (iq < m.P) lg_store_f<HC>(DY + iq * m.RS + cq, dy0);  // d emb / n on every real node (L >= 2: no ReLU)
       __syncthreads();
       LG_MARK(PROF, clk, 1);
+      if (PROF) lg_nanchk(DY, m.P * m.RS, prof, 30);
     }
     const int32_t* iptr = reinterpret_cast<const int32_t*>(lds + m.iptr);
     const uint16_t* isrc = reinterpret_cast<const uint16_t*>(lds + m.isrc);
@@ -638,10 +696,10 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
       lg_linear<HV>(frag, blk, blk ? k2b : false, vb, Sin, XL, XR, m);
       __syncthreads();
       LG_MARK(PROF, clk, 2);
-      const int tq = lg_tid(), pq = tq >> 1, cq = (tq & 1) * HC;
+      const int tq = lg_tid(), pq = tq / NL, cq = (tq % NL) * HC;
       const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
       float y[HC];
-      lg_attend<HC, kLgUf>(y, iq, n, cq, vb, true, XL, XR, iptr, isrc, deg, m);
+      lg_attend<HC, kLgUb, NL>(y, iq, n, cq, cq + HC == HV, vb, true, XL, XR, iptr, isrc, deg, m);
       __syncthreads();
       LG_MARK(PROF, clk, 3);
       if (iq < m.P32) lg_store_bf16<HC>(reinterpret_cast<__bf16*>(lds + m.slot[l]) + iq * kMfRS + cq, y);
@@ -657,8 +715,8 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
       if (l == 0 && a.L >= 2) {  // the input image again (its slot held conv L-2's output meanwhile)
         const int tq = lg_tid();
         float xv[8];
-        lg_load_x(xv, a, b, tq >> 1, tq & 1);
-        lg_put_x(Sin, xv, tq >> 1, tq & 1, m);
+        lg_load_x(xv, a, b, tq / NL, tq % NL);
+        lg_put_x(Sin, xv, tq / NL, tq % NL, m);
         __syncthreads();
         LG_MARK(PROF, clk, 5);
       }
@@ -666,26 +724,44 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
       lg_linear<HV>(frag, blk, blk ? k2b : false, vb, Sin, XL, XR, m);
       {
         const int tq = lg_tid();
-        lg_put_ht<HC>(HT, Sin, tq >> 1, (tq & 1) * HC, Fi, m);
+        lg_put_ht<HC, HV>(HT, Sin, tq / NL, (tq % NL) * HC, Fi, m);
       }
       __syncthreads();
       LG_MARK(PROF, clk, 6);
+      if (PROF) {
+        lg_nanchk(XL, m.P * m.RS, prof, 13);
+        lg_nanchk(XR, m.P * m.RS, prof, 14);
+        lg_nanchk(DY, m.P * m.RS, prof, 15);
+        lg_nanchk(reinterpret_cast<const float*>(HT), 16 * m.TS, prof, 29);
+      }
       // 2 + 3
-      // lane pair p: step 2's target = the node of in-degree rank p, step 3's source = the node of out-degree rank p
-      float dxr[HC], dxl[HC];
+      // node group p: step 2's target = the node of in-degree rank p, step 3's source = the node of out-degree rank p
+      float dxr[HC], dxl[HC], gv[HC];  // gv: this conv's bias, then attention-vector gradient (this lane's share)
       {
-        const int tq = lg_tid(), pq = tq >> 1, hq = tq & 1;
+        const int tq = lg_tid(), pq = tq / NL, cq = (tq % NL) * HC;
         const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
-        if (blk == 0) lg_bwd_targets<HC, kLgUb>(dxr, gbias0, iq, n, hq * HC, hq, vb, lds, m);
-        else lg_bwd_targets<HC, kLgUb>(dxr, gbias1, iq, n, hq * HC, hq, vb, lds, m);
+#pragma unroll
+        for (int k = 0; k < HC; ++k) gv[k] = 0.f;
+        lg_bwd_targets<HC, kLgUb, NL>(dxr, gv, iq, n, cq, cq + HC == HV, vb, lds, m);
+        lg_wave_accum<HC, NL>(reinterpret_cast<float*>(lds + m.wacc) + (wave * 4 + 2 * blk + 1) * 32 + cq, gv, tq & 63);
       }
       __syncthreads();
       LG_MARK(PROF, clk, 7);
       {
-        const int tq = lg_tid(), pq = tq >> 1, hq = tq & 1;
+        const int tq = lg_tid(), pq = tq / NL, cq = (tq % NL) * HC;
         const int jq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[m.P + pq] : pq;
-        if (blk == 0) lg_bwd_sources<HC, kLgUb>(dxl, gatt0, jq, n, hq * HC, vb, lds, m);
-        else lg_bwd_sources<HC, kLgUb>(dxl, gatt1, jq, n, hq * HC, vb, lds, m);
+#pragma unroll
+        for (int k = 0; k < HC; ++k) gv[k] = 0.f;
+        lg_bwd_sources<HC, kLgUb>(dxl, gv, jq, n, cq, vb, lds, m);
+        lg_wave_accum<HC, NL>(reinterpret_cast<float*>(lds + m.wacc) + (wave * 4 + 2 * blk) * 32 + cq, gv, tq & 63);
+      }
+      if (PROF) {
+        for (int k = 0; k < HC; ++k) {
+          if (!isfinite(dxr[k])) atomicAdd(prof + 31, 1ull);
+          if (!isfinite(dxl[k])) atomicAdd(prof + 12, 1ull);
+        }
+        lg_nanchk(reinterpret_cast<const float*>(lds + m.sc), a.M, prof, 6);
+        lg_nanchk(reinterpret_cast<const float*>(lds + m.ds), a.M, prof, 7);
       }
       __syncthreads();  // XL / XR / DY are dead: their region takes DT / DN
       LG_MARK(PROF, clk, 8);
@@ -695,7 +771,7 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
       __bf16* DNl = reinterpret_cast<__bf16*>(lds + m.dnl);
       __bf16* DNr = reinterpret_cast<__bf16*>(lds + m.dnr);
       {
-        const int tq = lg_tid(), pq = tq >> 1, hq = tq & 1, cq = hq * HC;
+        const int tq = lg_tid(), pq = tq / NL, cq = (tq % NL) * HC;
         const uint16_t* ord = reinterpret_cast<const uint16_t*>(lds + m.ord);
         const int iq = pq < m.P ? (int)ord[pq] : pq, jq = pq < m.P ? (int)ord[m.P + pq] : pq;
         if (pq < m.PK) {  // columns P..PK-1: zero (idle lanes hold zeros)
@@ -710,9 +786,12 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
         if (l > 0 && pq < m.P32) {
           lg_store_bf16<HC>(DNl + jq * kMfRS + cq, dxl);
           lg_store_bf16<HC>(DNr + iq * kMfRS + cq, dxr);
-          if (hq == 1 && HV < 32) {  // K columns HV..31 of the dX product: zero (the region held fp32 rows)
-            *reinterpret_cast<bf16x8*>(DNl + jq * kMfRS + 24) = bf16x8{};
-            *reinterpret_cast<bf16x8*>(DNr + iq * kMfRS + 24) = bf16x8{};
+          if (cq + HC == HV) {  // K columns HV..31 of the dX product: zero (the region held fp32 rows)
+#pragma unroll
+            for (int c = HV; c < 32; c += 8) {
+              *reinterpret_cast<bf16x8*>(DNl + jq * kMfRS + c) = bf16x8{};
+              *reinterpret_cast<bf16x8*>(DNr + iq * kMfRS + c) = bf16x8{};
+            }
           }
         }
       }
@@ -764,26 +843,6 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
         LG_MARK(PROF, clk, 11);
       }
     }
-    {  // block 0's per-graph sums: DPP row sums -> red (row partials) -> thread c adds their fixed-order sum into
-       // acc0[which][c] (the last conv's barrier ordered every earlier use of red)
-      const int tq = lg_tid(), cq = (tq & 1) * HC;
-      float* acc0 = reinterpret_cast<float*>(lds + m.acc0);
-      for (int which = 0; which < 2; ++which) {
-#pragma unroll
-        for (int k = 0; k < HC; ++k) {
-          const float v = lg_row_parity_sum(which == 0 ? gatt0[k] : gbias0[k]);
-          if ((tq & 14) == 14) red[(tq >> 4) * 32 + cq + k] = v;
-        }
-        __syncthreads();
-        if (tq < a.H) {
-          float s = 0.f;
-#pragma unroll 8
-          for (int w = 0; w < kLgRows; ++w) s += red[w * 32 + tq];
-          acc0[which * 32 + tq] += s;
-        }
-        __syncthreads();
-      }
-    }
     LG_MARK(PROF, clk, 12);
   }
   if (PROF && threadIdx.x == 0)
@@ -791,7 +850,7 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
   // ---- this workgroup's gradient row (module layout per block: Wl, bl, Wr, br, att, bias)
   float* row = a.partials + (long)blockIdx.x * a.n_params;
   const int H = a.H;
-  const int tid = threadIdx.x, c0 = (tid & 1) * HC, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int tid = threadIdx.x, c0 = (tid % NL) * HC, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   if (wave < 4 && wblk < a.n_blocks) {
     const int Fi = wblk == 0 ? a.Fin : H, o = cl_block_offset(wblk, a.Fin, H) + wside * (H * Fi + H);
 #pragma unroll
@@ -803,26 +862,15 @@ __global__ __launch_bounds__(kLgThreads, 1) void gnn_lg_bwd_kernel(ClArgs a, LgL
       }
     }
   }
-  for (int blk = 0; blk < a.n_blocks; ++blk) {
-    const int Fi = blk == 0 ? a.Fin : H, o = cl_block_offset(blk, a.Fin, H) + 2 * H * Fi + 2 * H;
-    for (int which = 0; which < 2; ++which) {  // att, bias
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < HC; ++k) {
-        if (blk == 1) {
-          const float v = lg_row_parity_sum(which == 0 ? gatt1[k] : gbias1[k]);
-          if ((lane & 14) == 14) red[(tid >> 4) * 32 + c0 + k] = v;
-        }
-      }
-      __syncthreads();
-      if (tid < H) {
+  __syncthreads();
+  if (tid < H) {
+    const float* wacc = reinterpret_cast<const float*>(lds + m.wacc);
+    for (int blk = 0; blk < a.n_blocks; ++blk) {
+      const int Fi = blk == 0 ? a.Fin : H, o = cl_block_offset(blk, a.Fin, H) + 2 * H * Fi + 2 * H;
+      for (int which = 0; which < 2; ++which) {  // att, bias: the waves' slots in a fixed order
         float s = 0.f;
-        if (blk == 1) {
-#pragma unroll 8
-          for (int w = 0; w < kLgRows; ++w) s += red[w * 32 + tid];
-        } else {
-          s = reinterpret_cast<const float*>(lds + m.acc0)[which * 32 + tid];
-        }
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) s += wacc[(w * 4 + 2 * blk + which) * 32 + tid];
         row[o + which * H + tid] = s;
       }
     }
@@ -861,7 +909,6 @@ static LgLayout lg_layout(const ClArgs& a, int HV, bool bwd) {
     m.odst = take(M * 2);
     m.sc = take(M * 4);
     m.ds = take(M * 4);
-    m.zb = take(M * 4);
   }
   for (int s = 0; s < m.nslots; ++s) m.slot[s] = take(m.P32 * kMfRS * 2);
   const long fb = ((long)m.P * m.RS * 4 + 15) & ~15L;
@@ -876,8 +923,8 @@ static LgLayout lg_layout(const ClArgs& a, int HV, bool bwd) {
   m.dnl = m.R + 2 * (int)dt;
   m.dnr = m.R + 2 * (int)dt + (int)dn;
   if (bwd) m.ht = take(dt);
-  m.red = take(kLgRows * 32 * 4);
-  if (bwd) m.acc0 = take(64 * 4);
+  m.red = take((bwd ? kLgBwdThreads : kLgThreads) / 64 * 32 * 4);  // one 32-channel partial per wave
+  if (bwd) m.wacc = take(kLgBwdThreads / 64 * 128 * 4);
   m.total = o;
   return m;
 }
@@ -942,14 +989,34 @@ static int lg_launch_bwd(const ClArgs& a, hipStream_t st, int cus, int max_rows)
   const size_t lds = m.total;
   GSC_CHECK(lds <= 160 * 1024, "GNN (large-graph fused) backward working set exceeds LDS");
   const bool prof = lg_prof_on();
-  const void* fn = prof ? (const void*)gnn_lg_bwd_kernel<HV, true> : (const void*)gnn_lg_bwd_kernel<HV, false>;
+  const char* e = getenv("GSC_LG_BWD_NL");
+  const bool nl2 = e && e[0] == '2';
+  const void* fn = nl2 ? (prof ? (const void*)gnn_lg_bwd_kernel<HV, 2, true> : (const void*)gnn_lg_bwd_kernel<HV, 2, false>)
+                       : (prof ? (const void*)gnn_lg_bwd_kernel<HV, 4, true> : (const void*)gnn_lg_bwd_kernel<HV, 4, false>);
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   long grid = cus;
   if (grid > a.B) grid = a.B;
   if (grid > max_rows) grid = max_rows;
   if (grid < 1) grid = 1;
-  if (prof) hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, true>), dim3((unsigned)grid), dim3(kLgThreads), lds, st, a, m, g_lg_prof);
-  else hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, false>), dim3((unsigned)grid), dim3(kLgThreads), lds, st, a, m, nullptr);
+  const dim3 blk(nl2 ? 512 : kLgBwdThreads);
+  {  // a launch the device cannot run (LDS, threads x registers) must fail loudly, not leave the partials unwritten
+    hipFuncAttributes fa{};
+    GSC_HIP_CHECK(hipFuncGetAttributes(&fa, fn));
+    int dev = 0, maxlds = 0;
+    GSC_HIP_CHECK(hipGetDevice(&dev));
+    GSC_HIP_CHECK(hipDeviceGetAttribute(&maxlds, hipDeviceAttributeSharedMemPerBlockOptin, dev));
+    GSC_CHECK(fa.maxThreadsPerBlock >= (int)blk.x && (int)lds <= maxlds,
+              "large-graph GNN backward: " + std::to_string(blk.x) + " threads / " + std::to_string(lds) +
+                  " B LDS exceed the kernel's limits (" + std::to_string(fa.maxThreadsPerBlock) + " threads, " +
+                  std::to_string(maxlds) + " B)");
+  }
+  if (nl2) {
+    if (prof) hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, 2, true>), dim3((unsigned)grid), blk, lds, st, a, m, g_lg_prof);
+    else hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, 2, false>), dim3((unsigned)grid), blk, lds, st, a, m, nullptr);
+  } else {
+    if (prof) hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, 4, true>), dim3((unsigned)grid), blk, lds, st, a, m, g_lg_prof);
+    else hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, 4, false>), dim3((unsigned)grid), blk, lds, st, a, m, nullptr);
+  }
   check_launch();
   return (int)grid;
 }

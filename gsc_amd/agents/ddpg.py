@@ -32,6 +32,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from gsc_amd.envs.common import schedule_threshold
 from gsc_amd.models import Actor, GraphSet, QNetwork
 from gsc_amd.ops import FlatParams, FusedAdamPolyak, explore_postprocess
 from gsc_amd.parallel.dist import DistInfo, allreduce_sum_, broadcast_tensors
@@ -521,6 +522,7 @@ class BatchedTrainer:
         self._warmup_steps = max(int(self.learning_starts), 1)
         self.rand_mu = float(cfg.get("rand_mu", 0.0))
         self.rand_sigma = float(cfg.get("rand_sigma", 0.3))
+        self.sched_thr = schedule_threshold(cfg, sim.n_pad)  # reference 0.1 unless the config opts in
         self.global_step = 0
         self.episode = 0
         self.schedule = list(network_schedule) if network_schedule else [0]
@@ -735,6 +737,7 @@ class BatchedTrainer:
             self._pmask_ready = pm is not None
             return explore_postprocess(mu, self.masks, self.sim.n_pad, warm, self.rand_mu, self.rand_sigma,
                                        seed=self.t.seed * 131 + self.dist.rank, step=self.global_step,
+                                       threshold=self.sched_thr,
                                        out=self._act_bufs[k], topo=topo, pmask=pm)
 
     def _check_handoff(self) -> None:

@@ -33,7 +33,7 @@ import torch
 from tqdm import tqdm
 
 from gsc_amd.coordsim import reader
-from gsc_amd.envs.common import threshold_normalize
+from gsc_amd.envs.common import schedule_threshold, threshold_normalize
 from gsc_amd.envs.graph import GraphObs
 from gsc_amd.models import GraphSet
 from gsc_amd.parallel.dist import DistInfo
@@ -163,7 +163,7 @@ class SimpleDDPG(RLSPAgent):
         return np.clip(self.actor.unscale_action(scaled), 0.0, 1.0)
 
     def post_process_actions(self, action: np.ndarray) -> np.ndarray:
-        return threshold_normalize(action, self.n_pad, SCHEDULE_THRESHOLD, passes=2)
+        return threshold_normalize(action, self.n_pad, schedule_threshold(self.cfg, self.n_pad), passes=2)
 
     # ------------------------------------------------------------------------------------------
     # training

@@ -27,6 +27,28 @@ def normalize_scheduling_probabilities(input_list) -> list:
     return out
 
 
+REFERENCE_SCHEDULE_THRESHOLD = 0.1  # src/rlsp/agents/simple_ddpg.py:130
+
+
+def schedule_threshold(cfg: dict, n_pad: int) -> float:
+    """Post-processing threshold of the schedule rows.  Default: the reference's fixed 0.1
+    (``simple_ddpg.py:130``).  Opt-in agent key ``schedule_threshold`` (new; docs/DEVIATIONS.md): a float, or
+    ``auto`` = 0.1 * 24 / n_pad -- the reference's value at its 24-node padding, scaled with 1/n so that a row of
+    ~n comparable weights (each ~1/n after normalising) is not zeroed wholesale at 50-200 nodes, which turns every
+    row into the uniform schedule and leaves the critic no action variation (profiles/learning_curves.md)."""
+    v = cfg.get("schedule_threshold", None)
+    if v is None:
+        return REFERENCE_SCHEDULE_THRESHOLD
+    if isinstance(v, str):
+        if v.strip().lower() == "auto":
+            return REFERENCE_SCHEDULE_THRESHOLD if n_pad <= 24 else 2.4 / float(n_pad)
+        v = float(v)
+    v = float(v)
+    if not 0.0 <= v < 1.0:
+        raise ValueError(f"schedule_threshold must be in [0, 1) or 'auto', got {v}")
+    return v
+
+
 def threshold_normalize(action: np.ndarray, slice_len: int, threshold: float = 0.1, passes: int = 2) -> np.ndarray:
     """Per slice of ``slice_len``: zero entries below ``threshold`` then normalise; repeated ``passes`` times.
 

@@ -76,32 +76,44 @@ def uniform_rows(act, masks, topo, n_pad):
     return float((uni & real).sum()) / max(float(real.sum()), 1.0)
 
 
-def evaluate(policy, cfg, pre, E, seed, learner=None, dev="cuda"):
-    """Success ratio and mean return of ``policy`` over E test episodes (one per env) on the held-out topology."""
+def evaluate(policy, cfg, net, pre, E, seed, learner=None, dev="cuda"):
+    """Success ratio and mean return of ``policy`` over E test episodes (one per env) on topology ``net``.
+
+    trained     greedy actor, post-processed like training actions (threshold / normalise)
+    trained_raw greedy actor, raw weights (the reference's test path: no noise, no post-processing, Q7)
+    noisy       actor + the training exploration noise, post-processed (the behaviour policy)
+    random      uniform random weights per destination, post-processed (the warm-up policy)
+    uniform     equal weights on every real destination"""
     import torch
+    from gsc_amd.envs.common import schedule_threshold
     from gsc_amd.models.graphs import GraphSet
     from gsc_amd.native import load
     from gsc_amd.ops.explore import explore_postprocess
     from gsc_amd.sim.batched import load_batched_from_paths
-    sim = load_batched_from_paths([pre["test"]], pre["service"], pre["sim"], cfg, E, device=dev, seed=seed)
+    sim = load_batched_from_paths([net], pre["service"], pre["sim"], cfg, E, device=dev, seed=seed)
     obs = sim.reset().clone()
     graphs = GraphSet(sim.topologies, sim.n_pad, sim.device)
     masks = graphs.action_masks(sim.C, sim.F)
+    thr = schedule_threshold(cfg, sim.n_pad)
     topo = torch.zeros(E, dtype=torch.int64, device=dev)
     acc = torch.zeros(4, dtype=torch.float64, device=dev)
     nat = load()
     uni = []
+    sigma = float(cfg.get("rand_sigma", 0.3))
     for step in range(sim.episode_steps):
-        if policy == "trained":
+        pp = dict(seed=seed, step=step, topo=topo, threshold=thr)
+        if policy in ("trained", "trained_raw", "noisy"):
             with learner._autocast(), torch.no_grad():
                 mu = learner.actor(obs, topo, graphs, masks).float()
-            act = explore_postprocess(mu, masks, sim.n_pad, False, 0.0, 0.0, seed=seed, step=step, topo=topo)
+            if policy == "trained_raw":
+                act = (mu * masks[topo]).contiguous()
+            else:
+                act = explore_postprocess(mu, masks, sim.n_pad, False, 0.0, sigma if policy == "noisy" else 0.0, **pp)
         elif policy == "random":
             mu = torch.zeros(E, sim.action_dim, device=dev)
-            act = explore_postprocess(mu, masks, sim.n_pad, True, 0.0, 0.0, seed=seed + 17, step=step, topo=topo)
+            act = explore_postprocess(mu, masks, sim.n_pad, True, 0.0, 0.0, **dict(pp, seed=seed + 17))
         else:  # uniform: equal weights on the real destinations
-            act = explore_postprocess(masks[topo].contiguous(), masks, sim.n_pad, False, 0.0, 0.0, seed=seed,
-                                      step=step, topo=topo)
+            act = explore_postprocess(masks[topo].contiguous(), masks, sim.n_pad, False, 0.0, 0.0, **pp)
         uni.append(uniform_rows(act, masks, topo, sim.n_pad))
         out = sim.step(act, buffer_set=step & 1)
         st = out.stats
@@ -112,8 +124,8 @@ def evaluate(policy, cfg, pre, E, seed, learner=None, dev="cuda"):
         torch.cuda.synchronize()
     sim.check_flags()
     s, d, r, e = [float(v) for v in acc.cpu()]
-    return {"success_ratio": s / max(s + d, 1.0), "episodes": int(e), "mean_return": r / max(e, 1.0),
-            "succ": s, "drop": d, "uniform_rows": round(sum(uni) / len(uni), 4)}
+    return {"success_ratio": round(s / max(s + d, 1.0), 4), "episodes": int(e), "mean_return": round(r / max(e, 1.0), 3),
+            "uniform_rows": round(sum(uni) / len(uni), 4)}
 
 
 def main():
@@ -124,6 +136,9 @@ def main():
     ap.add_argument("--train-steps", type=int, default=8000, help="lockstep steps of --envs envs")
     ap.add_argument("--eval-envs", type=int, default=64, help="test episodes on the held-out topology")
     ap.add_argument("--episode-steps", type=int, default=None)
+    ap.add_argument("--schedule-threshold", default=None,
+                    help="opt-in post-processing threshold (float or 'auto' = 2.4 / n_pad); default: the reference's 0.1")
+    ap.add_argument("--on-train", action="store_true", help="also evaluate every policy on each training network")
     a = ap.parse_args()
     import torch
     import yaml
@@ -135,12 +150,18 @@ def main():
     cfg = yaml.safe_load(open(pre["agent"]))
     cfg["actor_output_activation"] = "sigmoid"
     cfg["episode_steps"] = int(a.episode_steps or pre["episode_steps"])
+    if a.schedule_threshold is not None:
+        cfg["schedule_threshold"] = a.schedule_threshold
     torch.manual_seed(a.seed)
     res = {"preset": a.preset, "seed": a.seed, "train": [os.path.basename(p) for p in pre["train"]],
-           "test": os.path.basename(pre["test"]), "episode_steps": cfg["episode_steps"]}
+           "test": os.path.basename(pre["test"]), "episode_steps": cfg["episode_steps"],
+           "schedule_threshold": cfg.get("schedule_threshold", 0.1)}
+    nets = [pre["test"]] + (list(pre["train"]) if a.on_train else [])
+    evals = {os.path.basename(n): {} for n in nets}
     # baselines first (independent of training)
-    for pol in ("random", "uniform"):
-        res[pol] = evaluate(pol, cfg, pre, a.eval_envs, 1000 + a.seed, dev=dev)
+    for n in nets:
+        for pol in ("random", "uniform"):
+            evals[os.path.basename(n)][pol] = evaluate(pol, cfg, n, pre, a.eval_envs, 1000 + a.seed, dev=dev)
     sim = load_batched_from_paths(pre["train"], pre["service"], pre["sim"], cfg, a.envs, device=dev, seed=a.seed)
     T = len(pre["train"])
     tr = BatchedTrainer(cfg, sim, TrainerConfig(num_envs=a.envs, seed=a.seed, check_every=0),
@@ -163,7 +184,11 @@ def main():
     res["train_env_steps"] = a.train_steps * a.envs
     res["train_curve_every_10_episodes"] = curve
     res["train_uniform_rows"] = round(sum(uni) / max(len(uni), 1), 4)
-    res["trained"] = evaluate("trained", cfg, pre, a.eval_envs, 1000 + a.seed, learner=tr.learner, dev=dev)
+    for n in nets:
+        for pol in ("trained", "trained_raw", "noisy"):
+            evals[os.path.basename(n)][pol] = evaluate(pol, cfg, n, pre, a.eval_envs, 1000 + a.seed, learner=tr.learner,
+                                                       dev=dev)
+    res["eval"] = evals
     print(json.dumps(res), flush=True)
 
 
