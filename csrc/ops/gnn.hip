@@ -184,6 +184,12 @@ static void mt_forward_queued(ClArgs c, uintptr_t stream) {
   }
 }
 
+// Large-graph forward: the same overlap-mode work queue (full-device grid claiming graphs)
+static void lg_forward_queued(ClArgs c, uintptr_t stream) {
+  c.work = work_slot(stream_of(stream));
+  gnn_lg_forward(&c, stream, c.work ? device_cus() : num_cus());
+}
+
 void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo, uintptr_t emb, int B, int P, int Fin,
                  int H, std::vector<int> layer_of, uintptr_t stream, uintptr_t blob) {
   GnnPath path;
@@ -191,7 +197,7 @@ void gnn_forward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo,
   c.emb = ptr<float>(emb);
   c.blob = reinterpret_cast<void*>(blob);
   if (path == kPathMf) gnn_mf_forward(&c, stream, num_cus());
-  else if (path == kPathLg) gnn_lg_forward(&c, stream, num_cus());
+  else if (path == kPathLg) lg_forward_queued(c, stream);
   else mt_forward_queued(c, stream);
 }
 
@@ -211,10 +217,10 @@ void gnn_forward2(py::dict tables, uintptr_t params, uintptr_t params2, uintptr_
     return;
   }
   if (path == kPathLg) {
-    gnn_lg_forward(&c, stream, num_cus());
+    lg_forward_queued(c, stream);
     c.params = ptr<const float>(params2);
     c.emb = ptr<float>(emb2);
-    gnn_lg_forward(&c, stream, num_cus());
+    lg_forward_queued(c, stream);
     return;
   }
   mt_forward_queued(c, stream);
@@ -234,8 +240,9 @@ void gnn_backward(py::dict tables, uintptr_t params, uintptr_t x, uintptr_t topo
   int rows;
   if (path == kPathMf) {
     rows = gnn_mf_backward(&c, stream, num_cus(), max_rows);
-  } else if (path == kPathLg) {
-    rows = gnn_lg_backward(&c, stream, num_cus(), max_rows);  // recomputes the forward: no saved state
+  } else if (path == kPathLg) {  // recomputes the forward: no saved state; work queue in overlap mode
+    c.work = work_slot(stream_of(stream));
+    rows = gnn_lg_backward(&c, stream, c.work ? device_cus() : num_cus(), max_rows);
   } else if ((c.work = work_slot(stream_of(stream))) != nullptr) {
     // CU-masked partner stream (overlap mode): the grid spans every CU and claims graphs from a counter,
     // so the CUs the simulator releases mid-kernel join in (a fixed-stride grid sized to the budget left

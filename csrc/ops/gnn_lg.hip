@@ -51,7 +51,7 @@ constexpr int kLgUb = 2;  // ... in the backward's row-reading loops  // message
 struct LgLayout {
   int P, P32, PK, RS, TS, L, nslots, xs;
   int frag, vec, ord, iptr, deg, isrc, optr, oq, odst, sc, ds, zb, slot[kClMaxLayers], R, xl, xr, dy, dtl, dtr, dnl, dnr, ht,
-      red, acc0, wacc, total;
+      red, acc0, wacc, wq, total;
 };
 
 // thread id through an opaque asm: the LDS addresses derived from it are recomputed at their use instead of
@@ -356,6 +356,15 @@ __device__ __forceinline__ void lg_put_x(__bf16* S, const float (&xv)[8], int i,
   }
 }
 
+// Next graph of this workgroup (every thread calls; one barrier): fixed stride, or -- a.work set (overlap mode: a
+// zeroed counter, full-device grid) -- claimed from the counter, so CUs the simulator frees mid-kernel join in
+// (per-workgroup gradient rows then depend on the claim order: summation order, not values, varies)
+__device__ __forceinline__ long lg_next_graph(const ClArgs& a, int* slot, long cur) {
+  if (threadIdx.x == 0) *slot = a.work ? atomicAdd(a.work, 1) : (int)(cur < 0 ? (long)blockIdx.x : cur + gridDim.x);
+  __syncthreads();
+  return *slot;
+}
+
 __device__ __forceinline__ void lg_zero(char* p, int bytes) {
   for (int k = 16 * threadIdx.x; k < bytes; k += 16 * blockDim.x) *reinterpret_cast<float4*>(p + k) = float4{0, 0, 0, 0};
 }
@@ -380,7 +389,8 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
   const bool k2b = a.H > 16;
   LgClock clk{};
   if (PROF) clk.last = __builtin_amdgcn_s_memtime();
-  for (long b = blockIdx.x; b < a.B; b += gridDim.x) {
+  int* wq = reinterpret_cast<int*>(lds + m.wq);
+  for (long b = lg_next_graph(a, wq, -1); b < a.B; b = lg_next_graph(a, wq, b)) {
     const int t = a.topo[b], n = a.nnodes[t];
     {
       const int tq = lg_tid();
@@ -668,7 +678,8 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
   const int wblk = wave >> 1, wside = wave & 1;  // waves 0..3: (block, l | r) of accW
   LgClock clk{};
   if (PROF) clk.last = __builtin_amdgcn_s_memtime();
-  for (long b = blockIdx.x; b < a.B; b += gridDim.x) {
+  int* wq = reinterpret_cast<int*>(lds + m.wq);
+  for (long b = lg_next_graph(a, wq, -1); b < a.B; b = lg_next_graph(a, wq, b)) {
     const int t = a.topo[b], n = a.nnodes[t];
     {
       const int tq = lg_tid(), iq = tq / NL, hq = tq % NL, cq = hq * HC;
@@ -924,6 +935,7 @@ static LgLayout lg_layout(const ClArgs& a, int HV, bool bwd) {
   m.dnr = m.R + 2 * (int)dt + (int)dn;
   if (bwd) m.ht = take(dt);
   m.red = take((bwd ? kLgBwdThreads : kLgThreads) / 64 * 32 * 4);  // one 32-channel partial per wave
+  m.wq = take(16);
   if (bwd) m.wacc = take(kLgBwdThreads / 64 * 128 * 4);
   m.total = o;
   return m;
