@@ -45,8 +45,8 @@ constexpr int kLgThreads = 512;  // 8 waves: 256 lane pairs = up to 256 nodes, 8
 constexpr int kLgMaxNodes = 256;
 constexpr int kLgBwdThreads = 1024;  // backward: 16 waves, 4 lanes per node
 constexpr float kLgSlope = 0.2f;
-constexpr int kLgUf = 2;
-constexpr int kLgUb = 2;  // ... in the backward's row-reading loops  // messages per chunk in the forward attention loop (registers: 4 waves / SIMD)
+constexpr int kLgUf = 2;  // messages per chunk in the forward attention loop (registers: 4 waves / SIMD)
+constexpr int kLgUb = 2;  // ... in the backward's row-reading loops
 
 struct LgLayout {
   int P, P32, PK, RS, TS, L, nslots, xs;
@@ -77,12 +77,7 @@ struct LgClock {
     }                                                          \
   } while (0)
 static unsigned long long* g_lg_prof = nullptr;
-// PROF variants only (debug): count non-finite fp32 words of an LDS region into prof[slot]
-__device__ __forceinline__ void lg_nanchk(const float* p, int n, unsigned long long* prof, int slot) {
-  unsigned c = 0;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) c += !isfinite(p[k]);
-  if (c) atomicAdd(prof + slot, (unsigned long long)c);
-}
+
 
 // Lane groups: NL consecutive lanes (2 or 4) hold one node, HV / NL channels each.
 // Sum over the node's NL lanes (the score's / dalpha's channel sum): DPP quad permutations, no LDS
@@ -694,7 +689,6 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
       if (iq < m.P) lg_store_f<HC>(DY + iq * m.RS + cq, dy0);  // d emb / n on every real node (L >= 2: no ReLU)
       __syncthreads();
       LG_MARK(PROF, clk, 1);
-      if (PROF) lg_nanchk(DY, m.P * m.RS, prof, 30);
     }
     const int32_t* iptr = reinterpret_cast<const int32_t*>(lds + m.iptr);
     const uint16_t* isrc = reinterpret_cast<const uint16_t*>(lds + m.isrc);
@@ -739,12 +733,6 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
       }
       __syncthreads();
       LG_MARK(PROF, clk, 6);
-      if (PROF) {
-        lg_nanchk(XL, m.P * m.RS, prof, 13);
-        lg_nanchk(XR, m.P * m.RS, prof, 14);
-        lg_nanchk(DY, m.P * m.RS, prof, 15);
-        lg_nanchk(reinterpret_cast<const float*>(HT), 16 * m.TS, prof, 29);
-      }
       // 2 + 3
       // node group p: step 2's target = the node of in-degree rank p, step 3's source = the node of out-degree rank p
       float dxr[HC], dxl[HC], gv[HC];  // gv: this conv's bias, then attention-vector gradient (this lane's share)
@@ -765,14 +753,6 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
         for (int k = 0; k < HC; ++k) gv[k] = 0.f;
         lg_bwd_sources<HC, kLgUb>(dxl, gv, jq, n, cq, vb, lds, m);
         lg_wave_accum<HC, NL>(reinterpret_cast<float*>(lds + m.wacc) + (wave * 4 + 2 * blk) * 32 + cq, gv, tq & 63);
-      }
-      if (PROF) {
-        for (int k = 0; k < HC; ++k) {
-          if (!isfinite(dxr[k])) atomicAdd(prof + 31, 1ull);
-          if (!isfinite(dxl[k])) atomicAdd(prof + 12, 1ull);
-        }
-        lg_nanchk(reinterpret_cast<const float*>(lds + m.sc), a.M, prof, 6);
-        lg_nanchk(reinterpret_cast<const float*>(lds + m.ds), a.M, prof, 7);
       }
       __syncthreads();  // XL / XR / DY are dead: their region takes DT / DN
       LG_MARK(PROF, clk, 8);

@@ -99,7 +99,8 @@ def test_lg_deterministic_and_forward2():
 
 
 def test_lg_cu_budget_grid():
-    """A CU budget (the trainer's masked learner stream) sizes the persistent backward grid; same numerics."""
+    """A CU budget (the trainer's masked learner stream) switches both kernels to the full-device grid claiming
+    graphs from a zeroed work-queue counter (csrc/ops/gnn.hip::work_slot); same numerics."""
     from gsc_amd.native import load
     nat = load()
     nat.gnn_set_cu_budget(48)
