@@ -9,8 +9,9 @@ small all-reduce.  The reference is single-process (SURVEY.md section 2.8, D1/D7
 new capability.
 
 ``GSC_DIST_FORCE=1`` with a single process builds a world-size-1 process group (RCCL on a GPU, gloo on the
-CPU) and routes every collective through it: the data-parallel code path (five captured graphs with eager
-collectives between them, ZeRO-1 reduce-scatter / all-gather, replica checks) then runs on one GPU,
+CPU) and routes every collective through it: the data-parallel code path (the gradient all-reduces captured
+in the update graph, or the fallback's eager collectives between five per-stage graphs, ZeRO-1
+reduce-scatter / all-gather, replica checks) then runs on one GPU,
 bit-identical to the process-local learner.  ``GSC_DP_GRAD_BF16=1`` all-reduces gradients in bf16 (half
 the xGMI bytes; fp32 master weights and Adam are unchanged, see ``GradReduce``).
 """

@@ -3,7 +3,8 @@
 world-size-1 ``nccl`` process group).
 
 Every collective of the DP path is issued through RCCL: the parameter broadcast, the critic / actor-MLP /
-actor-embedder gradient all-reduces between the five captured HIP graphs of ``update_graphed``, the ZeRO-1
+actor-embedder gradient all-reduces captured inside the one HIP graph of ``update_graphed`` (and, with
+``GSC_DP_GRAPH=0``, issued eagerly between five per-stage graphs), the ZeRO-1
 reduce-scatter / all-gather and its guard agreement, and (with ``--bf16``) the bf16 gradient all-reduce.
 With one rank every collective is an identity, so the result must equal the process-local learner
 (one captured graph, no collectives) bit for bit.
@@ -58,11 +59,16 @@ def main():
 
     ref = run(None)                       # process-local: one graph, no collectives
     res["ref_graphs"] = len(ref._graphs)
-    D = run(info)                         # DP path over RCCL: five graphs, all-reduces between them
+    D = run(info)                         # DP path over RCCL: all-reduces captured in the update graph
     res["dp_graphs"] = len(D._graphs)
     res["dp_bitwise"] = all(torch.equal(a, b) for a, b in zip(flats(D), flats(ref)))
     res["dp_grad_bitwise"] = (torch.equal(D.critic_flat.grad, ref.critic_flat.grad)
                               and torch.equal(D.actor_flat.grad, ref.actor_flat.grad))
+    os.environ["GSC_DP_GRAPH"] = "0"      # fallback: five graphs, eager all-reduces between them
+    E = run(info)
+    os.environ.pop("GSC_DP_GRAPH")
+    res["eager_graphs"] = len(E._graphs)
+    res["eager_bitwise"] = all(torch.equal(a, b) for a, b in zip(flats(E), flats(ref)))
     Z = run(info, zero=True)              # ZeRO-1 over RCCL (reduce-scatter, Adam on the shard, all-gather)
     pz, pr = per_param(Z), per_param(ref)
     dz = torch.cat([(pz[k] - pr[k]).abs().view(-1) for k in pr])

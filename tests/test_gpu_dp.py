@@ -42,9 +42,10 @@ def test_two_ranks_one_gpu_graphed_dp():
 
 
 def test_rccl_world1_dp_path_bit_identical():
-    """GSC_DIST_FORCE=1: a world-size-1 RCCL communicator carries every collective of the DP path (five
-    captured update graphs with all-reduces between them, ZeRO-1 reduce-scatter / all-gather, bf16
-    gradient all-reduce); with one rank the DP learner equals the process-local learner bit for bit."""
+    """GSC_DIST_FORCE=1: a world-size-1 RCCL communicator carries every collective of the DP path (the
+    gradient all-reduces captured in the one update graph; the fallback's five graphs with eager all-reduces
+    between them; ZeRO-1 reduce-scatter / all-gather; bf16 gradient all-reduce); with one rank the DP learner
+    equals the process-local learner bit for bit."""
     env = {**os.environ, "GSC_DIST_FORCE": "1", "OMP_NUM_THREADS": "2"}
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GSC_DIST_BACKEND", "GSC_DP_GRAD_BF16"):
         env.pop(k, None)
@@ -54,15 +55,15 @@ def test_rccl_world1_dp_path_bit_identical():
     res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
     print(res)
     assert res["backend"] == "nccl" and res["world"] == 1 and res["forced"]
-    assert res["ref_graphs"] == 1 and res["dp_graphs"] == 5
-    assert res["dp_bitwise"] and res["dp_grad_bitwise"], res
+    assert res["ref_graphs"] == 1 and res["dp_graphs"] == 1 and res["eager_graphs"] == 5
+    assert res["dp_bitwise"] and res["dp_grad_bitwise"] and res["eager_bitwise"], res
     assert res["zero"] and res["zero_max_abs_diff"] < 1e-6, res
     assert res["bf16"] and res["bf16_max_abs_diff"] < 4 * 1e-3, res
 
 
 def test_rccl_world1_bench_check_replicas():
     """bench.py's --check-replicas over the forced world-size-1 RCCL group, with the simulator on its
-    CU-masked stream and the learner's collectives issued between its captured graphs."""
+    CU-masked stream and the learner's collectives captured in its update graph."""
     env = {**os.environ, "GSC_DIST_FORCE": "1"}
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GSC_DIST_BACKEND"):
         env.pop(k, None)
