@@ -19,6 +19,8 @@
 // its fragments are read: the dense passes streamed 18.4 GB each at syn200, these read 2.2 GB of records.
 #include <pybind11/pybind11.h>
 
+#include <type_traits>
+
 #include "../common.h"
 
 namespace py = pybind11;
@@ -87,20 +89,30 @@ __global__ __launch_bounds__(256) void sparse_compress_kernel(const float* __res
   }
 }
 
-// ---- critic products on the records: dense MFMA tiles expanded in LDS --------------------------------------------
-// A row record expands to its P bf16 values (base below P, exceptions on top) with ~P/8 16-byte LDS stores and at
-// most 11 two-byte ones, far cheaper per element than the 32x32x16 MFMA work it feeds (64 outputs per element), so
-// both products run as bf16 MFMA GEMMs over one row block at a time: the replayed [B, A] block is never formed in
-// memory (86 KB per transition read instead of 720 KB) and the MFMA time (B A c1 2 FLOP per pass) is the bound.
+// ---- critic products on the records: base column + sparse deltas in persistent LDS images ----------------------
+// A row record is a rank-one part plus at most 11 point deltas: a[d] = base + delta[d], delta = v - base at the
+// listed exceptions and zero elsewhere.  Both products run as bf16 MFMA GEMMs over one row block at a time on
+// images that hold only the deltas plus ONE extra K column with the base value:
+//
+//   h[b] += sum_d a[b,d] W[:,d] = sum_d delta[b,d] W[:,d] + base_b * Wsum      (Wsum = sum_{d<P} W[:,d], per block)
+//   dW[:,d] = sum_b dh0[b] a[b,d] = sum_b dh0[b] delta[b,d] + G,  G = sum_b dh0[b] base_b (the base column's output)
+//
+// The sample images stay zero between blocks: a lane writes its <= 11 deltas and its base column, the MFMAs read
+// the image, and the same lane writes the deltas' positions back to zero -- ~24 two-byte LDS stores per sample
+// and block instead of re-expanding the whole P-wide row (25 sixteen-byte stores at P = 200 plus the exceptions),
+// which left the expansion and its barriers, not the MFMA, as the bound (round 5: sparse_fwd 3.0 ms, sparse_wgrad
+// 3.6 ms of the syn200 step at 13-20 % of MFMA peak).  Wsum enters the forward as two bf16 columns (hi + lo part,
+// each multiplied by base: ~2^-17 relative), computed per call by sparse_wsum_kernel.  delta = v - base is rounded
+// to bf16 (exact for the sparse rows, base 0; one bf16 rounding of the residual on uniform rows).
 typedef __attribute__((ext_vector_type(8))) __bf16 sp_bf16x8;
 typedef __attribute__((ext_vector_type(16))) float sp_f32x16;
 typedef __attribute__((ext_vector_type(8))) short sp_s16x8;
 typedef __attribute__((ext_vector_type(4))) short sp_s16x4;
 typedef __attribute__((address_space(3))) sp_s16x4 sp_lds_s16x4;
 
-constexpr int kSpC1 = 64;      // critic first-layer width (both products)
-constexpr int kSpMaxFwdP = 240;  // forward LDS: 5 x [64][LD] bf16 images within 160 KB
-constexpr int kSpBK = 64;      // samples per K step of the weight gradient
+constexpr int kSpC1 = 64;        // critic first-layer width (both products)
+constexpr int kSpMaxP = 238;     // forward LDS: 5 x [64][LD] bf16 images within 160 KB (K = P + 2 base columns)
+constexpr int kSpBK = 64;        // samples per K step of the weight gradient
 
 __device__ __forceinline__ sp_f32x16 sp_mma(const sp_s16x8& a, const sp_s16x8& b, const sp_f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(sp_bf16x8, a), __builtin_bit_cast(sp_bf16x8, b), c,
@@ -111,6 +123,10 @@ __device__ __forceinline__ sp_f32x16 sp_mma(const sp_s16x8& a, const sp_s16x8& b
 __host__ __device__ __forceinline__ int sp_ld_k(int Kp) { return (Kp / 8) % 2 ? Kp : Kp + 8; }
 // M/N-contiguous image row stride for ds_read_b64_tr_b16 fragments: 2 LD mod 256 bytes in {64, 192}
 __host__ __device__ __forceinline__ int sp_ld_tr(int C) { return (C / 32) % 2 ? C : C + 32; }
+// forward K extent: P destinations + the two base columns, in whole 16-column MFMA steps
+__host__ __device__ __forceinline__ int sp_kp_fwd(int P) { return (P + 2 + 15) & ~15; }
+// weight-gradient N extent: P destinations + the base column, in whole 32-column tiles
+__host__ __device__ __forceinline__ int sp_np_wgrad(int P) { return (P + 1 + 31) & ~31; }
 
 // 32x32x16 fragment of a [k][c] (M/N-contiguous) image: lane = column (c0 + lane & 31), 8 k values (mlp.hip frag)
 __device__ __forceinline__ sp_s16x8 sp_frag_tr(const short* img, int LD, int c0, int s, int lane) {
@@ -124,35 +140,18 @@ __device__ __forceinline__ sp_s16x8 sp_frag_tr(const short* img, int LD, int c0,
 
 typedef __attribute__((ext_vector_type(4))) uint32_t sp_u32x4;  // 16-byte LDS stores (ds_write_b128)
 
-// Expand a record into chunks [ch0, ch1) (8 columns each) of an LDS row: base below P, zero from P on, then the
-// record's exceptions inside the range (same lane, program order: they land after the base stores).  Row strides
-// of 4 x odd dwords put the 8 lanes of a ds_write_b128 group on distinct bank quads.
-__device__ __forceinline__ void sp_expand(short* row, const uint4& w0, const uint4& w1, const uint4& w2, int P,
-                                          int ch0, int ch1) {
-  const uint32_t head = w0.x, base = head & 0xffffu;
-  const int cnt = (int)(head >> 16);
-  const uint32_t bb = base | (base << 16);
-  const int full = min(ch1, P >> 3);
-  int c = ch0;
-  for (; c < full; ++c) *reinterpret_cast<sp_u32x4*>(row + 8 * c) = sp_u32x4{bb, bb, bb, bb};
-  for (; c < ch1; ++c) {  // the chunk holding column P (P % 8 != 0) and the zero padding after it
-    sp_u32x4 v;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      v[j] = (8 * c + 2 * j < P ? base : 0u) | ((8 * c + 2 * j + 1 < P ? base : 0u) << 16);
-    *reinterpret_cast<sp_u32x4*>(row + 8 * c) = v;
-  }
+// slot k of a record held as three uint4 (header word first)
+__device__ __forceinline__ uint32_t sp_slot(const uint4& w0, const uint4& w1, const uint4& w2, int k) {
   const uint32_t sl[kSpSlots] = {w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y, w2.z, w2.w};
-  const int lo = 8 * ch0, hi = 8 * ch1;
-#pragma unroll
-  for (int k = 0; k < kSpSlots; ++k) {
-    const int d = (int)(sl[k] & 0xffffu);
-    if (k < cnt && d >= lo && d < hi) row[d] = (short)(sl[k] >> 16);
-  }
+  return sl[k];
+}
+// bf16 bits of (v - base), v and base bf16 bits
+__device__ __forceinline__ short sp_delta(uint32_t v, uint32_t base) {
+  return (short)bf16_bits(bf16_val(v) - bf16_val(base));
 }
 
 // Records of the next D steps in registers (q[0] = this step's): a sampled record is a random HBM access, so its
-// load is issued D - 1 steps before the expansion that reads it.
+// load is issued D - 1 steps before the step that reads it.
 template <int D>
 struct SpRecQueue {
   uint4 q[D][3];
@@ -168,55 +167,87 @@ struct SpRecQueue {
     }
   }
 };
-constexpr int kSpFwdDepth = 3;
-constexpr int kSpWgradDepth = 4;
+constexpr int kSpFwdW = 3;  // W_a blocks and records in flight (forward)
+
+// Wsum of every row block: out[r][o] = bf16 hi | bf16 lo << 16 of sum_{d<P} W_a[o][r P + d] (fp32, fixed order).
+// One wave per (r, o): four destinations per lane, DPP-free shuffle tree.
+__global__ __launch_bounds__(256) void sparse_wsum_kernel(const __bf16* __restrict__ wa, long lda, int R, int P,
+                                                          uint32_t* __restrict__ out) {
+  const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= (long)R * kSpC1) return;
+  const int r = (int)(w / kSpC1), o = (int)(w - (long)r * kSpC1);
+  const __bf16* src = wa + (long)o * lda + (long)r * P;
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int d = 64 * q + lane;
+    if (d < P) s += (float)src[d];
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  if (lane == 0) {
+    const uint32_t hi = bf16_bits(s);
+    const uint32_t lo = bf16_bits(s - bf16_val(hi));
+    out[(long)r * kSpC1 + o] = hi | (lo << 16);
+  }
+}
 
 // Forward: part[s][b][:64] = sum_{r in split s} a[b, r P : r P + P] W_a[:, r P : r P + P]^T.
 // 256 samples x one split of the row blocks per workgroup (4 waves x 64 samples, 64 x 64 outputs per wave).  Per
-// row block: the W_a block [64][P] (aligned copy, zero past P) goes to a shared LDS image and every lane expands its
-// sample's record into its wave's [64][P] image (no cross-wave dependence); the next block's W_a chunks and records
-// are loaded into registers while the MFMAs run.  LDS: 5 x 64 x LD x 2 bytes (138 KB at P = 200).
+// row block: the W_a block [64][P] plus its two Wsum columns goes to a shared LDS image; every lane writes its
+// sample's deltas and base columns into its wave's persistent [64][Kp] image and clears the deltas after the
+// MFMAs (the wave's own LDS operations run in order); the next block's W_a chunks and records load into registers
+// while the MFMAs run.  LDS: 5 x 64 x LD x 2 bytes (138 KB at P = 200).
 // WVEC: P % 8 == 0 and 16-byte aligned W_a rows (16-byte loads of every chunk below P)
 template <bool WVEC>
 __global__ __launch_bounds__(256) void sparse_fwd_kernel(const uint32_t* __restrict__ ring, const int* __restrict__ rows,
                                                          int B, int R, int P, const __bf16* __restrict__ wa, long lda,
-                                                         float* __restrict__ part) {
+                                                         const uint32_t* __restrict__ wsum, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) short sp_lds[];
-  const int Kp = (P + 15) & ~15, LD = sp_ld_k(Kp), CPR = Kp / 8, KS = Kp / 16;
+  const int Kp = sp_kp_fwd(P), LD = sp_ld_k(Kp), CPR = Kp / 8, KS = Kp / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   short* Ws = sp_lds;                           // [64][LD]: W_a block (row = output o)
   short* As = sp_lds + (1 + wave) * 64 * LD;    // [64][LD]: this wave's 64 samples
+  short* myrow = As + lane * LD;
   const int S = gridDim.y, sp = blockIdx.y;
   const int r_lo = (int)((long)R * sp / S), r_hi = (int)((long)R * (sp + 1) / S);
   const long b0 = (long)blockIdx.x * 256 + 64 * wave;
   const bool on = b0 + lane < B;
   const uint32_t* rec = ring + (long)(on ? rows[b0 + lane] : 0) * R * kSpWords;
+  for (int c = 0; c < CPR; ++c) *reinterpret_cast<sp_u32x4*>(myrow + 8 * c) = sp_u32x4{0, 0, 0, 0};
   // W_a block: thread t loads row o = t / 4, chunks t % 4 + 4 i (CPR <= 30 chunks per row)
-  constexpr int WPER = (kSpMaxFwdP / 8 + 3) / 4;
+  constexpr int WPER = ((kSpMaxP + 2 + 15) / 16 * 2 + 3) / 4;
   const int wo = tid >> 2, wc = tid & 3;
   const __bf16* wrow = wa + (long)wo * lda;
   short* wdst = Ws + wo * LD + 8 * wc;
-  sp_u32x4 wr[WPER];
-  SpRecQueue<kSpFwdDepth> nq;
+  // W_a blocks of the next kSpFwdW row blocks in a register ring (set r mod kSpFwdW): a block is shared by the
+  // workgroups of one split, whose first read of it misses in L2, and one MFMA phase (~0.7 us) did not cover
+  // that latency (round 6: 17 % MFMA-busy with a one-block lead)
+  sp_u32x4 wr[kSpFwdW][WPER];
+  uint32_t ws[kSpFwdW];  // this thread's row o: Wsum hi | lo of the block in wr (stored by the wc == 0 thread)
+  SpRecQueue<kSpFwdW> nq;  // this lane's records of the same blocks (set r mod kSpFwdW; no register shifting)
 #pragma unroll
-  for (int k = 0; k < kSpFwdDepth; ++k) {
+  for (int k = 0; k < kSpFwdW; ++k) {
     nq.clear(k);
     if (on && r_lo + k < r_hi) nq.fetch(k, rec + (long)(r_lo + k) * kSpWords);
   }
-  auto load = [&](int r) {  // W_a block r
+  auto load = [&](auto set, int r) {  // W_a block r (zero beyond P) into ring set `set`
+    constexpr int SET = decltype(set)::value;
     const __bf16* src = wrow + (long)r * P + 8 * wc;
+    ws[SET] = wsum[(long)r * kSpC1 + wo];
 #pragma unroll
     for (int i = 0; i < WPER; ++i) {
       const int col = 8 * (wc + 4 * i);
       if (col >= 8 * CPR) break;
       if constexpr (WVEC) {
-        wr[i] = col < P ? *reinterpret_cast<const sp_u32x4*>(src + 32 * i) : sp_u32x4{0, 0, 0, 0};
+        wr[SET][i] = col < P ? *reinterpret_cast<const sp_u32x4*>(src + 32 * i) : sp_u32x4{0, 0, 0, 0};
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint32_t x0 = col + 2 * j < P ? __builtin_bit_cast(uint16_t, src[32 * i + 2 * j]) : 0u;
           const uint32_t x1 = col + 2 * j + 1 < P ? __builtin_bit_cast(uint16_t, src[32 * i + 2 * j + 1]) : 0u;
-          wr[i][j] = x0 | (x1 << 16);
+          wr[SET][i][j] = x0 | (x1 << 16);
         }
       }
     }
@@ -228,31 +259,71 @@ __global__ __launch_bounds__(256) void sparse_fwd_kernel(const uint32_t* __restr
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-  if (r_lo < r_hi) load(r_lo);
+  static_assert(kSpFwdW == 3, "ring prologue / loop below are written for three sets");
+  if (r_lo < r_hi) load(std::integral_constant<int, 0>{}, r_lo);
+  if (r_lo + 1 < r_hi) load(std::integral_constant<int, 1>{}, r_lo + 1);
+  if (r_lo + 2 < r_hi) load(std::integral_constant<int, 2>{}, r_lo + 2);
   const int r32 = lane & 31, h = lane >> 5;
-  for (int r = r_lo; r < r_hi; ++r) {
-    __syncthreads();  // the previous block's fragments are read
+  auto block = [&](auto set, int r) {
+    constexpr int SET = decltype(set)::value;
+    __syncthreads();  // the previous block's W_a fragments are read
 #pragma unroll
     for (int i = 0; i < WPER; ++i) {
       if (wc + 4 * i >= CPR) break;
-      *reinterpret_cast<sp_u32x4*>(wdst + 32 * i) = wr[i];
+      *reinterpret_cast<sp_u32x4*>(wdst + 32 * i) = wr[SET][i];
     }
-    sp_expand(As + lane * LD, nq.q[0][0], nq.q[0][1], nq.q[0][2], P, 0, CPR);
-    if (r + 1 < r_hi) load(r + 1);
-    nq.shift();
-    if (on && r + kSpFwdDepth < r_hi) nq.fetch(kSpFwdDepth - 1, rec + (long)(r + kSpFwdDepth) * kSpWords);
+    if (wc == 0) {  // the two Wsum columns (after the chunk stores of this row: same wave, in order)
+      Ws[wo * LD + P] = (short)(ws[SET] & 0xffffu);
+      Ws[wo * LD + P + 1] = (short)(ws[SET] >> 16);
+    }
+    const uint4 w0 = nq.q[SET][0], w1 = nq.q[SET][1], w2 = nq.q[SET][2];
+    const uint32_t base = w0.x & 0xffffu;
+    const int cnt = (int)(w0.x >> 16);
+#pragma unroll
+    for (int k = 0; k < kSpSlots; ++k) {
+      const uint32_t e = sp_slot(w0, w1, w2, k);
+      if (k < cnt) myrow[e & 0xffffu] = sp_delta(e >> 16, base);
+    }
+    myrow[P] = (short)base;
+    myrow[P + 1] = (short)base;
+    if (r + kSpFwdW < r_hi) {
+      load(set, r + kSpFwdW);
+      if (on) nq.fetch(SET, rec + (long)(r + kSpFwdW) * kSpWords);
+    }
     __syncthreads();
-    for (int s = 0; s < KS; ++s) {
-      sp_s16x8 fa[2], fb[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const sp_s16x8*>(As + (32 * i + r32) * LD + 16 * s + 8 * h);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = *reinterpret_cast<const sp_s16x8*>(Ws + (32 * j + r32) * LD + 16 * s + 8 * h);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = sp_mma(fa[i], fb[j], acc[i][j]);
+    {
+      // software-pipelined K walk: step s + 1's fragments are read before step s's MFMAs issue (one wave per
+      // SIMD: nothing else hides the LDS latency)
+      const short* pa = As + r32 * LD + 8 * h;
+      const short* pb = Ws + r32 * LD + 8 * h;
+      sp_s16x8 fa0 = *reinterpret_cast<const sp_s16x8*>(pa), fa1 = *reinterpret_cast<const sp_s16x8*>(pa + 32 * LD);
+      sp_s16x8 fb0 = *reinterpret_cast<const sp_s16x8*>(pb), fb1 = *reinterpret_cast<const sp_s16x8*>(pb + 32 * LD);
+      for (int s = 0; s < KS; ++s) {
+        const sp_s16x8 a0 = fa0, a1 = fa1, b0_ = fb0, b1 = fb1;
+        if (s + 1 < KS) {
+          const int o = 16 * (s + 1);
+          fa0 = *reinterpret_cast<const sp_s16x8*>(pa + o);
+          fa1 = *reinterpret_cast<const sp_s16x8*>(pa + 32 * LD + o);
+          fb0 = *reinterpret_cast<const sp_s16x8*>(pb + o);
+          fb1 = *reinterpret_cast<const sp_s16x8*>(pb + 32 * LD + o);
+        }
+        acc[0][0] = sp_mma(a0, b0_, acc[0][0]);
+        acc[0][1] = sp_mma(a0, b1, acc[0][1]);
+        acc[1][0] = sp_mma(a1, b0_, acc[1][0]);
+        acc[1][1] = sp_mma(a1, b1, acc[1][1]);
+      }
     }
+    // clear the deltas (this wave's fragment reads of its image are issued above: in order)
+#pragma unroll
+    for (int k = 0; k < kSpSlots; ++k) {
+      const uint32_t e = sp_slot(w0, w1, w2, k);
+      if (k < cnt) myrow[e & 0xffffu] = 0;
+    }
+  };
+  for (int r = r_lo; r < r_hi; r += kSpFwdW) {
+    block(std::integral_constant<int, 0>{}, r);
+    if (r + 1 < r_hi) block(std::integral_constant<int, 1>{}, r + 1);
+    if (r + 2 < r_hi) block(std::integral_constant<int, 2>{}, r + 2);
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -268,28 +339,47 @@ __global__ __launch_bounds__(256) void sparse_fwd_kernel(const uint32_t* __restr
 }
 
 // Gradient: dW_a[o, r P + d] = sum_b dh0[b, o] a[b, r P + d].  One workgroup per row block r: output [64][Np]
-// (Np = P rounded up to 32: 2 x Np/32 tiles of 32 x 32, wave w owns column tiles w, w + 4 for both row tiles), K =
-// the B samples in steps of 64: dh0 rows -> [64][96] and the 64 records expanded (4 threads per sample, a quarter
-// of the row each) -> [64][LDB], both M/N-contiguous images read with ds_read_b64_tr_b16.  Every gradient element
-// is written once (no atomics, deterministic); the next step's dh0 chunk and the records kSpWgradDepth - 1 steps
-// ahead load during the MFMAs.
+// (Np = P + 1 rounded up to 32: 2 x Np/32 tiles of 32 x 32, wave w owns column tiles w, w + 4 for both row tiles),
+// K = the B samples in steps of 64: dh0 rows -> [64][96] and the 64 records' deltas + base column (column P) ->
+// the persistent [64][LDB] image, both M/N-contiguous images read with ds_read_b64_tr_b16.  Four threads per
+// sample: thread `quarter` loads only the record words it writes (the header and slots quarter, quarter + 4,
+// quarter + 8: four dwords), kSpWgQ steps ahead -- a sampled record is a random HBM access (~2 us under load)
+// and a step's MFMAs take ~0.2 us, so the queue must cover ~10 steps (it covered 3 at 12 dwords per slot:
+// 46 % of wave cycles waiting).  The previous step's deltas are cleared after the barrier that ends its MFMAs.
+// Row blocks are grouped by XCD (workgroup i runs on XCD i mod 8 and takes block (i mod 8) R8 + i / 8), so the
+// blocks in flight on one XCD are consecutive and share the records' cache lines in that XCD's L2 (48-byte
+// records, 128-byte lines).  The base column's output G[o] = sum_b dh0[b, o] base_b is added to every
+// destination at the end.  Every gradient element is written once (no atomics, deterministic).
+constexpr int kSpWgQ = 10;
 __global__ __launch_bounds__(256) void sparse_wgrad_kernel(const uint32_t* __restrict__ ring, const int* __restrict__ rows,
                                                            int B, int R, int P, const __bf16* __restrict__ dh0, long ldd,
                                                            float* __restrict__ gw, long ldg) {
   extern __shared__ __attribute__((aligned(16))) short sp_lds[];
-  const int Np = (P + 31) & ~31, LDB = sp_ld_tr(Np), NT = Np / 32, CPQ = Np / 32;  // chunks per quarter row
+  const int R8 = (R + 7) / 8;
+  const int r = (int)(blockIdx.x % 8) * R8 + (int)(blockIdx.x / 8);
+  if (r >= R) return;
+  const int Np = sp_np_wgrad(P), LDB = sp_ld_tr(Np), NT = Np / 32;
   constexpr int LDA = 96;  // sp_ld_tr(64)
   short* Ai = sp_lds;                 // [64 samples][LDA]: dh0 (m = o)
-  short* Bi = sp_lds + kSpBK * LDA;   // [64 samples][LDB]: expanded records (n = d)
-  const int r = blockIdx.x;
+  short* Bi = sp_lds + kSpBK * LDA;   // [64 samples][LDB]: deltas + base column (n = d)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int srow = tid >> 2, quarter = tid & 3;  // expansion: sample srow of the step, chunk quarter
+  const int srow = tid >> 2, quarter = tid & 3;  // sample srow of the step, slots k = quarter mod 4
+  short* brow = Bi + srow * LDB;
+  for (int c = quarter; c < Np / 8; c += 4) *reinterpret_cast<sp_u32x4*>(brow + 8 * c) = sp_u32x4{0, 0, 0, 0};
   sp_u32x4 d0 = {0, 0, 0, 0}, d1 = d0;
-  SpRecQueue<kSpWgradDepth> nq;
-  auto fetch = [&](int k, int bs) {  // records of step bs into queue slot k
+  // record words of the next kSpWgQ steps: [header, slot quarter, slot quarter + 4, slot quarter + 8]
+  uint32_t q[kSpWgQ][4];
+  auto fetch = [&](int k, int bs) {
     const long b = bs + srow;
-    if (b < B) nq.fetch(k, ring + ((long)rows[b] * R + r) * kSpWords);
-    else nq.clear(k);
+    if (b < B) {
+      const uint32_t* rec = ring + ((long)rows[b] * R + r) * kSpWords;
+      q[k][0] = rec[0];
+      q[k][1] = rec[1 + quarter];
+      q[k][2] = rec[5 + quarter];
+      q[k][3] = quarter < 3 ? rec[9 + quarter] : 0u;
+    } else {
+      q[k][0] = q[k][1] = q[k][2] = q[k][3] = 0u;
+    }
   };
   auto load = [&](int bs) {
     // dh0 chunk [64][64] bf16: 512 x 16 B, two per thread
@@ -299,25 +389,42 @@ __global__ __launch_bounds__(256) void sparse_wgrad_kernel(const uint32_t* __res
     d1 = bb < B ? *reinterpret_cast<const sp_u32x4*>(dh0 + bb * ldd + 8 * (i1 & 7)) : sp_u32x4{0, 0, 0, 0};
   };
 #pragma unroll
-  for (int k = 0; k < kSpWgradDepth; ++k) fetch(k, k * kSpBK);
+  for (int k = 0; k < kSpWgQ; ++k) fetch(k, k * kSpBK);
   sp_f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+      for (int t = 0; t < 16; ++t) acc[i][j][t] = 0.f;
   const bool t1 = wave + 4 < NT;  // second column tile of this wave
   const bool t0 = wave < NT;
+  uint32_t prev[4] = {0u, 0u, 0u, 0u};  // the previous step's words (its deltas to clear)
   load(0);
   for (int bs = 0; bs < B; bs += kSpBK) {
-    __syncthreads();
+    __syncthreads();  // the previous step's fragments are read
     *reinterpret_cast<sp_u32x4*>(Ai + (tid >> 3) * LDA + 8 * (tid & 7)) = d0;
     *reinterpret_cast<sp_u32x4*>(Ai + ((tid + 256) >> 3) * LDA + 8 * (tid & 7)) = d1;
-    sp_expand(Bi + srow * LDB, nq.q[0][0], nq.q[0][1], nq.q[0][2], P, quarter * CPQ, quarter * CPQ + CPQ);
+    {
+      const int pc = (int)(prev[0] >> 16);
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+        if (quarter + 4 * m < pc) brow[prev[1 + m] & 0xffffu] = 0;
+      const uint32_t base = q[0][0] & 0xffffu;
+      const int cnt = (int)(q[0][0] >> 16);
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+        if (quarter + 4 * m < cnt) brow[q[0][1 + m] & 0xffffu] = sp_delta(q[0][1 + m] >> 16, base);
+      if (quarter == 0) brow[P] = (short)base;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) prev[m] = q[0][m];
+    }
     if (bs + kSpBK < B) load(bs + kSpBK);
-    nq.shift();
-    fetch(kSpWgradDepth - 1, bs + kSpWgradDepth * kSpBK);
+#pragma unroll
+    for (int k = 0; k + 1 < kSpWgQ; ++k)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) q[k][m] = q[k + 1][m];
+    fetch(kSpWgQ - 1, bs + kSpWgQ * kSpBK);
     __syncthreads();
     if (t0) {
 #pragma unroll
@@ -334,7 +441,20 @@ __global__ __launch_bounds__(256) void sparse_wgrad_kernel(const uint32_t* __res
       }
     }
   }
+  // G[o] (the base column's output, column P: tile P / 32 of wave (P / 32) % 4, lanes P % 32 and P % 32 + 32)
+  __syncthreads();
+  float* G = reinterpret_cast<float*>(sp_lds);  // [64] (the dh0 image is no longer read)
   const int col = lane & 31, h = lane >> 5;
+  {
+    const int tp = P / 32, jp = tp / 4;
+    if (wave == tp % 4 && col == P % 32) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 16; ++t) G[32 * i + (t & 3) + 8 * (t >> 2) + 4 * h] = jp ? acc[i][1][t] : acc[i][0][t];
+    }
+  }
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int d = 32 * (wave + 4 * j) + col;
@@ -342,18 +462,18 @@ __global__ __launch_bounds__(256) void sparse_wgrad_kernel(const uint32_t* __res
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int o = 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h;
-        gw[(long)o * ldg + (long)r * P + d] = acc[i][j][q];
+      for (int t = 0; t < 16; ++t) {
+        const int o = 32 * i + (t & 3) + 8 * (t >> 2) + 4 * h;
+        gw[(long)o * ldg + (long)r * P + d] = acc[i][j][t] + G[o];
       }
   }
 }
 
-static size_t sp_fwd_lds(int P) { return (size_t)5 * 64 * sp_ld_k((P + 15) & ~15) * 2; }
-static size_t sp_wgrad_lds(int P) { return (size_t)kSpBK * (96 + sp_ld_tr((P + 31) & ~31)) * 2; }
+static size_t sp_fwd_lds(int P) { return (size_t)5 * 64 * sp_ld_k(sp_kp_fwd(P)) * 2; }
+static size_t sp_wgrad_lds(int P) { return (size_t)kSpBK * (96 + sp_ld_tr(sp_np_wgrad(P))) * 2; }
 
 static void sp_check(int R, int P, int c1 = 1) {
-  GSC_CHECK(R > 0 && P > 0 && P <= 256, "sparse actions: 1..256 destinations per row");
+  GSC_CHECK(R > 0 && P > 0 && P <= kSpMaxP, "sparse actions: 1..238 destinations per row");
   GSC_CHECK(c1 > 0 && c1 <= 256, "sparse actions: critic first layer width 1..256");
 }
 
@@ -369,14 +489,19 @@ void register_sparse_act(py::module_& m) {
                        ptr<int>(bad));
     check_launch();
   });
-  // part: fp32 [splits, B, 64] partial sums (reduce with splitk_reduce); wa: the [64][lda] action block of W
+  // part: fp32 [splits, B, 64] partial sums (reduce with splitk_reduce); wa: the [64][lda] action block of W;
+  // wsum: [R][64] uint32 scratch (the per-block column sums, written here)
   m.def("sparse_fwd", [](uintptr_t ring, uintptr_t rows, int B, int R, int P, uintptr_t wa, long lda, int c1,
-                         uintptr_t part, int splits, uintptr_t stream) {
+                         uintptr_t wsum, uintptr_t part, int splits, uintptr_t stream) {
     sp_check(R, P, c1);
     GSC_CHECK(c1 == kSpC1, "sparse critic products: first layer width 64");
-    GSC_CHECK(P <= kSpMaxFwdP, "sparse_fwd: at most 240 destinations per row");
     GSC_CHECK(splits >= 1 && splits <= R, "sparse_fwd: 1 <= splits <= R");
     GSC_CHECK(ring % 16 == 0, "sparse_fwd: 16-byte aligned record ring");
+    GSC_CHECK(wsum != 0 && wsum % 4 == 0, "sparse_fwd: a [R][64] uint32 scratch for the block sums");
+    const long waves = (long)R * kSpC1;
+    hipLaunchKernelGGL(sparse_wsum_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream_of(stream),
+                       ptr<const __bf16>(wa), lda, R, P, ptr<uint32_t>(wsum));
+    check_launch();
     const bool wvec = (wa % 16 == 0) && (lda % 8 == 0) && (P % 8 == 0);
     const size_t lds = sp_fwd_lds(P);
     static size_t attr[2] = {0, 0};
@@ -389,10 +514,12 @@ void register_sparse_act(py::module_& m) {
     const dim3 grid((B + 255) / 256, splits);
     if (wvec)
       hipLaunchKernelGGL(sparse_fwd_kernel<true>, grid, dim3(256), lds, stream_of(stream), ptr<const uint32_t>(ring),
-                         ptr<const int>(rows), B, R, P, ptr<const __bf16>(wa), lda, ptr<float>(part));
+                         ptr<const int>(rows), B, R, P, ptr<const __bf16>(wa), lda, ptr<const uint32_t>(wsum),
+                         ptr<float>(part));
     else
       hipLaunchKernelGGL(sparse_fwd_kernel<false>, grid, dim3(256), lds, stream_of(stream), ptr<const uint32_t>(ring),
-                         ptr<const int>(rows), B, R, P, ptr<const __bf16>(wa), lda, ptr<float>(part));
+                         ptr<const int>(rows), B, R, P, ptr<const __bf16>(wa), lda, ptr<const uint32_t>(wsum),
+                         ptr<float>(part));
     check_launch();
   });
   m.def("sparse_wgrad", [](uintptr_t ring, uintptr_t rows, int B, int R, int P, uintptr_t dh0, long ldd, int c1,
@@ -401,7 +528,7 @@ void register_sparse_act(py::module_& m) {
     GSC_CHECK(c1 == kSpC1, "sparse critic products: first layer width 64");
     GSC_CHECK(ring % 16 == 0 && dh0 % 16 == 0 && ldd % 8 == 0, "sparse_wgrad: 16-byte aligned ring and dh0 rows");
     const size_t lds = sp_wgrad_lds(P);
-    hipLaunchKernelGGL(sparse_wgrad_kernel, dim3(R), dim3(256), lds, stream_of(stream), ptr<const uint32_t>(ring),
+    hipLaunchKernelGGL(sparse_wgrad_kernel, dim3(8 * ((R + 7) / 8)), dim3(256), lds, stream_of(stream), ptr<const uint32_t>(ring),
                        ptr<const int>(rows), B, R, P, ptr<const __bf16>(dh0), ldd, ptr<float>(gw), ldg);
     check_launch();
   });

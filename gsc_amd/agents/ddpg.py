@@ -469,7 +469,7 @@ def replay_plan(cap: int, n_pad: int, n_obs: int, action_dim: int, action_bytes:
 
     Dense rows take ``action_bytes`` per action entry within 60 % of HBM; sparse row records (48 B per n_pad-wide
     destination row, ``csrc/ops/sparse_act.hip``) within 65 % (syn200: 2M x 91 KB = 182 GB of 288 GB; the learner
-    needs < 40 GB).  ``mode`` auto: sparse only when ``eligible`` (native GPU learner, n_pad <= 240, critic
+    needs < 40 GB).  ``mode`` auto: sparse only when ``eligible`` (native GPU learner, n_pad <= 238, critic
     first layer 64 wide) and the dense ring cannot hold ``cap`` transitions; "1" forces sparse where eligible,
     "0" dense.  Without HBM (CPU) the budget is 4 GB, dense."""
     obs_bytes = 4 * (2 * n_pad * n_obs + 4)
@@ -517,10 +517,10 @@ class BatchedTrainer:
         # per row instead of 2 n_pad B.  GSC_SPARSE_REPLAY=auto (default) picks sparse only when the dense ring
         # cannot hold the reference's min(mem_limit E, replay_cap_max) transitions in 60 % of HBM (config 5:
         # 2M x 720 KB; config 4's 2M x 45 KB fits dense, whose GEMMs are faster at small A); 1 forces it where
-        # the native kernels apply (n_pad <= 240, critic first layer 64 wide), 0 disables it.
+        # the native kernels apply (n_pad <= 238, critic first layer 64 wide), 0 disables it.
         R_rows = sim.action_dim // sim.n_pad
         hbm = _replay_hbm(self.device)
-        eligible = bool(self.learner.native_ok and self.device.type == "cuda" and sim.n_pad <= 240
+        eligible = bool(self.learner.native_ok and self.device.type == "cuda" and sim.n_pad <= 238
                         and self.learner.critic.mlp.layers[0].weight.shape[0] == 64)
         self.sparse_replay, per, budget = replay_plan(
             cap, sim.n_pad, sim.n_obs, sim.action_dim, torch.empty((), dtype=adt).element_size(), hbm, eligible,

@@ -232,9 +232,10 @@ class NativeDDPGUpdate:
     def set_sparse(self, ring: torch.Tensor, R: int, P: int) -> None:
         if self.critic.width(0) != 64:
             raise ValueError("sparse replayed actions need the critic's first layer width 64 (GSC_SPARSE_REPLAY=0)")
-        if P > 240:
-            raise ValueError("sparse replayed actions: at most 240 destinations per row (GSC_SPARSE_REPLAY=0)")
+        if P > 238:
+            raise ValueError("sparse replayed actions: at most 238 destinations per row (GSC_SPARSE_REPLAY=0)")
         self.sparse = (ring, int(R), int(P))
+        self.sp_wsum = torch.empty(int(R) * 64, dtype=torch.int32, device=self.dev)  # per-block W_a column sums
         # row-block splits of the forward (one 138 KB-LDS workgroup per CU): the split count whose workgroup
         # total best fills whole dispatch rounds of the CUs, within the split-K slabs
         self.sp_splits = sparse_fwd_splits(self.B, int(R), self.slabs.numel() // (self.B * 64), self.dev)
@@ -428,7 +429,7 @@ class NativeDDPGUpdate:
         H, A, c1 = self.H, self.A, c.width(0)
         wa, st, S = self._wa(c, "c"), self._stream(), self.sp_splits
         self.nat.sparse_fwd(ring.data_ptr(), rows.data_ptr(), self.B, R, P, wa.data_ptr(), wa.stride(0), c1,
-                            self.slabs.data_ptr(), S, st)
+                            self.sp_wsum.data_ptr(), self.slabs.data_ptr(), S, st)
         self.nat.splitk_reduce(self.slabs.data_ptr(), self.B * c1, S, self.B, c1, c1, self.hacc.data_ptr(),
                                self.hacc.stride(0), 1.0, 0, st)
         self._first(c, self.emb["c"], self._rowtab(c, "c"), self.hid_c[0], acc_ready=True)

@@ -54,6 +54,15 @@ PRESETS = {
                   test="configs/networks/abilene/abilene-in4-rand-cap1-2.graphml",
                   agent="configs/config/agent/sample_agent.yaml", service="configs/service_functions/abc.yaml",
                   sim="configs/config/simulator/sample_config.yaml", episode_steps=200, period=10),
+    # diagnosis controls: one training network, tested on that same network (no transfer, no network switches)
+    "solo_rc12": dict(train=["configs/networks/abilene/abilene-in4-rand-cap1-2.graphml"],
+                      test="configs/networks/abilene/abilene-in4-rand-cap1-2.graphml",
+                      agent="configs/config/agent/sample_agent.yaml", service="configs/service_functions/abc.yaml",
+                      sim="configs/config/simulator/sample_config.yaml", episode_steps=200, period=10),
+    "solo_cap1": dict(train=["configs/networks/abilene/abilene-in4-cap1.graphml"],
+                      test="configs/networks/abilene/abilene-in4-cap1.graphml",
+                      agent="configs/config/agent/sample_agent.yaml", service="configs/service_functions/abc.yaml",
+                      sim="configs/config/simulator/sample_config.yaml", episode_steps=200, period=10),
     # 200-node: s0 / s1 for training (as bench config 5), s2 held out
     "syn200": dict(train=[f"{NET}/syn200-in16-cap1-3-s0.graphml", f"{NET}/syn200-in16-cap1-3-s1.graphml"],
                    test=f"{NET}/syn200-in16-cap1-3-s2.graphml", agent="configs/config/agent/agent_syn200.yaml",

@@ -57,12 +57,13 @@ def main():
     dh0 = torch.randn(B, c1, device="cuda").to(torch.bfloat16)
     S = a.splits or sparse_fwd_splits(B, R, 64, torch.device("cuda"))
     part = torch.empty(S, B, c1, device="cuda")
+    wsum = torch.empty(R * c1, dtype=torch.int32, device="cuda")
     hacc = torch.empty(B, c1, device="cuda")
     gw = torch.empty(c1, A, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
 
     def fwd():
-        nat.sparse_fwd(ring.data_ptr(), rows.data_ptr(), B, R, P, wa.data_ptr(), lda, c1, part.data_ptr(), S, s)
+        nat.sparse_fwd(ring.data_ptr(), rows.data_ptr(), B, R, P, wa.data_ptr(), lda, c1, wsum.data_ptr(), part.data_ptr(), S, s)
         nat.splitk_reduce(part.data_ptr(), B * c1, S, B, c1, c1, hacc.data_ptr(), c1, 1.0, 0, s)
 
     def wgrad():

@@ -69,10 +69,11 @@ def test_sparse_critic_products_match_fp32_dense(P):
     dh0 = (torch.randn(B, c1, device="cuda", generator=g)).to(torch.bfloat16)
     S = 4
     part = torch.zeros(S, B, c1, device="cuda")
+    wsum = torch.empty(R * c1, dtype=torch.int32, device="cuda")
     hacc = torch.zeros(B, c1, device="cuda")
     gw = torch.zeros(c1, A, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
-    nat.sparse_fwd(rep.actions.data_ptr(), rows.data_ptr(), B, R, P, wa.data_ptr(), lda, c1, part.data_ptr(), S, s)
+    nat.sparse_fwd(rep.actions.data_ptr(), rows.data_ptr(), B, R, P, wa.data_ptr(), lda, c1, wsum.data_ptr(), part.data_ptr(), S, s)
     nat.splitk_reduce(part.data_ptr(), B * c1, S, B, c1, c1, hacc.data_ptr(), c1, 1.0, 0, s)
     nat.sparse_wgrad(rep.actions.data_ptr(), rows.data_ptr(), B, R, P, dh0.data_ptr(), c1, c1, gw.data_ptr(), A, s)
     torch.cuda.synchronize()
