@@ -267,6 +267,24 @@ int actor_proj(uintptr_t h, long ldh, uintptr_t w, long ldw, uintptr_t bias, uin
   // left 200 workgroups walking every tile (1.2 ms at B = 25,600): 8 splits, one per XCD.  Small
   // batches: >= 256 workgroups with S a multiple of 8 (XCD grouping).
   int S = rbs >= 128 ? (tiles >= 128 ? 8 : 1) : ((256 + rbs - 1) / rbs + 7) / 8 * 8;
+  if (rbs >= 128 && tiles >= 128) {
+    // long action spaces at large batches: the multiple of 8 whose rbs x S workgroups (one per CU at a time) best
+    // fill whole dispatch rounds, the smaller S within 1 % (config 5, rbs = 200: S = 8 left the 7th round a
+    // quarter full, 7.26 ms; S = 32 fills 25 rounds, 6.62 ms; profiles/aproj_bench.txt)
+    int dev = 0, cus = 256;
+    GSC_HIP_CHECK(hipGetDevice(&dev));
+    GSC_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    double best = 0.0;
+    for (int c = 8; c <= 64; c += 8) {
+      if ((long)c * M * J > slab_floats || tiles / c < 64) break;  // >= 64 tiles per workgroup (H load amortised)
+      const long wgs = (long)rbs * c, rounds = (wgs + cus - 1) / cus;
+      const double eff = (double)wgs / (double)(rounds * cus);
+      if (eff > best + 0.01) {
+        best = eff;
+        S = c;
+      }
+    }
+  }
   static const int s_env = getenv("GSC_APROJ_SPLITS") ? atoi(getenv("GSC_APROJ_SPLITS")) : 0;  // tuning override
   if (s_env > 0) S = s_env;
   while (S > 1 && (long)S * M * J > slab_floats) S = S > 8 ? S - 8 : 1;

@@ -195,7 +195,8 @@ class NativeDDPGUpdate:
         self.big_tiles = ({"act": {"tile": 1, "bk": 64}, "dw": {"tile": 2, "bk": 64}, "mc": {"tile": 3}}
                           if A >= int(os.environ.get("GSC_LARGE_A_MIN", "16384"))
                           and os.environ.get("GSC_LARGE_A_TILES", "1") != "0" else {})
-        self.slabs = mk(16 << 20)                            # split-K slabs (64 MB; bounds the split count)
+        # split-K slabs (bound the split count): 64 MB, or 32 splits of the actor projection's [B, 64] partials
+        self.slabs = mk(max(16 << 20, 32 * self.B * 64) if self.A >= 8192 else 16 << 20)
         self.head_blocks = max(64, min(256, -(-B // 64)))    # one block per CU (>= 16 rows per wave)
         cm = self.critic.width(self.critic.nh - 1)
         self.part = mk(self.head_blocks * (cm + 3))

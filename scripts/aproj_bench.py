@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--J", type=int, default=64)
     ap.add_argument("--T", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--slab-mb", type=int, default=64, help="split-K slab bytes (bounds the split count)")
     a = ap.parse_args()
     nat = load_native()
     dev = "cuda"
@@ -35,7 +36,7 @@ def main():
     topo = torch.randint(0, a.T, (a.M,), device=dev, generator=g, dtype=torch.int32)
     wa = torch.zeros(a.J, A8, device=dev, dtype=torch.bfloat16)
     wa[:, :a.A] = (torch.randn(a.J, a.A, device=dev, generator=g) * 0.01).to(torch.bfloat16)
-    slabs = torch.empty(16 << 20, device=dev)
+    slabs = torch.empty(a.slab_mb << 18, device=dev)
     z = torch.empty(a.M, a.J, device=dev)
     s = torch.cuda.current_stream().cuda_stream
 

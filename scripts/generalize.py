@@ -148,6 +148,8 @@ def main():
     ap.add_argument("--schedule-threshold", default=None,
                     help="opt-in post-processing threshold (float or 'auto' = 2.4 / n_pad); default: the reference's 0.1")
     ap.add_argument("--on-train", action="store_true", help="also evaluate every policy on each training network")
+    ap.add_argument("--check-every", type=int, default=0,
+                    help="read the simulator's overflow / bad-state flags every N steps (0: at episode ends only)")
     a = ap.parse_args()
     import torch
     import yaml
@@ -173,7 +175,7 @@ def main():
             evals[os.path.basename(n)][pol] = evaluate(pol, cfg, n, pre, a.eval_envs, 1000 + a.seed, dev=dev)
     sim = load_batched_from_paths(pre["train"], pre["service"], pre["sim"], cfg, a.envs, device=dev, seed=a.seed)
     T = len(pre["train"])
-    tr = BatchedTrainer(cfg, sim, TrainerConfig(num_envs=a.envs, seed=a.seed, check_every=0),
+    tr = BatchedTrainer(cfg, sim, TrainerConfig(num_envs=a.envs, seed=a.seed, check_every=a.check_every),
                         network_schedule=list(range(T)), period=int(pre.get("period", 1)))
     t0 = time.time()
     curve = []

@@ -56,3 +56,23 @@ def test_fused_adam_matches_torch_adam_and_polyak():
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
     for a, b in zip(tgt.parameters(), tgt_ref.parameters()):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
+
+
+def test_schedule_threshold_opt_in():
+    """The opt-in post-processing threshold (docs/DEVIATIONS.md): absent -> the reference's 0.1; `auto` scales it
+    with 1/n_pad beyond 24 nodes; at 50 nodes the reference's 0.1 turns a row of comparable weights into the
+    uniform row, `auto` keeps its shape."""
+    import pytest
+    from gsc_amd.envs.common import schedule_threshold
+    assert schedule_threshold({}, 200) == 0.1
+    assert schedule_threshold({"schedule_threshold": "auto"}, 24) == 0.1
+    assert abs(schedule_threshold({"schedule_threshold": "auto"}, 50) - 0.048) < 1e-12
+    assert schedule_threshold({"schedule_threshold": 0.02}, 50) == 0.02
+    with pytest.raises(ValueError):
+        schedule_threshold({"schedule_threshold": 1.5}, 50)
+    P = 50
+    row = np.random.default_rng(3).random(P) + 0.5   # comparable weights, each ~1/50 after normalising
+    ref = threshold_normalize(row, P, 0.1, 2)
+    auto = threshold_normalize(row, P, schedule_threshold({"schedule_threshold": "auto"}, P), 2)
+    assert np.allclose(ref, 1.0 / P)                  # reference threshold: uniform schedule
+    assert auto.std() > 0 and abs(auto.sum() - 1) < 1e-12  # auto: shape kept (some weights zeroed, rest renormalised)
