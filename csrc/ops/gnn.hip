@@ -75,6 +75,8 @@ static GnnPath fused_path(int M, int NM, int P, int Fin, int H, const std::vecto
   if (!uniq || layer_of.empty() || (int)layer_of.size() > kClMaxLayers) return kPathNone;
   const int L = (int)layer_of.size(), nb = n_blocks_of(layer_of);
   if (gnn_mf_supported(Fin, H, NM, L, nb, layer_of.data())) return kPathMf;
+  // 33 .. 64-node graphs: packs of the large-graph kernels (several graphs per workgroup, every conv in LDS)
+  if (NM > 32 && lg_enabled() && gnn_lg_supported(Fin, H, NM, P, M, L, nb, layer_of.data())) return kPathLg;
   if (gnn_mt_supported(Fin, H, NM, M, L, nb, layer_of.data())) return kPathMt;
   if (lg_enabled() && gnn_lg_supported(Fin, H, NM, P, M, L, nb, layer_of.data())) return kPathLg;
   return kPathNone;

@@ -50,6 +50,7 @@ constexpr int kLgUb = 2;  // ... in the backward's row-reading loops
 
 struct LgLayout {
   int P, P32, PK, RS, TS, L, nslots, xs;
+  int G, NP, gm, nv;  // graphs per pack (one workgroup's unit of work), nodes per graph (n_pad), pack meta, node valid
   int frag, vec, ord, iptr, deg, isrc, optr, oq, odst, sc, ds, zb, slot[kClMaxLayers], R, xl, xr, dy, dtl, dtr, dnl, dnr, ht,
       red, acc0, wacc, wq, total;
 };
@@ -242,16 +243,16 @@ __device__ __forceinline__ void lg_linear(const bf16x8* frag, int set, bool k2, 
 }
 
 // Forward attention of target node i (lane pair, channels c0 .. c0 + HC): PyG segment softmax (online, one
-// rescale per chunk) and mean aggregation; returns the conv output half-row (bias, optional ReLU; zero for i >= n).
+// rescale per chunk) and mean aggregation; returns the conv output half-row (bias, optional ReLU; zero unless real).
 // Messages go U at a time: the U source ids, then the U rows are loaded before any of them is used (clamped to
 // the segment's last message), so one LDS round trip serves U messages.
 template <int HC, int U, int NL>
-__device__ __forceinline__ void lg_attend(float (&y)[HC], int i, int n, int c0, bool hi, const float* vec, bool relu,
+__device__ __forceinline__ void lg_attend(float (&y)[HC], int i, bool real, int c0, bool hi, const float* vec, bool relu,
                                           const float* XL, const float* XR, const int32_t* iptr,
                                           const uint16_t* isrc, const float* deg, const LgLayout& m) {
 #pragma unroll
   for (int k = 0; k < HC; ++k) y[k] = 0.f;
-  if (i >= n) return;
+  if (!real) return;
   // score = att . LeakyReLU(z) = 0.6 (u_j + v_i) + 0.4 att . |z|: one FMA per channel with the |z| source
   // modifier; the lane holding channel HV - 1 (u + v; hi) adds the linear part
   float xr[HC], a4[HC], acc[HC];
@@ -310,36 +311,79 @@ __device__ __forceinline__ void lg_attend(float (&y)[HC], int i, int n, int c0, 
   if (hi) y[HC - 1] = 0.f;  // channel HV - 1 carried u: not an output channel
 }
 
-// Topology rows of graph type t into LDS (u16 message arrays; the backward also the source-sorted CSR)
+// Topology rows of pack pk's graphs into LDS (u16 message arrays; the backward also the source-sorted CSR).  A pack
+// is G consecutive batch entries b0 .. b0 + G - 1 laid out as one disjoint graph of G x NP nodes: graph g's node v
+// is node g NP + v and its messages follow graph g - 1's (offsets in the pack meta).  Graphs past the batch are
+// empty (no real nodes, no messages).  G = 1 (200 nodes): the topology of b0 as is.  Lane-pair order interleaves
+// the graphs (rank p -> graph p mod G, that graph's node of degree rank p / G): every wave gets a similar mix.
+// Pack meta (LDS ints): [0, 8) topology (-1: empty), [8, 16) real nodes, [16, 25) message offsets.
 template <bool BWD, int NT>
-__device__ __forceinline__ void lg_stage_topo(const ClArgs& a, int t, char* lds, const LgLayout& m) {
+__device__ __forceinline__ void lg_stage_topo(const ClArgs& a, long b0, char* lds, const LgLayout& m) {
   int32_t* iptr = reinterpret_cast<int32_t*>(lds + m.iptr);
   float* deg = reinterpret_cast<float*>(lds + m.deg);
   uint16_t* isrc = reinterpret_cast<uint16_t*>(lds + m.isrc);
-  const int P = m.P, M = a.M;
   uint16_t* ord = reinterpret_cast<uint16_t*>(lds + m.ord);
-  for (int k = threadIdx.x; k < 2 * P; k += NT) ord[k] = (uint16_t)a.deg_order[(long)t * 2 * P + k];
-  for (int k = threadIdx.x; k <= P; k += NT) {
-    iptr[k] = a.in_ptr[(long)t * (P + 1) + k];
-    if (k < P) deg[k] = a.deg[(long)t * P + k];
-    if (BWD) reinterpret_cast<int32_t*>(lds + m.optr)[k] = a.out_ptr[(long)t * (P + 1) + k];
+  uint8_t* nv = reinterpret_cast<uint8_t*>(lds + m.nv);
+  int* gm = reinterpret_cast<int*>(lds + m.gm);
+  const int P = m.P, NP = m.NP, G = m.G, M = a.M;
+  if (threadIdx.x == 0) {
+    int off = 0;
+    for (int g = 0; g < G; ++g) {
+      const long b = b0 + g;
+      const int t = b < a.B ? a.topo[b] : -1;
+      gm[g] = t;
+      gm[8 + g] = t >= 0 ? a.nnodes[t] : 0;
+      gm[16 + g] = off;
+      off += t >= 0 ? a.in_ptr[(long)t * (NP + 1) + NP] : 0;
+    }
+    gm[16 + G] = off;
   }
-  for (int k = threadIdx.x; k < M; k += NT) {
-    isrc[k] = (uint16_t)a.in_src[(long)t * M + k];
+  __syncthreads();
+  const int total = gm[16 + G];
+  for (int k = threadIdx.x; k < 2 * P; k += NT) {
+    const int half = k >= P, p = k - half * P, g = p % G, r = p / G, t = gm[g];
+    ord[k] = (uint16_t)(g * NP + (t >= 0 ? a.deg_order[(long)t * 2 * NP + half * NP + r] : r));
+  }
+  for (int u = threadIdx.x; u <= P; u += NT) {
+    if (u == P) {
+      iptr[P] = total;
+      if (BWD) reinterpret_cast<int32_t*>(lds + m.optr)[P] = total;
+      continue;
+    }
+    const int g = u / NP, v = u - g * NP, t = gm[g], o = gm[16 + g];
+    iptr[u] = o + (t >= 0 ? a.in_ptr[(long)t * (NP + 1) + v] : 0);
+    deg[u] = t >= 0 ? a.deg[(long)t * NP + v] : 1.f;
+    nv[u] = (uint8_t)(v < gm[8 + g]);
+    if (BWD) reinterpret_cast<int32_t*>(lds + m.optr)[u] = o + (t >= 0 ? a.out_ptr[(long)t * (NP + 1) + v] : 0);
+  }
+  for (int k = threadIdx.x; k < total; k += NT) {
+    int g = 0;
+    while (g + 1 < G && k >= gm[16 + g + 1]) ++g;
+    const int t = gm[g], o = gm[16 + g], q = k - o;
+    isrc[k] = (uint16_t)(g * NP + a.in_src[(long)t * M + q]);
     if (BWD) {
-      reinterpret_cast<uint16_t*>(lds + m.oq)[k] = (uint16_t)a.out_q[(long)t * M + k];
-      reinterpret_cast<uint16_t*>(lds + m.odst)[k] = (uint16_t)a.out_dst[(long)t * M + k];
+      reinterpret_cast<uint16_t*>(lds + m.oq)[k] = (uint16_t)(o + a.out_q[(long)t * M + q]);
+      reinterpret_cast<uint16_t*>(lds + m.odst)[k] = (uint16_t)(g * NP + a.out_dst[(long)t * M + q]);
     }
   }
 }
 
-// input rows of graph b as the bf16 image (channels 0..15: F_in <= 16, zero past F_in and for rows >= P)
+// node u of the pack is a real node (not padding, not an empty graph's)
+__device__ __forceinline__ bool lg_real(const char* lds, const LgLayout& m, int u) {
+  return u < m.P && reinterpret_cast<const uint8_t*>(lds + m.nv)[u] != 0;
+}
+
+// input rows of pack node i (graph b0 + i / NP, node i mod NP) as the bf16 image (channels 0..15: F_in <= 16, zero
+// past F_in, for rows >= P and for graphs past the batch)
 // (g = the lane's position in its node group: lanes 0 / 1 of the group take channels 0..7 / 8..15)
-__device__ __forceinline__ void lg_load_x(float (&xv)[8], const ClArgs& a, long b, int i, int g) {
+__device__ __forceinline__ void lg_load_x(float (&xv)[8], const ClArgs& a, const LgLayout& m, long b0, int i, int g) {
+  const int gi = i / m.NP, v = i - gi * m.NP;
+  const long b = b0 + gi;
+  const bool ok = i < m.P && g < 2 && b < a.B;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int c = 8 * g + k;
-    xv[k] = (i < a.P && g < 2 && c < a.Fin) ? a.x[(b * a.P + i) * a.Fin + c] : 0.f;
+    xv[k] = (ok && c < a.Fin) ? a.x[(b * m.NP + v) * a.Fin + c] : 0.f;
   }
 }
 __device__ __forceinline__ void lg_put_x(__bf16* S, const float (&xv)[8], int i, int hf, const LgLayout& m) {
@@ -385,15 +429,16 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
   LgClock clk{};
   if (PROF) clk.last = __builtin_amdgcn_s_memtime();
   int* wq = reinterpret_cast<int*>(lds + m.wq);
-  for (long b = lg_next_graph(a, wq, -1); b < a.B; b = lg_next_graph(a, wq, b)) {
-    const int t = a.topo[b], n = a.nnodes[t];
+  const long npk = (a.B + m.G - 1) / m.G;
+  for (long pk = lg_next_graph(a, wq, -1); pk < npk; pk = lg_next_graph(a, wq, pk)) {
+    const long b0 = pk * m.G;
     {
       const int tq = lg_tid();
       float xv[8];
-      lg_load_x(xv, a, b, tq / NL, tq % NL);
-      __syncthreads();  // the previous graph is done with every LDS image
+      lg_load_x(xv, a, m, b0, tq / NL, tq % NL);
+      __syncthreads();  // the previous pack is done with every LDS image
       LG_MARK(PROF, clk, 0);
-      lg_stage_topo<false, kLgThreads>(a, t, lds, m);
+      lg_stage_topo<false, kLgThreads>(a, b0, lds, m);
       lg_put_x(S, xv, tq / NL, tq % NL, m);
       __syncthreads();
       LG_MARK(PROF, clk, 1);
@@ -401,6 +446,7 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
     const int32_t* iptr = reinterpret_cast<const int32_t*>(lds + m.iptr);
     const uint16_t* isrc = reinterpret_cast<const uint16_t*>(lds + m.isrc);
     const float* deg = reinterpret_cast<const float*>(lds + m.deg);
+    const int* gm = reinterpret_cast<const int*>(lds + m.gm);
     for (int l = 0; l < a.L; ++l) {
       const int blk = a.layer_of[l];
       const float* vb = vec + blk * kMfVec;
@@ -412,7 +458,7 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
       const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
       float y[HC];
       const bool last = l + 1 == a.L;
-      lg_attend<HC, kLgUf, NL>(y, iq, n, cq, cq + HC == HV, vb, !last, XL, XR, iptr, isrc, deg, m);
+      lg_attend<HC, kLgUf, NL>(y, iq, lg_real(lds, m, iq), cq, cq + HC == HV, vb, !last, XL, XR, iptr, isrc, deg, m);
       if (!last) {
         __syncthreads();  // S (this conv's input) was read by the node linears before the previous barrier;
                           // the barrier orders this conv's XL reads before the next node linears' XL writes
@@ -420,18 +466,29 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
         if (iq < m.P32) lg_store_bf16<HC>(S + iq * kMfRS + cq, y);
         __syncthreads();
         LG_MARK(PROF, clk, 4);
-      } else {  // mean pool over the real nodes: wave sums (DPP + two swaps), then the waves in a fixed order
+      } else if (m.G == 1) {  // mean pool over the real nodes: wave sums (DPP + two swaps), then the waves in a fixed order
 #pragma unroll
         for (int k = 0; k < HC; ++k) {
-          const float v = lg_wave_sum<NL>(y[k]);  // y is zero for i >= n
+          const float v = lg_wave_sum<NL>(y[k]);  // y is zero for nodes that are not real
           if (lane >= 64 - NL) red[wave * 32 + cq + k] = v;
         }
         __syncthreads();
-        if (tq < a.H) {
+        if (tq < a.H && b0 < a.B) {
           float s = 0.f;
 #pragma unroll
           for (int w = 0; w < kLgThreads / 64; ++w) s += red[w * 32 + tq];
-          a.emb[b * a.H + tq] = s / (float)n;
+          a.emb[b0 * a.H + tq] = s / (float)gm[8];
+        }
+        LG_MARK(PROF, clk, 5);
+      } else {  // packs: the rows into LDS (XR is dead), then one thread per (graph, channel) sums its graph's rows
+        __syncthreads();  // every lane's XR reads are done
+        if (iq < m.P) lg_store_f<HC>(XR + iq * m.RS + cq, y);
+        __syncthreads();
+        if (tq < m.G * a.H) {
+          const int g = tq / a.H, c = tq - g * a.H, n = gm[8 + g];
+          float s = 0.f;
+          for (int v = 0; v < n; ++v) s += XR[(g * m.NP + v) * m.RS + c];
+          if (n > 0) a.emb[(b0 + g) * a.H + c] = s / (float)n;
         }
         LG_MARK(PROF, clk, 5);
       }
@@ -452,11 +509,11 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
 // no per-message sign bits, no second row pass.  A row-free pass then writes alpha and ds for step 3.
 // [z > 0] is saturate(z * 2^126): exact except for denormal z.
 template <int HC, int U, int NL>
-__device__ __forceinline__ void lg_bwd_targets(float (&dxr)[HC], float (&gbias)[HC], int i, int n, int c0, bool hi,
+__device__ __forceinline__ void lg_bwd_targets(float (&dxr)[HC], float (&gbias)[HC], int i, bool real, int c0, bool hi,
                                                const float* vec, char* lds, const LgLayout& m) {
 #pragma unroll
   for (int k = 0; k < HC; ++k) dxr[k] = 0.f;
-  if (i >= n) return;
+  if (!real) return;
   const float* XL = reinterpret_cast<const float*>(lds + m.xl);
   const float* XR = reinterpret_cast<const float*>(lds + m.xr);
   const float* DY = reinterpret_cast<const float*>(lds + m.dy);
@@ -557,11 +614,11 @@ __device__ __forceinline__ void lg_bwd_targets(float (&dxr)[HC], float (&gbias)[
 // step 3: per source node j through the source-sorted CSR -- d x_l[j] and the attention-vector gradient (U
 // out-messages at a time: ids, then the target rows of x_r and dY, all loaded before use)
 template <int HC, int U>
-__device__ __forceinline__ void lg_bwd_sources(float (&dxl)[HC], float (&gatt)[HC], int j, int n, int c0,
+__device__ __forceinline__ void lg_bwd_sources(float (&dxl)[HC], float (&gatt)[HC], int j, bool real, int c0,
                                                const float* vec, char* lds, const LgLayout& m) {
 #pragma unroll
   for (int k = 0; k < HC; ++k) dxl[k] = 0.f;
-  if (j >= n) return;
+  if (!real) return;
   const float* XL = reinterpret_cast<const float*>(lds + m.xl);
   const float* XR = reinterpret_cast<const float*>(lds + m.xr);
   const float* DY = reinterpret_cast<const float*>(lds + m.dy);
@@ -674,19 +731,27 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
   LgClock clk{};
   if (PROF) clk.last = __builtin_amdgcn_s_memtime();
   int* wq = reinterpret_cast<int*>(lds + m.wq);
-  for (long b = lg_next_graph(a, wq, -1); b < a.B; b = lg_next_graph(a, wq, b)) {
-    const int t = a.topo[b], n = a.nnodes[t];
+  const long npk = (a.B + m.G - 1) / m.G;
+  for (long pk = lg_next_graph(a, wq, -1); pk < npk; pk = lg_next_graph(a, wq, pk)) {
+    const long b0 = pk * m.G;
     {
       const int tq = lg_tid(), iq = tq / NL, hq = tq % NL, cq = hq * HC;
-      float xv[8], dy0[HC];
-      lg_load_x(xv, a, b, iq, hq);
-#pragma unroll
-      for (int k = 0; k < HC; ++k) dy0[k] = (iq < n && cq + k < a.H) ? a.demb[b * a.H + cq + k] / (float)n : 0.f;
-      __syncthreads();  // the previous graph is done with every LDS image
+      float xv[8];
+      lg_load_x(xv, a, m, b0, iq, hq);
+      __syncthreads();  // the previous pack is done with every LDS image
       LG_MARK(PROF, clk, 0);
-      lg_stage_topo<true, NT>(a, t, lds, m);
+      lg_stage_topo<true, NT>(a, b0, lds, m);
       lg_put_x(reinterpret_cast<__bf16*>(lds + m.slot[m.xs]), xv, iq, hq, m);
-      if (iq < m.P) lg_store_f<HC>(DY + iq * m.RS + cq, dy0);  // d emb / n on every real node (L >= 2: no ReLU)
+      // d emb / n of node iq's graph on every real node (L >= 2: no ReLU after the last conv)
+      const int* gm = reinterpret_cast<const int*>(lds + m.gm);
+      const int g = iq / m.NP;
+      // (from the pack meta, visible since lg_stage_topo's barrier; the node-valid bytes are not yet)
+      const bool real = iq < m.P && iq - g * m.NP < gm[8 + g];
+      const float rn = real ? 1.f / (float)gm[8 + g] : 0.f;
+      float dy0[HC];
+#pragma unroll
+      for (int k = 0; k < HC; ++k) dy0[k] = (real && cq + k < a.H) ? a.demb[(b0 + g) * a.H + cq + k] * rn : 0.f;
+      if (iq < m.P) lg_store_f<HC>(DY + iq * m.RS + cq, dy0);
       __syncthreads();
       LG_MARK(PROF, clk, 1);
     }
@@ -704,7 +769,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
       const int tq = lg_tid(), pq = tq / NL, cq = (tq % NL) * HC;
       const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
       float y[HC];
-      lg_attend<HC, kLgUb, NL>(y, iq, n, cq, cq + HC == HV, vb, true, XL, XR, iptr, isrc, deg, m);
+      lg_attend<HC, kLgUb, NL>(y, iq, lg_real(lds, m, iq), cq, cq + HC == HV, vb, true, XL, XR, iptr, isrc, deg, m);
       __syncthreads();
       LG_MARK(PROF, clk, 3);
       if (iq < m.P32) lg_store_bf16<HC>(reinterpret_cast<__bf16*>(lds + m.slot[l]) + iq * kMfRS + cq, y);
@@ -720,7 +785,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
       if (l == 0 && a.L >= 2) {  // the input image again (its slot held conv L-2's output meanwhile)
         const int tq = lg_tid();
         float xv[8];
-        lg_load_x(xv, a, b, tq / NL, tq % NL);
+        lg_load_x(xv, a, m, b0, tq / NL, tq % NL);
         lg_put_x(Sin, xv, tq / NL, tq % NL, m);
         __syncthreads();
         LG_MARK(PROF, clk, 5);
@@ -741,7 +806,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
         const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
 #pragma unroll
         for (int k = 0; k < HC; ++k) gv[k] = 0.f;
-        lg_bwd_targets<HC, kLgUb, NL>(dxr, gv, iq, n, cq, cq + HC == HV, vb, lds, m);
+        lg_bwd_targets<HC, kLgUb, NL>(dxr, gv, iq, lg_real(lds, m, iq), cq, cq + HC == HV, vb, lds, m);
         lg_wave_accum<HC, NL>(reinterpret_cast<float*>(lds + m.wacc) + (wave * 4 + 2 * blk + 1) * 32 + cq, gv, tq & 63);
       }
       __syncthreads();
@@ -751,7 +816,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
         const int jq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[m.P + pq] : pq;
 #pragma unroll
         for (int k = 0; k < HC; ++k) gv[k] = 0.f;
-        lg_bwd_sources<HC, kLgUb>(dxl, gv, jq, n, cq, vb, lds, m);
+        lg_bwd_sources<HC, kLgUb>(dxl, gv, jq, lg_real(lds, m, jq), cq, vb, lds, m);
         lg_wave_accum<HC, NL>(reinterpret_cast<float*>(lds + m.wacc) + (wave * 4 + 2 * blk) * 32 + cq, gv, tq & 63);
       }
       __syncthreads();  // XL / XR / DY are dead: their region takes DT / DN
@@ -871,11 +936,30 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-static LgLayout lg_layout(const ClArgs& a, int HV, bool bwd) {
+static LgLayout lg_layout_g(const ClArgs& a, int HV, bool bwd, int G);
+static int lg_hv(int H);
+
+// graphs per pack: one graph of 65 .. 256 nodes, else the most n_pad-node graphs (<= 8, <= 256 lane groups) whose
+// forward and backward working sets fit the CU's LDS (n_pad 50: 4 graphs = 200 nodes, as config 5's one graph)
+static int lg_pack(const ClArgs& a) {
+  if (a.P > 128) return 1;
+  for (int G = (256 / a.P > 8 ? 8 : 256 / a.P); G > 1; --G) {
+    if ((long)G * a.M > 8192) continue;
+    const int HV = lg_hv(a.H);
+    if (lg_layout_g(a, HV, false, G).total <= 160 * 1024 && lg_layout_g(a, HV, true, G).total <= 160 * 1024) return G;
+  }
+  return 1;
+}
+
+static LgLayout lg_layout(const ClArgs& a, int HV, bool bwd) { return lg_layout_g(a, HV, bwd, lg_pack(a)); }
+
+static LgLayout lg_layout_g(const ClArgs& a, int HV, bool bwd, int G) {
   LgLayout m{};
-  m.P = a.P;
-  m.P32 = (a.P + 31) & ~31;
-  m.PK = (a.P + 15) & ~15;
+  m.G = G;
+  m.NP = a.P;
+  m.P = m.G * a.P;
+  m.P32 = (m.P + 31) & ~31;
+  m.PK = (m.P + 15) & ~15;
   m.RS = HV + 4;   // 16 B x odd: the per-message row gathers spread over the bank quads
   m.TS = m.PK + 8;
   m.L = a.L;
@@ -887,7 +971,7 @@ static LgLayout lg_layout(const ClArgs& a, int HV, bool bwd) {
     o += (int)((bytes + 15) & ~15L);
     return at;
   };
-  const int M = a.M;
+  const int M = m.G * a.M;  // the pack's messages
   m.frag = take((bwd ? 3 : 2) * 4 * 64 * 16);
   m.vec = take(2 * kMfVec * 4);
   m.ord = take(2 * m.P * 2);
@@ -916,6 +1000,8 @@ static LgLayout lg_layout(const ClArgs& a, int HV, bool bwd) {
   if (bwd) m.ht = take(dt);
   m.red = take((bwd ? kLgBwdThreads : kLgThreads) / 64 * 32 * 4);  // one 32-channel partial per wave
   m.wq = take(16);
+  m.gm = take(25 * 4);
+  m.nv = take(m.P);
   if (bwd) m.wacc = take(kLgBwdThreads / 64 * 128 * 4);
   m.total = o;
   return m;
@@ -943,17 +1029,26 @@ std::vector<unsigned long long> gnn_lg_prof() {
 
 static int lg_hv(int H) { return H < 16 ? 16 : (H < 24 ? 24 : 32); }  // H < HV: channel HV - 1 free for u / v
 
+// GSC_GNN_LG_PACK=0: 33 .. 64-node graphs stay on the multi-tile kernels (gnn_mt.hip) instead of packs here
+bool gnn_lg_pack_enabled() {
+  const char* e = getenv("GSC_GNN_LG_PACK");
+  return !(e && e[0] == '0');
+}
+
 bool gnn_lg_supported(int Fin, int H, int NM, int P, int M, int L, int n_blocks, const int* layer_of) {
   // encoder + one shared process block, >= 2 convs (no ReLU after the last), bias gradients from a ones row of
-  // the augmented dW product (F_in, H < 32), node ids / message positions as u16
-  if (!(Fin >= 1 && Fin <= 16 && H >= 1 && H <= 31 && NM > 64 && P >= NM && P <= kLgMaxNodes && M <= 8192 && L >= 2 &&
-        L <= kClMaxLayers && n_blocks == 2))
+  // the augmented dW product (F_in, H < 32), node ids / message positions as u16; graphs of 65 .. 256 nodes one
+  // per workgroup, 33 .. 64-node graphs (n_pad <= 128) in packs of 256 / n_pad
+  const bool big = NM > 64, packed = NM > 32 && P <= 128 && gnn_lg_pack_enabled();
+  if (!(Fin >= 1 && Fin <= 16 && H >= 1 && H <= 31 && (big || packed) && P >= NM && P <= kLgMaxNodes && M <= 8192 &&
+        L >= 2 && L <= kClMaxLayers && n_blocks == 2))
     return false;
   for (int l = 0; l < L; ++l)
     if ((l == 0) != (layer_of[l] == 0)) return false;
   ClArgs a{};
   a.Fin = Fin; a.H = H; a.NM = NM; a.M = M; a.P = P; a.L = L; a.n_blocks = n_blocks;
   const int HV = lg_hv(H);
+  if (packed && !big && lg_pack(a) < 2) return false;  // a pack of one small graph: the multi-tile kernels
   return lg_layout(a, HV, false).total <= 160 * 1024 && lg_layout(a, HV, true).total <= 160 * 1024;
 }
 
@@ -968,7 +1063,8 @@ static void lg_launch_fwd(const ClArgs& a, hipStream_t st, int cus) {
   int per_cu = (int)((160 * 1024) / lds);
   per_cu = per_cu > 2 ? 2 : (per_cu < 1 ? 1 : per_cu);
   long grid = (long)cus * per_cu;
-  if (grid > a.B) grid = a.B;
+  const long npk = (a.B + m.G - 1) / m.G;
+  if (grid > npk) grid = npk;
   if (grid < 1) grid = 1;
   if (prof) hipLaunchKernelGGL((gnn_lg_fwd_kernel<HV, true>), dim3((unsigned)grid), dim3(kLgThreads), lds, st, a, m, g_lg_prof);
   else hipLaunchKernelGGL((gnn_lg_fwd_kernel<HV, false>), dim3((unsigned)grid), dim3(kLgThreads), lds, st, a, m, nullptr);
@@ -987,7 +1083,8 @@ static int lg_launch_bwd(const ClArgs& a, hipStream_t st, int cus, int max_rows)
                        : (prof ? (const void*)gnn_lg_bwd_kernel<HV, 4, true> : (const void*)gnn_lg_bwd_kernel<HV, 4, false>);
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   long grid = cus;
-  if (grid > a.B) grid = a.B;
+  const long npk = (a.B + m.G - 1) / m.G;
+  if (grid > npk) grid = npk;
   if (grid > max_rows) grid = max_rows;
   if (grid < 1) grid = 1;
   const dim3 blk(nl2 ? 512 : kLgBwdThreads);
@@ -1014,7 +1111,8 @@ static int lg_launch_bwd(const ClArgs& a, hipStream_t st, int cus, int max_rows)
 }
 
 static void lg_check(const ClArgs& a) {
-  GSC_CHECK(a.P <= kLgMaxNodes && a.P >= a.NM && a.M <= 8192 && a.H <= 31 && a.Fin <= 16 && a.L >= 2 && a.n_blocks == 2,
+  GSC_CHECK(a.P <= kLgMaxNodes && a.P >= a.NM && (long)lg_pack(a) * a.M <= 8192 && a.H <= 31 && a.Fin <= 16 &&
+                a.L >= 2 && a.n_blocks == 2,
             "large-graph fused GNN: shape outside the kernel's assumptions (gnn_lg_supported)");
 }
 

@@ -26,7 +26,7 @@ def _mixed(P=200):
     return GraphSet(topos, P, DEV)
 
 
-def _check(gs, P, B, layers=2, iters=2, hidden=22, seed=0):
+def _check(gs, P, B, layers=2, iters=2, hidden=22, seed=0, tol=3e-2):
     from gsc_amd.native import load
     from gsc_amd.ops.gnn import _tables, gnn_fits
     torch.manual_seed(seed)
@@ -43,7 +43,7 @@ def _check(gs, P, B, layers=2, iters=2, hidden=22, seed=0):
     gout = torch.autograd.grad((out * w).sum(), params)
     assert _rel(out, ref) < 1e-2, _rel(out, ref)
     for i, (a, b) in enumerate(zip(gout, gref)):
-        assert _rel(a, b) < 3e-2, (i, a.shape, _rel(a, b))
+        assert _rel(a, b) < tol, (i, a.shape, _rel(a, b))
     return emb, x, topo, out, gout
 
 
@@ -108,3 +108,22 @@ def test_lg_cu_budget_grid():
         _check(GraphSet([load_topology(p) for p in SYN200], 200, DEV), 200, 500)
     finally:
         nat.gnn_set_cu_budget(0)
+
+
+SYN50 = [cfg_path("networks", "synthetic", f"syn50-in8-cap1-3{s}.graphml") for s in ("", "-s1", "-s2", "-s3")]
+
+
+@pytest.mark.parametrize("hidden", [22, 16])
+def test_lg_packs_of_50_node_graphs(hidden):
+    """BASELINE config-4 shape (n_pad 50): five graphs per workgroup as one disjoint 250-node graph; B = 1,003 leaves
+    a partial last pack (its missing graphs are empty)."""
+    gs = GraphSet([load_topology(p) for p in SYN50], 50, DEV)
+    _check(gs, 50, 1003, hidden=hidden)
+
+
+def test_lg_packs_mixed_sizes():
+    """n_pad 64 (packs of four): 50 / 53 / 42 / 11-node graphs, padded rows and padded graphs in one pack."""
+    topos = [load_topology(SYN50[0]), load_topology(cfg_path("networks", "tinet", "tinet-in4-rand-cap0-2.graphml")),
+             load_topology(cfg_path("networks", "chinanet", "chinanet-in4-rand-cap0-2.graphml")),
+             load_topology(cfg_path("networks", "abilene", "abilene-in4-rand-cap1-2.graphml"))]
+    _check(GraphSet(topos, 64, DEV), 64, 777, seed=2)

@@ -43,16 +43,20 @@ def test_gnn_native_matches_reference(layers, iters, hidden, fused):
     _check_gnn(layers, iters, hidden, gs, bf16=True)
 
 
+@pytest.mark.parametrize("pack", ["1", "0"], ids=["lg-pack", "mt"])
 @pytest.mark.parametrize("hidden", [22, 32, 16])
-def test_gnn_mfma_two_tiles_matches_reference(hidden):
-    """33..64-node graphs on the two-tile MFMA kernels (gnn_mt.hip): 50-node synthetic, TiNet (53),
-    ChinaNet (42) and Abilene (11, second tile empty) in one batch, forward + backward vs fp32."""
+def test_gnn_mfma_two_tiles_matches_reference(hidden, pack, monkeypatch):
+    """33..64-node graphs: 50-node synthetic, TiNet (53), ChinaNet (42) and Abilene (11, second tile empty) in one
+    batch, forward + backward vs fp32 -- on the two-tile MFMA kernels (gnn_mt.hip; GSC_GNN_LG_PACK=0, and H = 32
+    always) and in packs of four graphs on the large-graph kernels (gnn_lg.hip, H <= 31: nothing saved)."""
     from gsc_amd.native import load
     from gsc_amd.ops.gnn import _tables, gnn_use_fused
+    monkeypatch.setenv("GSC_GNN_LG_PACK", pack)
     gs = _mid_graphs(DEV)
     emb = GNNEmbedder(3, hidden, 2, "mean", 2)
     assert gnn_use_fused(emb, gs, 64, 3)
-    assert load().gnn_saved_bytes(_tables(gs), 64, 3, hidden, [0, 1, 1]) > 0
+    saved = load().gnn_saved_bytes(_tables(gs), 64, 3, hidden, [0, 1, 1])
+    assert (saved == 0) == (pack == "1" and hidden <= 31), saved
     _check_gnn(2, 2, hidden, gs, 64, bf16=True)
 
 
@@ -63,11 +67,13 @@ def test_gnn_50_nodes_padded_50():
     _check_gnn(2, 2, 22, gs, 50, bf16=True)
 
 
-def test_gnn_mfma_two_tiles_work_queue():
+@pytest.mark.parametrize("pack", ["1", "0"], ids=["lg-pack", "mt"])
+def test_gnn_mfma_two_tiles_work_queue(pack, monkeypatch):
     """The overlap mode's two-tile backward: a CU budget set (as the trainer does for its masked learner
-    stream) switches gnn_mt's backward to a full-device grid claiming graphs from a zeroed counter; the
-    gradients must match the fp32 reference as with the fixed-stride grid."""
+    stream) switches the backward to a full-device grid claiming graphs (gnn_mt) or packs (gnn_lg) from a zeroed
+    counter; the gradients must match the fp32 reference as with the fixed-stride grid."""
     from gsc_amd.native import load
+    monkeypatch.setenv("GSC_GNN_LG_PACK", pack)
     nat = load()
     nat.gnn_set_cu_budget(64)
     try:
