@@ -464,8 +464,15 @@ __device__ __forceinline__ void device_step_env(const SimArgs& a, const SimConst
 // LDS_STATE: 0 = the state blob stays in HBM, 1 = the whole blob is staged in LDS, 2 = only its hot
 // prefix is (the [N, C, S, N] schedule / WRR tables stay in HBM: 50- and 200-node topologies).
 // TLDS: the topology tables are staged in LDS (SimContext: topo_stage_ > 0), known at compile time.
+// GSC_SIM_MAX_SGPR (A/B builds only, scripts/sim_sgpr_ab.py): cap the step kernel's SGPR budget to measure what
+// SGPR spills (to VGPR lanes) cost per spill
+#ifdef GSC_SIM_MAX_SGPR
+#define GSC_SIM_SGPR_ATTR __attribute__((amdgpu_num_sgpr(GSC_SIM_MAX_SGPR)))
+#else
+#define GSC_SIM_SGPR_ATTR
+#endif
 template <int QSETS, int LDS_STATE, bool PROF = false, bool TLDS = false>
-__global__ __launch_bounds__(64) void sim_step_kernel(SimArgs a) {
+__global__ __launch_bounds__(64) GSC_SIM_SGPR_ATTR void sim_step_kernel(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int env = blockIdx.x;
   const int lane = threadIdx.x;
