@@ -318,7 +318,7 @@ __device__ __forceinline__ void lg_attend(float (&y)[HC], int i, bool real, int 
 // the graphs (rank p -> graph p mod G, that graph's node of degree rank p / G): every wave gets a similar mix.
 // Pack meta (LDS ints): [0, 8) topology (-1: empty), [8, 16) real nodes, [16, 25) message offsets.
 template <bool BWD, int NT>
-__device__ __forceinline__ void lg_stage_topo(const ClArgs& a, long b0, char* lds, const LgLayout& m) {
+__device__ __forceinline__ void lg_stage_topo(const ClArgs& a, long b0, int t1, int n1, char* lds, const LgLayout& m) {
   int32_t* iptr = reinterpret_cast<int32_t*>(lds + m.iptr);
   float* deg = reinterpret_cast<float*>(lds + m.deg);
   uint16_t* isrc = reinterpret_cast<uint16_t*>(lds + m.isrc);
@@ -326,6 +326,32 @@ __device__ __forceinline__ void lg_stage_topo(const ClArgs& a, long b0, char* ld
   uint8_t* nv = reinterpret_cast<uint8_t*>(lds + m.nv);
   int* gm = reinterpret_cast<int*>(lds + m.gm);
   const int P = m.P, NP = m.NP, G = m.G, M = a.M;
+  if (G == 1) {  // one graph (topology t1, n1 nodes: loaded by the caller before its barrier): its tables as they are
+    const int t = t1, n = n1;
+    if (threadIdx.x == 0) {
+      gm[0] = t;
+      gm[8] = n;
+      gm[16] = 0;
+      gm[17] = a.in_ptr[(long)t * (P + 1) + P];
+    }
+    for (int k = threadIdx.x; k < 2 * P; k += NT) ord[k] = (uint16_t)a.deg_order[(long)t * 2 * P + k];
+    for (int k = threadIdx.x; k <= P; k += NT) {
+      iptr[k] = a.in_ptr[(long)t * (P + 1) + k];
+      if (k < P) {
+        deg[k] = a.deg[(long)t * P + k];
+        nv[k] = (uint8_t)(k < n);
+      }
+      if (BWD) reinterpret_cast<int32_t*>(lds + m.optr)[k] = a.out_ptr[(long)t * (P + 1) + k];
+    }
+    for (int k = threadIdx.x; k < M; k += NT) {
+      isrc[k] = (uint16_t)a.in_src[(long)t * M + k];
+      if (BWD) {
+        reinterpret_cast<uint16_t*>(lds + m.oq)[k] = (uint16_t)a.out_q[(long)t * M + k];
+        reinterpret_cast<uint16_t*>(lds + m.odst)[k] = (uint16_t)a.out_dst[(long)t * M + k];
+      }
+    }
+    return;
+  }
   if (threadIdx.x == 0) {
     int off = 0;
     for (int g = 0; g < G; ++g) {
@@ -368,8 +394,9 @@ __device__ __forceinline__ void lg_stage_topo(const ClArgs& a, long b0, char* ld
   }
 }
 
-// node u of the pack is a real node (not padding, not an empty graph's)
-__device__ __forceinline__ bool lg_real(const char* lds, const LgLayout& m, int u) {
+// node u of the pack is a real node (not padding, not an empty graph's); G = 1: u < n1, the graph's node count
+__device__ __forceinline__ bool lg_real(const char* lds, const LgLayout& m, int u, int n1) {
+  if (m.G == 1) return u < n1;
   return u < m.P && reinterpret_cast<const uint8_t*>(lds + m.nv)[u] != 0;
 }
 
@@ -377,7 +404,7 @@ __device__ __forceinline__ bool lg_real(const char* lds, const LgLayout& m, int 
 // past F_in, for rows >= P and for graphs past the batch)
 // (g = the lane's position in its node group: lanes 0 / 1 of the group take channels 0..7 / 8..15)
 __device__ __forceinline__ void lg_load_x(float (&xv)[8], const ClArgs& a, const LgLayout& m, long b0, int i, int g) {
-  const int gi = i / m.NP, v = i - gi * m.NP;
+  const int gi = m.G == 1 ? 0 : i / m.NP, v = i - gi * m.NP;
   const long b = b0 + gi;
   const bool ok = i < m.P && g < 2 && b < a.B;
 #pragma unroll
@@ -432,13 +459,14 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
   const long npk = (a.B + m.G - 1) / m.G;
   for (long pk = lg_next_graph(a, wq, -1); pk < npk; pk = lg_next_graph(a, wq, pk)) {
     const long b0 = pk * m.G;
+    const int t1 = a.topo[b0], n1 = a.nnodes[t1];  // (G = 1: the staging's topology, loaded before the barrier)
     {
       const int tq = lg_tid();
       float xv[8];
       lg_load_x(xv, a, m, b0, tq / NL, tq % NL);
       __syncthreads();  // the previous pack is done with every LDS image
       LG_MARK(PROF, clk, 0);
-      lg_stage_topo<false, kLgThreads>(a, b0, lds, m);
+      lg_stage_topo<false, kLgThreads>(a, b0, t1, n1, lds, m);
       lg_put_x(S, xv, tq / NL, tq % NL, m);
       __syncthreads();
       LG_MARK(PROF, clk, 1);
@@ -458,7 +486,7 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
       const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
       float y[HC];
       const bool last = l + 1 == a.L;
-      lg_attend<HC, kLgUf, NL>(y, iq, lg_real(lds, m, iq), cq, cq + HC == HV, vb, !last, XL, XR, iptr, isrc, deg, m);
+      lg_attend<HC, kLgUf, NL>(y, iq, lg_real(lds, m, iq, n1), cq, cq + HC == HV, vb, !last, XL, XR, iptr, isrc, deg, m);
       if (!last) {
         __syncthreads();  // S (this conv's input) was read by the node linears before the previous barrier;
                           // the barrier orders this conv's XL reads before the next node linears' XL writes
@@ -734,23 +762,34 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
   const long npk = (a.B + m.G - 1) / m.G;
   for (long pk = lg_next_graph(a, wq, -1); pk < npk; pk = lg_next_graph(a, wq, pk)) {
     const long b0 = pk * m.G;
+    const int t1 = a.topo[b0], n1 = a.nnodes[t1];  // (G = 1: the staging's topology, loaded before the barrier)
     {
       const int tq = lg_tid(), iq = tq / NL, hq = tq % NL, cq = hq * HC;
-      float xv[8];
+      float xv[8], dy0[HC];
       lg_load_x(xv, a, m, b0, iq, hq);
+      // d emb / n on every real node of the node's graph (L >= 2: no ReLU after the last conv); G = 1: loaded
+      // before the barrier
+      if (m.G == 1) {  // raw loads (no dependence on n1: they overlap the barrier), masked after it
+#pragma unroll
+        for (int k = 0; k < HC; ++k) dy0[k] = a.demb[b0 * a.H + min(cq + k, a.H - 1)];
+      }
       __syncthreads();  // the previous pack is done with every LDS image
       LG_MARK(PROF, clk, 0);
-      lg_stage_topo<true, NT>(a, b0, lds, m);
+      lg_stage_topo<true, NT>(a, b0, t1, n1, lds, m);
       lg_put_x(reinterpret_cast<__bf16*>(lds + m.slot[m.xs]), xv, iq, hq, m);
-      // d emb / n of node iq's graph on every real node (L >= 2: no ReLU after the last conv)
-      const int* gm = reinterpret_cast<const int*>(lds + m.gm);
-      const int g = iq / m.NP;
-      // (from the pack meta, visible since lg_stage_topo's barrier; the node-valid bytes are not yet)
-      const bool real = iq < m.P && iq - g * m.NP < gm[8 + g];
-      const float rn = real ? 1.f / (float)gm[8 + g] : 0.f;
-      float dy0[HC];
+      if (m.G == 1) {
+        const float rn = 1.f / (float)n1;
 #pragma unroll
-      for (int k = 0; k < HC; ++k) dy0[k] = (real && cq + k < a.H) ? a.demb[(b0 + g) * a.H + cq + k] * rn : 0.f;
+        for (int k = 0; k < HC; ++k) dy0[k] = (iq < n1 && cq + k < a.H) ? dy0[k] * rn : 0.f;
+      }
+      if (m.G > 1) {  // the node's graph from the pack meta (visible since lg_stage_topo's barrier)
+        const int* gm = reinterpret_cast<const int*>(lds + m.gm);
+        const int g = iq / m.NP, ng = gm[8 + g];
+        const bool real = iq < m.P && iq - g * m.NP < ng;
+        const float rn = real ? 1.f / (float)ng : 0.f;
+#pragma unroll
+        for (int k = 0; k < HC; ++k) dy0[k] = (real && cq + k < a.H) ? a.demb[(b0 + g) * a.H + cq + k] * rn : 0.f;
+      }
       if (iq < m.P) lg_store_f<HC>(DY + iq * m.RS + cq, dy0);
       __syncthreads();
       LG_MARK(PROF, clk, 1);
@@ -769,7 +808,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
       const int tq = lg_tid(), pq = tq / NL, cq = (tq % NL) * HC;
       const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
       float y[HC];
-      lg_attend<HC, kLgUb, NL>(y, iq, lg_real(lds, m, iq), cq, cq + HC == HV, vb, true, XL, XR, iptr, isrc, deg, m);
+      lg_attend<HC, kLgUb, NL>(y, iq, lg_real(lds, m, iq, n1), cq, cq + HC == HV, vb, true, XL, XR, iptr, isrc, deg, m);
       __syncthreads();
       LG_MARK(PROF, clk, 3);
       if (iq < m.P32) lg_store_bf16<HC>(reinterpret_cast<__bf16*>(lds + m.slot[l]) + iq * kMfRS + cq, y);
@@ -806,7 +845,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
         const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
 #pragma unroll
         for (int k = 0; k < HC; ++k) gv[k] = 0.f;
-        lg_bwd_targets<HC, kLgUb, NL>(dxr, gv, iq, lg_real(lds, m, iq), cq, cq + HC == HV, vb, lds, m);
+        lg_bwd_targets<HC, kLgUb, NL>(dxr, gv, iq, lg_real(lds, m, iq, n1), cq, cq + HC == HV, vb, lds, m);
         lg_wave_accum<HC, NL>(reinterpret_cast<float*>(lds + m.wacc) + (wave * 4 + 2 * blk + 1) * 32 + cq, gv, tq & 63);
       }
       __syncthreads();
@@ -816,7 +855,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
         const int jq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[m.P + pq] : pq;
 #pragma unroll
         for (int k = 0; k < HC; ++k) gv[k] = 0.f;
-        lg_bwd_sources<HC, kLgUb>(dxl, gv, jq, lg_real(lds, m, jq), cq, vb, lds, m);
+        lg_bwd_sources<HC, kLgUb>(dxl, gv, jq, lg_real(lds, m, jq, n1), cq, vb, lds, m);
         lg_wave_accum<HC, NL>(reinterpret_cast<float*>(lds + m.wacc) + (wave * 4 + 2 * blk) * 32 + cq, gv, tq & 63);
       }
       __syncthreads();  // XL / XR / DY are dead: their region takes DT / DN
@@ -1039,7 +1078,8 @@ bool gnn_lg_supported(int Fin, int H, int NM, int P, int M, int L, int n_blocks,
   // encoder + one shared process block, >= 2 convs (no ReLU after the last), bias gradients from a ones row of
   // the augmented dW product (F_in, H < 32), node ids / message positions as u16; graphs of 65 .. 256 nodes one
   // per workgroup, 33 .. 64-node graphs (n_pad <= 128) in packs of 256 / n_pad
-  const bool big = NM > 64, packed = NM > 32 && P <= 128 && gnn_lg_pack_enabled();
+  const char* pk = getenv("GSC_GNN_LG_PACK");
+  const bool big = NM > 64, packed = NM > (pk && pk[0] == '2' ? 0 : 32) && P <= 128 && gnn_lg_pack_enabled();
   if (!(Fin >= 1 && Fin <= 16 && H >= 1 && H <= 31 && (big || packed) && P >= NM && P <= kLgMaxNodes && M <= 8192 &&
         L >= 2 && L <= kClMaxLayers && n_blocks == 2))
     return false;
