@@ -317,7 +317,7 @@ __device__ __forceinline__ void lg_attend(float (&y)[HC], int i, bool real, int 
 // empty (no real nodes, no messages).  G = 1 (200 nodes): the topology of b0 as is.  Lane-pair order interleaves
 // the graphs (rank p -> graph p mod G, that graph's node of degree rank p / G): every wave gets a similar mix.
 // Pack meta (LDS ints): [0, 8) topology (-1: empty), [8, 16) real nodes, [16, 25) message offsets.
-template <bool BWD, int NT>
+template <bool BWD, int NT, bool PK>
 __device__ __forceinline__ void lg_stage_topo(const ClArgs& a, long b0, int t1, int n1, char* lds, const LgLayout& m) {
   int32_t* iptr = reinterpret_cast<int32_t*>(lds + m.iptr);
   float* deg = reinterpret_cast<float*>(lds + m.deg);
@@ -325,22 +325,14 @@ __device__ __forceinline__ void lg_stage_topo(const ClArgs& a, long b0, int t1, 
   uint16_t* ord = reinterpret_cast<uint16_t*>(lds + m.ord);
   uint8_t* nv = reinterpret_cast<uint8_t*>(lds + m.nv);
   int* gm = reinterpret_cast<int*>(lds + m.gm);
-  const int P = m.P, NP = m.NP, G = m.G, M = a.M;
-  if (G == 1) {  // one graph (topology t1, n1 nodes: loaded by the caller before its barrier): its tables as they are
-    const int t = t1, n = n1;
-    if (threadIdx.x == 0) {
-      gm[0] = t;
-      gm[8] = n;
-      gm[16] = 0;
-      gm[17] = a.in_ptr[(long)t * (P + 1) + P];
-    }
+  const int P = m.P, NP = m.NP, G = PK ? m.G : 1, M = a.M;
+  if constexpr (!PK) {  // one graph (topology t1, n1 nodes: loaded by the caller before its barrier): its tables as they are
+    const int t = t1;
+    if (threadIdx.x == 0) gm[8] = n1;  // (the pooling's node count; validity is u < n1 in registers)
     for (int k = threadIdx.x; k < 2 * P; k += NT) ord[k] = (uint16_t)a.deg_order[(long)t * 2 * P + k];
     for (int k = threadIdx.x; k <= P; k += NT) {
       iptr[k] = a.in_ptr[(long)t * (P + 1) + k];
-      if (k < P) {
-        deg[k] = a.deg[(long)t * P + k];
-        nv[k] = (uint8_t)(k < n);
-      }
+      if (k < P) deg[k] = a.deg[(long)t * P + k];
       if (BWD) reinterpret_cast<int32_t*>(lds + m.optr)[k] = a.out_ptr[(long)t * (P + 1) + k];
     }
     for (int k = threadIdx.x; k < M; k += NT) {
@@ -395,16 +387,18 @@ __device__ __forceinline__ void lg_stage_topo(const ClArgs& a, long b0, int t1, 
 }
 
 // node u of the pack is a real node (not padding, not an empty graph's); G = 1: u < n1, the graph's node count
+template <bool PK>
 __device__ __forceinline__ bool lg_real(const char* lds, const LgLayout& m, int u, int n1) {
-  if (m.G == 1) return u < n1;
+  if constexpr (!PK) return u < n1;
   return u < m.P && reinterpret_cast<const uint8_t*>(lds + m.nv)[u] != 0;
 }
 
 // input rows of pack node i (graph b0 + i / NP, node i mod NP) as the bf16 image (channels 0..15: F_in <= 16, zero
 // past F_in, for rows >= P and for graphs past the batch)
 // (g = the lane's position in its node group: lanes 0 / 1 of the group take channels 0..7 / 8..15)
+template <bool PK>
 __device__ __forceinline__ void lg_load_x(float (&xv)[8], const ClArgs& a, const LgLayout& m, long b0, int i, int g) {
-  const int gi = m.G == 1 ? 0 : i / m.NP, v = i - gi * m.NP;
+  const int gi = PK ? i / m.NP : 0, v = i - gi * m.NP;
   const long b = b0 + gi;
   const bool ok = i < m.P && g < 2 && b < a.B;
 #pragma unroll
@@ -438,7 +432,7 @@ __device__ __forceinline__ void lg_zero(char* p, int bytes) {
 // ---------------------------------------------------------------------------------------------
 // forward: emb[b] = mean over real nodes of the last conv's rows (a.params2 / a.emb2: unused here; two launches)
 // ---------------------------------------------------------------------------------------------
-template <int HV, bool PROF>
+template <int HV, bool PROF, bool PK>
 __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4))) void gnn_lg_fwd_kernel(ClArgs a, LgLayout m, unsigned long long* prof) {
   constexpr int NL = 2, HC = HV / NL;  // lane pairs: 2 workgroups of 8 waves per CU
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -456,17 +450,18 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
   LgClock clk{};
   if (PROF) clk.last = __builtin_amdgcn_s_memtime();
   int* wq = reinterpret_cast<int*>(lds + m.wq);
-  const long npk = (a.B + m.G - 1) / m.G;
+  const int G = PK ? m.G : 1;  // graphs per pack (PK: packs of small graphs; else one graph per workgroup)
+  const long npk = (a.B + G - 1) / G;
   for (long pk = lg_next_graph(a, wq, -1); pk < npk; pk = lg_next_graph(a, wq, pk)) {
-    const long b0 = pk * m.G;
+    const long b0 = pk * G;
     const int t1 = a.topo[b0], n1 = a.nnodes[t1];  // (G = 1: the staging's topology, loaded before the barrier)
     {
       const int tq = lg_tid();
       float xv[8];
-      lg_load_x(xv, a, m, b0, tq / NL, tq % NL);
+      lg_load_x<PK>(xv, a, m, b0, tq / NL, tq % NL);
       __syncthreads();  // the previous pack is done with every LDS image
       LG_MARK(PROF, clk, 0);
-      lg_stage_topo<false, kLgThreads>(a, b0, t1, n1, lds, m);
+      lg_stage_topo<false, kLgThreads, PK>(a, b0, t1, n1, lds, m);
       lg_put_x(S, xv, tq / NL, tq % NL, m);
       __syncthreads();
       LG_MARK(PROF, clk, 1);
@@ -486,7 +481,7 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
       const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
       float y[HC];
       const bool last = l + 1 == a.L;
-      lg_attend<HC, kLgUf, NL>(y, iq, lg_real(lds, m, iq, n1), cq, cq + HC == HV, vb, !last, XL, XR, iptr, isrc, deg, m);
+      lg_attend<HC, kLgUf, NL>(y, iq, lg_real<PK>(lds, m, iq, n1), cq, cq + HC == HV, vb, !last, XL, XR, iptr, isrc, deg, m);
       if (!last) {
         __syncthreads();  // S (this conv's input) was read by the node linears before the previous barrier;
                           // the barrier orders this conv's XL reads before the next node linears' XL writes
@@ -494,7 +489,7 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
         if (iq < m.P32) lg_store_bf16<HC>(S + iq * kMfRS + cq, y);
         __syncthreads();
         LG_MARK(PROF, clk, 4);
-      } else if (m.G == 1) {  // mean pool over the real nodes: wave sums (DPP + two swaps), then the waves in a fixed order
+      } else if (!PK) {  // mean pool over the real nodes: wave sums (DPP + two swaps), then the waves in a fixed order
 #pragma unroll
         for (int k = 0; k < HC; ++k) {
           const float v = lg_wave_sum<NL>(y[k]);  // y is zero for nodes that are not real
@@ -512,7 +507,7 @@ __global__ __launch_bounds__(kLgThreads) __attribute__((amdgpu_waves_per_eu(4, 4
         __syncthreads();  // every lane's XR reads are done
         if (iq < m.P) lg_store_f<HC>(XR + iq * m.RS + cq, y);
         __syncthreads();
-        if (tq < m.G * a.H) {
+        if (tq < G * a.H) {
           const int g = tq / a.H, c = tq - g * a.H, n = gm[8 + g];
           float s = 0.f;
           for (int v = 0; v < n; ++v) s += XR[(g * m.NP + v) * m.RS + c];
@@ -728,7 +723,7 @@ __device__ __forceinline__ void lg_put_ht(__bf16* HT, const __bf16* S, int i, in
   if (Fi >= HV && c0 + HC == HV) HT[Fi * m.TS + i] = (__bf16)(i < m.P ? 1.f : 0.f);  // ones row past the channels
 }
 
-template <int HV, int NL, bool PROF>
+template <int HV, int NL, bool PROF, bool PK>
 __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout m, unsigned long long* prof) {
   // node groups of NL lanes (HV / NL channels each).  NL = 4: 16 waves, so the one workgroup an LDS-full CU holds
   // still has 4 waves per SIMD to hide the message loops' LDS latency
@@ -759,30 +754,31 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
   LgClock clk{};
   if (PROF) clk.last = __builtin_amdgcn_s_memtime();
   int* wq = reinterpret_cast<int*>(lds + m.wq);
-  const long npk = (a.B + m.G - 1) / m.G;
+  const int G = PK ? m.G : 1;  // graphs per pack (PK: packs of small graphs; else one graph per workgroup)
+  const long npk = (a.B + G - 1) / G;
   for (long pk = lg_next_graph(a, wq, -1); pk < npk; pk = lg_next_graph(a, wq, pk)) {
-    const long b0 = pk * m.G;
+    const long b0 = pk * G;
     const int t1 = a.topo[b0], n1 = a.nnodes[t1];  // (G = 1: the staging's topology, loaded before the barrier)
     {
       const int tq = lg_tid(), iq = tq / NL, hq = tq % NL, cq = hq * HC;
       float xv[8], dy0[HC];
-      lg_load_x(xv, a, m, b0, iq, hq);
+      lg_load_x<PK>(xv, a, m, b0, iq, hq);
       // d emb / n on every real node of the node's graph (L >= 2: no ReLU after the last conv); G = 1: loaded
       // before the barrier
-      if (m.G == 1) {  // raw loads (no dependence on n1: they overlap the barrier), masked after it
+      if (!PK) {  // raw loads (no dependence on n1: they overlap the barrier), masked after it
 #pragma unroll
         for (int k = 0; k < HC; ++k) dy0[k] = a.demb[b0 * a.H + min(cq + k, a.H - 1)];
       }
       __syncthreads();  // the previous pack is done with every LDS image
       LG_MARK(PROF, clk, 0);
-      lg_stage_topo<true, NT>(a, b0, t1, n1, lds, m);
+      lg_stage_topo<true, NT, PK>(a, b0, t1, n1, lds, m);
       lg_put_x(reinterpret_cast<__bf16*>(lds + m.slot[m.xs]), xv, iq, hq, m);
-      if (m.G == 1) {
+      if (!PK) {
         const float rn = 1.f / (float)n1;
 #pragma unroll
         for (int k = 0; k < HC; ++k) dy0[k] = (iq < n1 && cq + k < a.H) ? dy0[k] * rn : 0.f;
       }
-      if (m.G > 1) {  // the node's graph from the pack meta (visible since lg_stage_topo's barrier)
+      if (PK) {  // the node's graph from the pack meta (visible since lg_stage_topo's barrier)
         const int* gm = reinterpret_cast<const int*>(lds + m.gm);
         const int g = iq / m.NP, ng = gm[8 + g];
         const bool real = iq < m.P && iq - g * m.NP < ng;
@@ -808,7 +804,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
       const int tq = lg_tid(), pq = tq / NL, cq = (tq % NL) * HC;
       const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
       float y[HC];
-      lg_attend<HC, kLgUb, NL>(y, iq, lg_real(lds, m, iq, n1), cq, cq + HC == HV, vb, true, XL, XR, iptr, isrc, deg, m);
+      lg_attend<HC, kLgUb, NL>(y, iq, lg_real<PK>(lds, m, iq, n1), cq, cq + HC == HV, vb, true, XL, XR, iptr, isrc, deg, m);
       __syncthreads();
       LG_MARK(PROF, clk, 3);
       if (iq < m.P32) lg_store_bf16<HC>(reinterpret_cast<__bf16*>(lds + m.slot[l]) + iq * kMfRS + cq, y);
@@ -824,7 +820,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
       if (l == 0 && a.L >= 2) {  // the input image again (its slot held conv L-2's output meanwhile)
         const int tq = lg_tid();
         float xv[8];
-        lg_load_x(xv, a, m, b0, tq / NL, tq % NL);
+        lg_load_x<PK>(xv, a, m, b0, tq / NL, tq % NL);
         lg_put_x(Sin, xv, tq / NL, tq % NL, m);
         __syncthreads();
         LG_MARK(PROF, clk, 5);
@@ -845,7 +841,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
         const int iq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[pq] : pq;
 #pragma unroll
         for (int k = 0; k < HC; ++k) gv[k] = 0.f;
-        lg_bwd_targets<HC, kLgUb, NL>(dxr, gv, iq, lg_real(lds, m, iq, n1), cq, cq + HC == HV, vb, lds, m);
+        lg_bwd_targets<HC, kLgUb, NL>(dxr, gv, iq, lg_real<PK>(lds, m, iq, n1), cq, cq + HC == HV, vb, lds, m);
         lg_wave_accum<HC, NL>(reinterpret_cast<float*>(lds + m.wacc) + (wave * 4 + 2 * blk + 1) * 32 + cq, gv, tq & 63);
       }
       __syncthreads();
@@ -855,7 +851,7 @@ __global__ __launch_bounds__(256 * NL) void gnn_lg_bwd_kernel(ClArgs a, LgLayout
         const int jq = pq < m.P ? (int)reinterpret_cast<const uint16_t*>(lds + m.ord)[m.P + pq] : pq;
 #pragma unroll
         for (int k = 0; k < HC; ++k) gv[k] = 0.f;
-        lg_bwd_sources<HC, kLgUb>(dxl, gv, jq, lg_real(lds, m, jq, n1), cq, vb, lds, m);
+        lg_bwd_sources<HC, kLgUb>(dxl, gv, jq, lg_real<PK>(lds, m, jq, n1), cq, vb, lds, m);
         lg_wave_accum<HC, NL>(reinterpret_cast<float*>(lds + m.wacc) + (wave * 4 + 2 * blk) * 32 + cq, gv, tq & 63);
       }
       __syncthreads();  // XL / XR / DY are dead: their region takes DT / DN
@@ -1097,8 +1093,9 @@ static void lg_launch_fwd(const ClArgs& a, hipStream_t st, int cus) {
   const LgLayout m = lg_layout(a, HV, false);
   const size_t lds = m.total;
   GSC_CHECK(lds <= 160 * 1024, "GNN (large-graph fused) forward working set exceeds LDS");
-  const bool prof = lg_prof_on();
-  const void* fn = prof ? (const void*)gnn_lg_fwd_kernel<HV, true> : (const void*)gnn_lg_fwd_kernel<HV, false>;
+  const bool prof = lg_prof_on(), pk = m.G > 1;
+  const void* fn = pk ? (prof ? (const void*)gnn_lg_fwd_kernel<HV, true, true> : (const void*)gnn_lg_fwd_kernel<HV, false, true>)
+                      : (prof ? (const void*)gnn_lg_fwd_kernel<HV, true, false> : (const void*)gnn_lg_fwd_kernel<HV, false, false>);
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int per_cu = (int)((160 * 1024) / lds);
   per_cu = per_cu > 2 ? 2 : (per_cu < 1 ? 1 : per_cu);
@@ -1106,8 +1103,9 @@ static void lg_launch_fwd(const ClArgs& a, hipStream_t st, int cus) {
   const long npk = (a.B + m.G - 1) / m.G;
   if (grid > npk) grid = npk;
   if (grid < 1) grid = 1;
-  if (prof) hipLaunchKernelGGL((gnn_lg_fwd_kernel<HV, true>), dim3((unsigned)grid), dim3(kLgThreads), lds, st, a, m, g_lg_prof);
-  else hipLaunchKernelGGL((gnn_lg_fwd_kernel<HV, false>), dim3((unsigned)grid), dim3(kLgThreads), lds, st, a, m, nullptr);
+  unsigned long long* pr = prof ? g_lg_prof : nullptr;
+  hipLaunchKernelGGL(reinterpret_cast<void (*)(ClArgs, LgLayout, unsigned long long*)>(const_cast<void*>(fn)),
+                     dim3((unsigned)grid), dim3(kLgThreads), lds, st, a, m, pr);
   check_launch();
 }
 
@@ -1116,11 +1114,12 @@ static int lg_launch_bwd(const ClArgs& a, hipStream_t st, int cus, int max_rows)
   const LgLayout m = lg_layout(a, HV, true);
   const size_t lds = m.total;
   GSC_CHECK(lds <= 160 * 1024, "GNN (large-graph fused) backward working set exceeds LDS");
-  const bool prof = lg_prof_on();
+  const bool prof = lg_prof_on(), pk = m.G > 1;
   const char* e = getenv("GSC_LG_BWD_NL");
-  const bool nl2 = e && e[0] == '2';
-  const void* fn = nl2 ? (prof ? (const void*)gnn_lg_bwd_kernel<HV, 2, true> : (const void*)gnn_lg_bwd_kernel<HV, 2, false>)
-                       : (prof ? (const void*)gnn_lg_bwd_kernel<HV, 4, true> : (const void*)gnn_lg_bwd_kernel<HV, 4, false>);
+  const bool nl2 = e && e[0] == '2' && !pk;  // (A/B knob of the one-graph kernels)
+  const void* fn = pk ? (prof ? (const void*)gnn_lg_bwd_kernel<HV, 4, true, true> : (const void*)gnn_lg_bwd_kernel<HV, 4, false, true>)
+                 : nl2 ? (prof ? (const void*)gnn_lg_bwd_kernel<HV, 2, true, false> : (const void*)gnn_lg_bwd_kernel<HV, 2, false, false>)
+                       : (prof ? (const void*)gnn_lg_bwd_kernel<HV, 4, true, false> : (const void*)gnn_lg_bwd_kernel<HV, 4, false, false>);
   if (lds > 65536) GSC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   long grid = cus;
   const long npk = (a.B + m.G - 1) / m.G;
@@ -1139,13 +1138,9 @@ static int lg_launch_bwd(const ClArgs& a, hipStream_t st, int cus, int max_rows)
                   " B LDS exceed the kernel's limits (" + std::to_string(fa.maxThreadsPerBlock) + " threads, " +
                   std::to_string(maxlds) + " B)");
   }
-  if (nl2) {
-    if (prof) hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, 2, true>), dim3((unsigned)grid), blk, lds, st, a, m, g_lg_prof);
-    else hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, 2, false>), dim3((unsigned)grid), blk, lds, st, a, m, nullptr);
-  } else {
-    if (prof) hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, 4, true>), dim3((unsigned)grid), blk, lds, st, a, m, g_lg_prof);
-    else hipLaunchKernelGGL((gnn_lg_bwd_kernel<HV, 4, false>), dim3((unsigned)grid), blk, lds, st, a, m, nullptr);
-  }
+  unsigned long long* pr = prof ? g_lg_prof : nullptr;
+  hipLaunchKernelGGL(reinterpret_cast<void (*)(ClArgs, LgLayout, unsigned long long*)>(const_cast<void*>(fn)),
+                     dim3((unsigned)grid), blk, lds, st, a, m, pr);
   check_launch();
   return (int)grid;
 }
