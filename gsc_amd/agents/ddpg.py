@@ -627,6 +627,9 @@ class BatchedTrainer:
                 # persistent GNN grids sized to the CUs free while the simulator runs (one full round)
                 budget = int(os.environ.get("GSC_GNN_CU_BUDGET", str(n - k)))
                 nat.gnn_set_cu_budget(budget)
+                # the budget is process-wide state of the native module (overlap mode: work-queue grids, whose
+                # per-workgroup gradient rows depend on the claim order): released with the trainer
+                weakref.finalize(self, nat.gnn_set_cu_budget, 0)
             else:
                 self.sim_stream = torch.cuda.Stream(self.device)
 
