@@ -1,17 +1,17 @@
 // Fused exploration noise + schedule post-processing (reference simple_ddpg.py:182-201, 338-395).
 //
-// Lane-parallel over each (env, src, sfc, sf) slice of n_pad destination weights: two slices per
-// wave (32 lanes each) up to n_pad = 32, one slice per wave with up to four consecutive weights per
-// lane up to n_pad = 256 (the 200-node configs).  Noise comes from a counter-based Philox stream keyed
-// by (seed, step, flat quad index) -- one draw per four weights -- so results do not depend on launch
-// shape.  The two
-// threshold/normalise passes run in fp64 (cross-lane sums; the reference sums Python floats left to
-// right, so results agree to float32 rounding) with the residual of the rounded sum added to the
-// first weight that can absorb it, found by a ballot.  Above 32 destinations most rows skip them: when
-// the second pass provably zeroes the whole row (FastExit), the kernel writes the uniform row directly.
-// At 200 nodes x 256 envs (92M weights): 565 -> 244 us noisy, 441 -> 159 us warm-up, against a 137 us
-// copy of the same bytes (profiles/explore_r5.txt); the remaining time is VALU issue (Philox-10 +
-// Box-Muller per weight quad).
+// Lane-parallel over each (env, src, sfc, sf) slice of n_pad destination weights: two slices per wave (32 lanes
+// each) up to n_pad = 32; one slice per wave with up to four consecutive weights per lane up to n_pad = 128; two
+// slices per wave with eight weights per lane above (the 200-node configs, n_pad % 8 == 0).  Noise comes from a
+// counter-based Philox stream: above 32 destinations keyed by (seed, step, flat octet index) -- one draw per eight
+// weights, 16-bit uniforms -- so results do not depend on which of those kernels runs; up to 32 the round-5 stream
+// (one draw per quad, 24-bit uniforms, explore_weight).  The two threshold/normalise passes run in fp64
+// (cross-lane sums; the reference sums Python floats left to right, so results agree to float32 rounding) with the
+// residual of the rounded sum added to the first weight that can absorb it, found by a ballot.  Above 32
+// destinations most rows skip them: when the second pass provably zeroes the whole row (FastExit), the kernel
+// writes the uniform row directly, and its destination bitset from a per-topology table.
+// At 200 nodes x 256 envs (92M weights): 565 -> 244 us noisy at round 5 (profiles/explore_r5.txt); round 6: raw
+// hardware transcendentals, eight weights per draw, two slices per wave (profiles/explore_r6.txt).
 #include <pybind11/pybind11.h>
 
 #include "../common.h"
@@ -30,6 +30,16 @@ __device__ __forceinline__ double round10(double x) { return rint(x * 1e10) * 1e
 // (v2, v3) -> weights 2, 3.  The value of a weight depends only on (seed, step, flat index).
 struct Quad { float x[4]; };
 
+// Box-Muller radius sqrt(-2 ln(1 - u0)) and (sin, cos)(2 pi u1) on the raw hardware transcendentals: v_log_f32
+// (log2; 1 - u0 >= 2^-24 is never denormal), v_sqrt_f32 and v_sin / v_cos_f32 (argument in revolutions, so
+// no 2 pi scaling).  The libm forms (__logf / sqrtf / __sincosf) add denormal scaling, an extended-precision
+// ln 2 product and a sqrt correction step: ~35 VALU per pair instead of 8.
+__device__ __forceinline__ float box_muller(float u0, float u1, float& sn, float& cs) {
+  sn = __builtin_amdgcn_sinf(u1);
+  cs = __builtin_amdgcn_cosf(u1);
+  return __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(1.0f - u0));
+}
+
 // Philox4x32-10 round keys of (seed, step) computed once on the host: the wave kernel reads them from its
 // arguments instead of bumping the key pair in every draw (20 scalar adds per wave).  Same bits as philox4x32_10.
 struct RoundKeys {
@@ -45,29 +55,54 @@ static RoundKeys round_keys(uint32_t k0, uint32_t k1) {
   }
   return rk;
 }
+// a ^ b ^ k in ONE v_bitop3_b32 (truth table 0x96; the compiler does not form it from two xors): the round's two
+// key mixes cost two VALU instead of four, 20 fewer per draw
+__device__ __forceinline__ uint32_t xor3_k(uint32_t a, uint32_t b, uint32_t k) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+}
+// philox4x32_10 (sim/philox.h) with the round keys from the host and the key mixes as xor3: same bits
 __device__ __forceinline__ Philox4 philox_keyed(const RoundKeys& K, uint64_t ctr) {
   uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0x9E3779B9u, c3 = 0x243F6A88u;
 #pragma unroll
-  for (int r = 0; r < 10; ++r) philox_round(c0, c1, c2, c3, K.k0[r], K.k1[r]);
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    c0 = xor3_k((uint32_t)(p1 >> 32), c1, K.k0[r]);
+    c1 = (uint32_t)p1;
+    c2 = xor3_k((uint32_t)(p0 >> 32), c3, K.k1[r]);
+    c3 = (uint32_t)p0;
+  }
   Philox4 o;
   o.v[0] = c0; o.v[1] = c1; o.v[2] = c2; o.v[3] = c3;
   return o;
 }
 
-__device__ __forceinline__ Quad explore_quad(uint64_t f4, int warmup, const RoundKeys& rk) {
-  const Philox4 r = philox_keyed(rk, f4);
-  Quad q;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) q.x[j] = (float)(r.v[j] >> 8) * (1.0f / 16777216.0f);  // [0, 1)
-  if (warmup) return q;
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const float rad = sqrtf(-2.0f * __logf(1.0f - q.x[2 * p]));  // 1 - u in (0, 1]
-    float sn, cs;
-    __sincosf(6.283185307179586f * q.x[2 * p + 1], &sn, &cs);
-    q.x[2 * p] = rad * cs;
-    q.x[2 * p + 1] = rad * sn;
+// Noise of flat octet o (weights 8o .. 8o + 7): ONE Philox4x32-10 draw keyed by (seed, step, o); its word p gives
+// weights 8o + 2p (low 16 bits) and 8o + 2p + 1 (high 16 bits): in warm-up the two uniforms h 2^-16, else one
+// Box-Muller pair (radius from the low half, angle from the high half; |z| <= 4.71, the 16-bit radius uniform's
+// bound).  Eight weights per draw instead of four: the Philox rounds were half of the kernel's VALU issue.  The
+// value of a weight depends only on (seed, step, flat index), whichever kernel computes it.
+__device__ __forceinline__ void noise_pair(uint32_t w, int warmup, float& a, float& b) {
+  const float u0 = (float)(w & 0xffffu) * (1.0f / 65536.0f), u1 = (float)(w >> 16) * (1.0f / 65536.0f);  // [0, 1)
+  if (warmup) {
+    a = u0;
+    b = u1;
+    return;
   }
+  float sn, cs;
+  const float rad = box_muller(u0, u1, sn, cs);
+  a = rad * cs;
+  b = rad * sn;
+}
+
+// The 4 weights of the 4-aligned quad f4: half of its octet's draw (words 0, 1 or 2, 3)
+__device__ __forceinline__ Quad explore_quad(uint64_t f4, int warmup, const RoundKeys& rk) {
+  const Philox4 r = philox_keyed(rk, f4 >> 3);
+  const bool hi = (f4 & 4) != 0;
+  Quad q;
+  noise_pair(hi ? r.v[2] : r.v[0], warmup, q.x[0], q.x[1]);
+  noise_pair(hi ? r.v[3] : r.v[1], warmup, q.x[2], q.x[3]);
   return q;
 }
 
@@ -75,12 +110,16 @@ __device__ __forceinline__ Quad explore_quad(uint64_t f4, int warmup, const Roun
 __device__ __forceinline__ float explore_apply(float z, float mu, float m, int warmup, float rand_mu, float rand_sigma) {
   if (warmup) return z * m;
   const float sv = 2.0f * mu - 1.0f + rand_mu + rand_sigma * z;
-  const float a = 0.5f * (sv + 1.0f);
-  return a < 0.f ? 0.f : (a > 1.f ? 1.f : a);
+  // 0.5 (sv + 1) as fma(0.5, sv, 0.5): the same bits (scaling by 2 commutes with rounding), one VALU, and the clip
+  // to [0, 1] folds into it as the clamp modifier
+  return __builtin_amdgcn_fmed3f(__builtin_fmaf(0.5f, sv, 0.5f), 0.f, 1.f);
 }
 
-// Noisy (or warm-up uniform) weight i of the slice starting at flat index base (explore_quad's value for it,
-// with only its own Box-Muller pair evaluated).
+// Noisy (or warm-up uniform) weight i of the slice starting at flat index base, for the lanes kernel (n_pad <= 32,
+// the Abilene-class configs): the round-5 stream, unchanged -- one Philox draw per 4-aligned quad of flat indices,
+// 24-bit uniforms, libm Box-Muller.  The lanes kernel computes one draw per lane and weight either way, so the
+// octet stream of the wider kernels would buy it nothing; keeping the stream keeps the headline config's action
+// sequence (and hence its simulated traffic) what it was.
 __device__ __forceinline__ float explore_weight(const float* __restrict__ mu, const float* __restrict__ mrow, long base,
                                                 int i, int warmup, float rand_mu, float rand_sigma, uint32_t seed,
                                                 uint32_t step) {
@@ -421,6 +460,113 @@ __global__ __launch_bounds__(256) void explore_postprocess_wave_kernel(const flo
   }
 }
 
+// Sum / max over each 32-lane half of the wave (fp32, non-negative max as signed ints): DPP row shifts within the
+// 16-lane rows, then row 0 -> 1 and row 2 -> 3 (row_bcast:15); the half totals end in lanes 31 and 63
+__device__ __forceinline__ float half_sum_f32(float v) {
+#define GSC_DPP_ADDF(ctrl, rm) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, rm, 0xF, false));
+  GSC_DPP_ADDF(0x111, 0xF) GSC_DPP_ADDF(0x112, 0xF) GSC_DPP_ADDF(0x114, 0xF) GSC_DPP_ADDF(0x118, 0xF)
+  GSC_DPP_ADDF(0x142, 0xA)
+#undef GSC_DPP_ADDF
+  return v;
+}
+__device__ __forceinline__ int half_max_i32(int v) {
+#define GSC_DPP_MAXI(ctrl, rm) v = max(v, __builtin_amdgcn_update_dpp(0, v, ctrl, rm, 0xF, false));
+  GSC_DPP_MAXI(0x111, 0xF) GSC_DPP_MAXI(0x112, 0xF) GSC_DPP_MAXI(0x114, 0xF) GSC_DPP_MAXI(0x118, 0xF)
+  GSC_DPP_MAXI(0x142, 0xA)
+#undef GSC_DPP_MAXI
+  return v;
+}
+
+// 128 < n_pad <= 256, n_pad % 8 == 0 (the 200-node configs): TWO slices per wave, one per 32-lane half, eight
+// consecutive weights per lane = one Philox draw per lane (explore_quad's noise, bit for bit) -- half the draws of
+// the one-slice-per-wave kernel and half its per-slice reduction / address work.  Rows the early uniform exit
+// decides are written from the host constants; their destination bitsets are the topology's real destinations,
+// copied from the precomputed table pbits [T][R][4] (no mask loads, no ballots).  The rare other rows take the
+// one-slice-per-wave path (four weights per lane: explore_raw + explore_general) for that row.
+template <int WU, bool RM>  // RM: rand_mu != 0 (else its add is skipped: x + 0 == x for the non-negative-zero sums here)
+__global__ __launch_bounds__(256) void explore_postprocess_oct_kernel(const float* __restrict__ mu,
+                                                                     const float* __restrict__ mask,
+                                                                     const long long* __restrict__ topo,
+                                                                     float* __restrict__ out, int R, int P,
+                                                                     float rand_mu, float rand_sigma, double thr,
+                                                                     int passes, PMask pm, FastExit fx, RoundKeys rk,
+                                                                     const uint64_t* __restrict__ pbits) {
+  const int rowA = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 8 + (threadIdx.x >> 6) * 2));
+  if (rowA >= R) return;  // whole waves exit together
+  constexpr int warmup = WU;
+  const int env = blockIdx.y, lane = threadIdx.x & 63, h = lane >> 5, i0 = 8 * (lane & 31);
+  const long tp = topo ? topo[env] : (long)env;  // mask table row of this env
+  const float* mtab = mask + tp * (long)R * P;
+  const int row = min(rowA + h, R - 1);  // a half past R (R odd) recomputes row R - 1 and stores nothing
+  const long base = ((long)env * R + row) * P;
+  const float* src = warmup ? mtab + (long)row * P : mu + base;
+  const float4 va = *reinterpret_cast<const float4*>(src + min(i0, P - 4));
+  const float4 vb = *reinterpret_cast<const float4*>(src + min(i0 + 4, P - 4));
+  const float v[8] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+  const Philox4 r = philox_keyed(rk, (uint64_t)(base + i0) >> 3);  // base + i0 is a multiple of 8 (P % 8 == 0)
+  float wf[8];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) noise_pair(r.v[p], warmup, wf[2 * p], wf[2 * p + 1]);
+  if (warmup) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wf[k] = explore_apply(wf[k], 0.f, v[k], 1, rand_mu, rand_sigma);
+  } else {
+    // explore_apply on weight pairs: 2 mu - 1 (+ rand_mu) + sigma z as packed FMAs (v_pk_fma_f32, the same
+    // per-element IEEE operations), then fma(0.5, ., 0.5) with the clamp modifier per element: 4 VALU per pair
+    typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      f2 sv = __builtin_elementwise_fma(f2{2.f, 2.f}, f2{v[2 * p], v[2 * p + 1]}, f2{-1.f, -1.f});
+      if (RM) sv = sv + f2{rand_mu, rand_mu};
+      sv = __builtin_elementwise_fma(f2{rand_sigma, rand_sigma}, f2{wf[2 * p], wf[2 * p + 1]}, sv);
+      wf[2 * p] = __builtin_amdgcn_fmed3f(__builtin_fmaf(0.5f, sv.x, 0.5f), 0.f, 1.f);
+      wf[2 * p + 1] = __builtin_amdgcn_fmed3f(__builtin_fmaf(0.5f, sv.y, 0.5f), 0.f, 1.f);
+    }
+  }
+  bool fast0 = false, fast1 = false;
+  if (fx.on) {
+    float ps = 0.f, mx = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float t = wf[k] >= fx.thr_f ? wf[k] : 0.f;
+      ps += t;
+      mx = fmaxf(mx, t);
+    }
+    if (i0 >= P) ps = mx = 0.f;  // P % 8 == 0: a lane's 8 weights are all real or all padding
+    const float sv = half_sum_f32(ps);
+    const int mv = half_max_i32(__float_as_int(mx));
+    const float s0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv), 31));
+    const float s1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv), 63));
+    const float m0 = __int_as_float(max(__builtin_amdgcn_readlane(mv, 31), 0));
+    const float m1 = __int_as_float(max(__builtin_amdgcn_readlane(mv, 63), 0));
+    fast0 = s0 == 0.f ? fx.zero_ok != 0 : (double)m0 < fx.bound * (double)s0;
+    fast1 = s1 == 0.f ? fx.zero_ok != 0 : (double)m1 < fx.bound * (double)s1;
+  }
+  const bool mine = (h ? fast1 : fast0) && rowA + h < R;
+  if (mine && i0 < P) {  // P % 8 == 0: all 8 weights of the lane are real
+    float* o = out + base + i0;
+    reinterpret_cast<float4*>(o)[0] = float4{i0 == 0 ? fx.uni0 : fx.uni, fx.uni, fx.uni, fx.uni};
+    reinterpret_cast<float4*>(o)[1] = float4{fx.uni, fx.uni, fx.uni, fx.uni};
+  }
+  if (pm.base && mine && (lane & 31) < 4) {  // every weight is positive: the bitset is the topology's real destinations
+    uint64_t* dst = pmask_dst(pm, env, row);
+    if (dst) dst[lane & 31] = pbits[((long)tp * R + row) * 4 + (lane & 31)];
+  }
+  // rows the early exit does not decide: the whole wave, four weights per lane (the same noise bits)
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    if ((hh ? fast1 : fast0) || rowA + hh >= R) continue;
+    const int rw = rowA + hh;
+    const long bw = ((long)env * R + rw) * P;
+    const float* mrow = mtab + (long)rw * P;
+    const float4 t = *reinterpret_cast<const float4*>((warmup ? mrow : mu + bw) + min(4 * lane, P - 4));
+    const float v4[4] = {t.x, t.y, t.z, t.w};
+    float w4[4];
+    explore_raw<4>(w4, v4, bw, 4 * lane, P, true, warmup, rand_mu, rand_sigma, rk);
+    explore_general<4>(mrow, out, bw, P, env, rw, lane, thr, passes, pm, w4[0], w4[1], w4[2], w4[3]);
+  }
+}
+
 // Host constants of the early uniform exit (see FastExit)
 static FastExit fast_exit(int P, double thr, int passes) {
   FastExit fx{};
@@ -442,7 +588,7 @@ static FastExit fast_exit(int P, double thr, int passes) {
 
 void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t out, int E, int A, int P, int warmup, float rand_mu,
                          float rand_sigma, uint32_t seed, uint32_t step, double thr, int passes, uintptr_t stream,
-                         py::object pmask) {
+                         py::object pmask, uintptr_t pbits) {
   GSC_CHECK(A % P == 0, "action dim must be a multiple of n_pad");
   GSC_CHECK(P <= 256, "n_pad > 256 not supported by the exploration kernel");
   PMask pm{nullptr, 0, 1, 1, 1, 1, 1, 0};
@@ -480,7 +626,18 @@ void explore_postprocess(uintptr_t mu, uintptr_t mask, uintptr_t topo, uintptr_t
                          passes, pm, fx, rk);
     };
     const bool vec = P % 4 == 0 && mu % 16 == 0 && mask % 16 == 0 && out % 16 == 0;
-    if (P <= 64) go(explore_postprocess_wave_kernel<1, S, false>);
+    // two slices per wave, 8 weights per lane: 128 < n_pad, n_pad % 8 == 0, and with the bitset hand-off only
+    // given the per-topology bitset table (GSC_EXPLORE_OCT=0: the one-slice-per-wave kernel)
+    const char* oe = getenv("GSC_EXPLORE_OCT");
+    const bool oct = P > 128 && P % 8 == 0 && vec && (!pm.base || (pbits && topo)) && !(oe && oe[0] == '0');
+    if (oct) {
+      const dim3 g8((unsigned)((A / P + 7) / 8), (unsigned)E);  // four waves x two slices per block
+      auto* kern = warmup ? explore_postprocess_oct_kernel<1, false>
+                          : (rand_mu != 0.f ? explore_postprocess_oct_kernel<0, true> : explore_postprocess_oct_kernel<0, false>);
+      hipLaunchKernelGGL(kern, g8, dim3(256), 0,
+                         stream_of(stream), ptr<const float>(mu), ptr<const float>(mask), ptr<const long long>(topo),
+                         ptr<float>(out), A / P, P, rand_mu, rand_sigma, thr, passes, pm, fx, rk, ptr<const uint64_t>(pbits));
+    } else if (P <= 64) go(explore_postprocess_wave_kernel<1, S, false>);
     else if (P <= 128) go(explore_postprocess_wave_kernel<2, S, false>);
     else if (P <= 192 && P % 2 == 1) go(explore_postprocess_wave_kernel<3, S, false>);
     else if (vec) go(explore_postprocess_wave_kernel<4, S, true>);
@@ -493,7 +650,7 @@ void register_explore(py::module_& m) {
   m.def("explore_postprocess", &explore_postprocess, "fused exploration + threshold/normalise (device)",
         py::arg("mu"), py::arg("mask"), py::arg("topo"), py::arg("out"), py::arg("E"), py::arg("A"), py::arg("P"),
         py::arg("warmup"), py::arg("rand_mu"), py::arg("rand_sigma"), py::arg("seed"), py::arg("step"), py::arg("thr"),
-        py::arg("passes"), py::arg("stream"), py::arg("pmask") = py::none());
+        py::arg("passes"), py::arg("stream"), py::arg("pmask") = py::none(), py::arg("pbits") = 0);
 }
 
 }  // namespace gsc

@@ -58,6 +58,28 @@ def explore_postprocess_reference(mu: torch.Tensor, mask: torch.Tensor, n_pad: i
     return out.view(E, A).float()
 
 
+_PBITS: dict = {}
+
+
+def mask_bitsets(mask: torch.Tensor, n_pad: int) -> torch.Tensor:
+    """[T, A] mask table -> [T, A / n_pad, 4] int64: bit d of word q of row r = (mask[t, r n_pad + 64 q + d] > 0), the
+    simulator's destination bitset of a row whose weights are all positive (the exploration kernel's early-exit
+    rows).  Cached per table (data pointer, version, shape; the entry keeps the table alive)."""
+    T, A = mask.shape
+    key = (mask.data_ptr(), mask._version, T, A, n_pad)
+    hit = _PBITS.get(key)
+    if hit is not None:
+        return hit[1]
+    R = A // n_pad
+    m = torch.zeros(T, R, 256, dtype=torch.int64, device=mask.device)
+    m[:, :, :n_pad] = (mask.view(T, R, n_pad) > 0).to(torch.int64)
+    bits = (m.view(T, R, 4, 64) << torch.arange(64, device=mask.device, dtype=torch.int64)).sum(-1)  # distinct bits
+    if len(_PBITS) > 8:
+        _PBITS.clear()
+    _PBITS[key] = (mask, bits.contiguous())  # the table itself is held: its address cannot be reused meanwhile
+    return _PBITS[key][1]
+
+
 def explore_postprocess(mu: torch.Tensor, mask: torch.Tensor, n_pad: int, warmup: bool, rand_mu: float,
                         rand_sigma: float, seed: int, step: int, threshold: float = 0.1, passes: int = 2,
                         out: Optional[torch.Tensor] = None, topo: Optional[torch.Tensor] = None,
@@ -77,10 +99,16 @@ def explore_postprocess(mu: torch.Tensor, mask: torch.Tensor, n_pad: int, warmup
             assert mask.shape[0] == E
         if out is None:
             out = torch.empty(E, A, device=mu.device, dtype=torch.float32)
+        pbits = 0
+        if pmask is not None and topo is not None and n_pad > 128 and n_pad % 8 == 0:
+            key = (mask.data_ptr(), mask._version, mask.shape[0], A, n_pad)
+            if key in _PBITS or not torch.cuda.is_current_stream_capturing():
+                pbits = mask_bitsets(mask, n_pad).data_ptr()
         nat.explore_postprocess(mu.data_ptr(), mask.data_ptr(), topo.data_ptr() if topo is not None else 0,
                                 out.data_ptr(), E, A, n_pad, int(warmup), float(rand_mu), float(rand_sigma),
                                 int(seed) & 0xffffffff, int(step), float(threshold), int(passes),
-                                torch.cuda.current_stream(mu.device).cuda_stream, pmask)
+                                torch.cuda.current_stream(mu.device).cuda_stream, pmask,
+                                **({"pbits": pbits} if pbits else {}))
         return out
     if topo is not None:
         mask = mask.index_select(0, topo.to(torch.int64))

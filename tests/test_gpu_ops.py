@@ -204,9 +204,9 @@ def test_explore_postprocess_device(P, n):
 
 
 def test_explore_noise_independent_of_slice_shape():
-    """The raw noisy weights (no threshold / normalisation passes) depend only on (seed, step, flat index):
-    the pair path (n_pad 200: one Philox draw per weight pair, 4 weights per lane) and the one-weight-per-lane
-    path (n_pad 40) give identical bits for the same flat action block."""
+    """The raw noisy weights (no threshold / normalisation passes) depend only on (seed, step, flat index) above 32
+    destinations: the octet path (n_pad 200: two slices per wave, 8 weights per lane) and the one-slice-per-wave path
+    (n_pad 40) give identical bits for the same action block.  (n_pad <= 32 keeps the round-5 stream.)"""
     torch.manual_seed(3)
     E, A = 4, 200 * 3 * 200
     mu = torch.rand(E, A, device=DEV)
@@ -215,6 +215,22 @@ def test_explore_noise_independent_of_slice_shape():
         a = explore_postprocess(mu, mask, 200, warm, 0.0, 0.3, seed=9, step=4, threshold=0.0, passes=0)
         b = explore_postprocess(mu, mask, 40, warm, 0.0, 0.3, seed=9, step=4, threshold=0.0, passes=0)
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("P", [40, 200])
+def test_explore_octet_stream_is_philox4x32_10(P):
+    """The wave kernels' noise words are Philox4x32-10 (key = (seed, step), counter = flat index / 8; the device
+    rounds use host round keys and one v_bitop3 xor3 per key mix) -- pinned against the pure-Python Philox of
+    tests/test_replay.py through the warm-up uniforms: weight f = 16-bit half (f & 1) of word (f & 7) / 2, * 2^-16."""
+    from tests.test_replay import philox4x32_10
+    E, A = 2, P * 3 * P
+    mask = torch.ones(E, A, device=DEV)
+    mu = torch.zeros(E, A, device=DEV)
+    u = explore_postprocess(mu, mask, P, True, 0.0, 0.3, seed=77, step=12, threshold=0.0, passes=0).cpu().flatten()
+    for f in list(range(0, 64)) + list(range(E * A - 40, E * A)) + [12345 % (E * A), 99999 % (E * A)]:
+        w = philox4x32_10(77, 12, f >> 3)[(f & 7) >> 1]
+        h = (w >> 16) if f & 1 else (w & 0xffff)
+        assert float(u[f]) == h / 65536.0, f
 
 
 @pytest.mark.parametrize("P,n", [(50, 50), (200, 200), (200, 131), (64, 7)])
@@ -241,6 +257,53 @@ def test_explore_noisy_rows_match_reference_postprocess(P, n):
         uniform = (ref.amax(-1) - ref.amin(-1)).abs() < 1e-6
         if not warm and n > 100:
             assert uniform.any() and (~uniform).any(), "both kernel paths exercised"
+
+
+@pytest.mark.parametrize("P", [20, 40, 200])
+def test_explore_noise_is_standard_normal(P):
+    """The raw exploration noise (passes 0, mu = 0.5, sigma 0.1: weight = 0.5 + 0.05 z) is standard normal in every
+    kernel family (lanes / one slice per wave / two slices per wave): moments and tail mass of ~1.2M samples, and
+    the warm-up uniforms are U[0, 1)."""
+    E, A = 4, P * 3 * P if P > 20 else 20 * 3 * 200
+    while E * A < 1_000_000:
+        E *= 2
+    mu = torch.full((E, A), 0.5, device=DEV)
+    mask = torch.ones(E, A, device=DEV)
+    a = explore_postprocess(mu, mask, P, False, 0.0, 0.1, seed=21, step=5, threshold=0.0, passes=0)
+    z = ((a.double() - 0.5) / 0.05).flatten()
+    assert abs(float(z.mean())) < 0.01 and abs(float(z.std()) - 1.0) < 0.01
+    assert abs(float((z ** 4).mean()) - 3.0) < 0.1                       # Gaussian kurtosis
+    assert abs(float((z.abs() > 2).double().mean()) - 0.0455) < 0.002    # two-sigma tail mass
+    assert abs(float(torch.corrcoef(torch.stack([z[0::2], z[1::2]]))[0, 1])) < 0.01  # Box-Muller pair partners
+    u = explore_postprocess(mu, mask, P, True, 0.0, 0.1, seed=21, step=5, threshold=0.0, passes=0).double().flatten()
+    assert float(u.min()) >= 0.0 and float(u.max()) < 1.0
+    assert abs(float(u.mean()) - 0.5) < 0.005 and abs(float(u.var()) - 1.0 / 12.0) < 0.002
+
+
+@pytest.mark.parametrize("P,n,R", [(200, 200, 600), (200, 131, 7), (256, 256, 9)])
+def test_explore_octet_kernel_matches_slice_kernel(P, n, R, monkeypatch):
+    """The two-slices-per-wave exploration kernel (n_pad > 128, n_pad % 8 == 0: one Philox draw per 8 weights per
+    lane) equals the one-slice-per-wave kernel bit for bit -- raw weights (passes 0), post-processed rows with both
+    the early uniform exit and the general loop, warm-up and noisy; an odd row count leaves a half-wave idle."""
+    torch.manual_seed(5)
+    E, A = 6, P * R
+    T = 2
+    tab = torch.zeros(T, R, P, device=DEV)
+    tab[:, :, :n] = 1
+    tab[1, :, n // 2:] = 0
+    topo = torch.tensor([0, 1, 1, 0, 1, 0], device=DEV)
+    mu = torch.rand(E, R, P, device=DEV) * 0.6
+    mu[:, ::3] = 0
+    mu[:, ::3, 0] = 1.0  # one-hot rows: the general loop
+    mu = mu.view(E, A)
+    tab = tab.view(T, A)
+    for warm in (True, False):
+        for kw in (dict(threshold=0.0, passes=0), dict()):
+            monkeypatch.setenv("GSC_EXPLORE_OCT", "1")
+            a = explore_postprocess(mu, tab, P, warm, 0.0, 0.1, seed=3, step=9, topo=topo, **kw)
+            monkeypatch.setenv("GSC_EXPLORE_OCT", "0")
+            b = explore_postprocess(mu, tab, P, warm, 0.0, 0.1, seed=3, step=9, topo=topo, **kw)
+            assert torch.equal(a, b), (warm, kw)
 
 
 def test_splitk_linear_matches_linear():
