@@ -789,6 +789,87 @@ void cast2d(uintptr_t src, long lds_, uintptr_t dst, long ldd, int R, int C, uin
   check_launch();
 }
 
+// Bit-mask fold with 16-byte weight loads (the 4-byte pair loop above is latency-bound: ~106 us for a 256 x 360,000
+// bf16 block that streams in ~25 us): the row is split at its first 16-byte-aligned element (rows are slices of a
+// wider weight matrix, e.g. the first layer's mask block at column H), the aligned body goes 8 weights per lane per
+// load with two loads in flight, the mask bits of those 8 weights come from one or two 32-bit words of the packed
+// table; the few head / tail elements take the scalar path.  Same products, different fp32 summation order.
+template <int TT>
+__global__ __launch_bounds__(256) void rowdot_bits8_kernel(const uint32_t* __restrict__ xb, long ldx, int T,
+                                                           const __hip_bfloat16* __restrict__ W, long ldw, int N,
+                                                           int A, int achunk, float* out, long ldo) {
+  __shared__ float red[4][TT];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n = blockIdx.x, z = blockIdx.y;
+  const int a0 = z * achunk, a1 = min(A, a0 + achunk);
+  const __hip_bfloat16* wr = W + (long)n * ldw;
+  const int mis = (int)((reinterpret_cast<uintptr_t>(wr + a0) >> 1) & 7);  // elements past a 16-byte boundary
+  const int ab = min(a1, a0 + ((8 - mis) & 7));                            // first aligned element
+  const int nv = (a1 - ab) >> 3;                                            // whole 8-element vectors
+  const int ae = ab + 8 * nv;                                               // tail start
+  float s[TT];
+#pragma unroll
+  for (int t = 0; t < TT; ++t) s[t] = 0.f;
+  auto bits8 = [&](int t, int a) -> uint32_t {  // mask bits of elements a .. a + 7 (bit e = element a + e)
+    const uint32_t* row = xb + (long)t * ldx;
+    const int w = a >> 5, sh = a & 31;
+    uint32_t v = row[w] >> sh;
+    if (sh > 24) v |= row[w + 1] << (32 - sh);
+    return v & 0xffu;
+  };
+  auto acc8 = [&](const uint4& q, int a) {
+    const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+    float wv8[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      wv8[2 * e] = __uint_as_float(u[e] << 16);
+      wv8[2 * e + 1] = __uint_as_float(u[e] & 0xffff0000u);
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      if (t >= T) continue;
+      const uint32_t b = bits8(t, a);
+      float v = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v += ((b >> e) & 1u) ? wv8[e] : 0.f;
+      s[t] += v;
+    }
+  };
+  // aligned body: vectors tid, tid + 256, ... four loads in flight
+  int k = threadIdx.x;
+  for (; k + 768 < nv; k += 1024) {
+    uint4 q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const uint4*>(wr + ab + 8 * (k + 256 * j));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc8(q[j], ab + 8 * (k + 256 * j));
+  }
+  for (; k < nv; k += 256) acc8(*reinterpret_cast<const uint4*>(wr + ab + 8 * k), ab + 8 * k);
+  // head [a0, ab) and tail [ae, a1): at most 7 elements each
+  const int h = threadIdx.x;
+  int a = h < ab - a0 ? a0 + h : (h - (ab - a0) < a1 - ae ? ae + h - (ab - a0) : -1);
+  if (h >= 16) a = -1;
+  if (a >= 0) {
+    const float w0 = __bfloat162float(wr[a]);
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+      if (t < T) s[t] += ((xb[(long)t * ldx + (a >> 5)] >> (a & 31)) & 1u) ? w0 : 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s[t] += __shfl_xor(s[t], off);
+    if (lane == 0) red[wv][t] = s[t];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < TT && (int)threadIdx.x < T) {
+    const int t = threadIdx.x;
+    const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    if (gridDim.y == 1) out[(long)t * ldo + n] = v;
+    else out[((long)z * T + t) * N + n] = v;  // partial slab z
+  }
+}
+
 // ws (optional, >= S T N floats): A split over S workgroups per row when N alone gives a small grid.
 void rowdot(uintptr_t x, long ldx, int T, uintptr_t W, long ldw, int N, int A, uintptr_t out, long ldo,
             uintptr_t stream, uintptr_t ws, long ws_floats, uintptr_t xbits, long ldb) {
@@ -813,7 +894,17 @@ void rowdot(uintptr_t x, long ldx, int T, uintptr_t W, long ldw, int N, int A, u
     hipLaunchKernelGGL(kern, dim3((unsigned)N, (unsigned)S), dim3(256), 0, s, xs, lx, T,
                        ptr<const __hip_bfloat16>(W), ldw, N, A, achunk, pair, dst, ldo);
   };
-  if (bits) {
+  const char* ve = getenv("GSC_ROWDOT_VEC");  // 0: the 4-byte pair loop (A/B)
+  const bool vec8_env = !(ve && ve[0] == '0');
+  if (bits && T <= 4 && vec8_env) {  // 16-byte weight loads (rowdot_bits8_kernel)
+    auto go8 = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((unsigned)N, (unsigned)S), dim3(256), 0, s, ptr<const uint32_t>(xbits), ldb, T,
+                         ptr<const __hip_bfloat16>(W), ldw, N, A, achunk, dst, ldo);
+    };
+    if (T <= 1) go8(rowdot_bits8_kernel<1>);
+    else if (T <= 2) go8(rowdot_bits8_kernel<2>);
+    else go8(rowdot_bits8_kernel<4>);
+  } else if (bits) {
     if (T <= 1) go(rowdot_kernel<1, true>);
     else if (T <= 2) go(rowdot_kernel<2, true>);
     else if (T <= 4) go(rowdot_kernel<4, true>);

@@ -356,9 +356,11 @@ def test_actor_proj_matches_reference(M, K, A, J, T):
 
 
 @pytest.mark.parametrize("T,N,A", [(3, 256, 360000), (1, 64, 1875), (2, 64, 1001)])
-def test_rowdot_mask_fold_bits_match_fp32(T, N, A):
-    """Mask fold out[t][n] = sum_a mask[t][a] W[n][a] (csrc/ops/mlp.hip rowdot): the packed-bit mask
-    variant equals the fp32-mask variant (0/1 weights: identical terms), and both match fp32 PyTorch."""
+def test_rowdot_mask_fold_bits_match_fp32(T, N, A, monkeypatch):
+    """Mask fold out[t][n] = sum_a mask[t][a] W[n][a] (csrc/ops/mlp.hip rowdot): the packed-bit mask variant on
+    the 4-byte pair loop equals the fp32-mask variant (0/1 weights: identical terms); the 16-byte-load bit variant
+    (rowdot_bits8_kernel, W rows starting 3 elements past a 16-byte boundary: head, vectors, tail) matches them to
+    fp32 summation order; all match fp32 PyTorch."""
     from gsc_amd.agents.native_update import mask_bits
     from gsc_amd.native import load
     nat = load()
@@ -368,7 +370,10 @@ def test_rowdot_mask_fold_bits_match_fp32(T, N, A):
     bits = mask_bits(masks)
     ws = torch.zeros(64 * T * N, device="cuda")
     outs = []
-    for xb in (None, bits):
+    monkeypatch.setenv("GSC_ROWDOT_VEC", "0")
+    for xb in (None, bits, bits):
+        if len(outs) == 2:
+            monkeypatch.setenv("GSC_ROWDOT_VEC", "1")
         o = torch.full((T, N), float("nan"), device="cuda")
         nat.rowdot(masks.data_ptr(), masks.stride(0), T, W.data_ptr(), W.stride(0), N, A, o.data_ptr(), o.stride(0),
                    torch.cuda.current_stream().cuda_stream, ws.data_ptr(), ws.numel(),
@@ -376,5 +381,21 @@ def test_rowdot_mask_fold_bits_match_fp32(T, N, A):
         outs.append(o)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+    torch.testing.assert_close(outs[2], outs[1], rtol=1e-5, atol=1e-5)
     ref = masks @ W[:, :A].float().t()
     assert float((outs[1] - ref).norm() / ref.norm()) < 1e-5
+    assert float((outs[2] - ref).norm() / ref.norm()) < 1e-5
+    # misaligned row slices (the first layer's mask block starts at column H): 16-byte path vs fp32 PyTorch
+    Wm = W[:, 3:]
+    o = torch.full((T, N), float("nan"), device="cuda")
+    nat.rowdot(masks.data_ptr(), masks.stride(0), T, Wm.data_ptr(), Wm.stride(0), N, A - 3, o.data_ptr(), o.stride(0),
+               torch.cuda.current_stream().cuda_stream, ws.data_ptr(), ws.numel(), 0, 0)
+    bm = mask_bits(masks[:, :A - 3].contiguous())
+    o8 = torch.full((T, N), float("nan"), device="cuda")
+    nat.rowdot(masks.data_ptr(), masks.stride(0), T, Wm.data_ptr(), Wm.stride(0), N, A - 3, o8.data_ptr(),
+               o8.stride(0), torch.cuda.current_stream().cuda_stream, ws.data_ptr(), ws.numel(), bm.data_ptr(),
+               bm.shape[1])
+    torch.cuda.synchronize()
+    ref_m = masks[:, :A - 3] @ Wm[:, :A - 3].float().t()
+    assert float((o8 - ref_m).norm() / ref_m.norm()) < 1e-5
+    torch.testing.assert_close(o8, o, rtol=1e-5, atol=1e-5)
