@@ -306,6 +306,31 @@ def test_explore_octet_kernel_matches_slice_kernel(P, n, R, monkeypatch):
             assert torch.equal(a, b), (warm, kw)
 
 
+@pytest.mark.parametrize("N,H,T,A", [(256, 22, 3, 360000), (64, 22, 1, 1728), (33, 5, 4, 1001)])
+def test_first_layer_grad_rows_kernel_bitwise(N, H, T, A, monkeypatch):
+    """First-layer gradient dW[n] = [tmp[n][:H] | sum_t tmp[n][H+1+t] mask_t], db[n] = tmp[n][H] (csrc/ops/mlp.hip):
+    the row-grid kernel equals the grid-stride kernel bit for bit and fp32 PyTorch to rounding."""
+    from gsc_amd.native import load
+    nat = load()
+    g = torch.Generator(device="cuda").manual_seed(2)
+    tmp = torch.randn(N, H + 1 + T, device="cuda", generator=g)
+    mask = (torch.rand(T, A + 3, device="cuda", generator=g) > 0.4).float()
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("GSC_FLG_ROWS", v)
+        gW = torch.full((N, H + A + 5), float("nan"), device="cuda")
+        gb = torch.full((N,), float("nan"), device="cuda")
+        nat.first_layer_grad(tmp.data_ptr(), N, H, T, A, mask.data_ptr(), mask.stride(0), gW.data_ptr(), gW.stride(0),
+                             gb.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        outs.append((gW, gb))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0][:, :H + A], outs[1][0][:, :H + A]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.isnan(outs[1][0][:, H + A:]).all()
+    ref = torch.cat([tmp[:, :H], tmp[:, H + 1:] @ mask[:, :A]], 1)
+    torch.testing.assert_close(outs[1][0][:, :H + A], ref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(outs[1][1], tmp[:, H])
+
+
 def test_splitk_linear_matches_linear():
     """Split-K weight gradient == plain GEMM gradient (fp32 reference, bf16 autocast tolerance)."""
     from gsc_amd.ops.linear import linear
