@@ -27,6 +27,26 @@ def _post_processed(E, R, P, seed, peaked=False):
     return explore_postprocess(mu, mask, P, False, 0.0, 0.3, seed, 1, topo=topo)
 
 
+@pytest.mark.parametrize("P", [52, 200])
+def test_sparse_compress_kernels_write_identical_records(P, monkeypatch):
+    """The 16-byte-load compress kernel (P % 4 == 0) writes the same record words -- base, count, exceptions in
+    ascending destination order -- as the lane-strided one, uniform and peaked rows alike."""
+    E, R, cap = 16, 24, 40
+    rings = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("GSC_SP_COMPRESS4", v)
+        rep = DeviceReplay(cap, P, 3, R * P, "cuda", action_dtype=torch.bfloat16, sparse_rows=R)
+        for k in range(2):
+            a = _post_processed(E, R, P, 20 + k, peaked=k == 1)
+            z = torch.zeros(E, P, 3, device="cuda")
+            rep.add(z, torch.zeros(E, dtype=torch.int64, device="cuda"), a, torch.zeros(E, device="cuda"), z,
+                    torch.zeros(E, device="cuda"))
+        torch.cuda.synchronize()
+        rep.check_sparse()
+        rings.append(rep.actions[:2 * E].clone())
+    assert torch.equal(rings[0], rings[1])
+
+
 @pytest.mark.parametrize("P", [50, 200])
 def test_sparse_ring_decodes_to_dense_bf16(P):
     E, R, cap = 16, 24, 40
