@@ -639,6 +639,30 @@ __global__ __launch_bounds__(256) void copy2d_kernel(const __hip_bfloat16* src, 
   }
 }
 
+// copy2d on a (column chunk, row) grid: no per-element 64-bit division (the grid-stride form above is VALU-bound on
+// it: ~40 us per 64 x 360,000 block at config 5); four independent elements per thread and iteration
+__global__ __launch_bounds__(256) void copy2d_rows_kernel(const __hip_bfloat16* __restrict__ src, long lds_,
+                                                          __hip_bfloat16* __restrict__ dst, long ldd, int C,
+                                                          const float* __restrict__ colmask) {
+  const int r = blockIdx.y;
+  const __hip_bfloat16* s = src + (long)r * lds_;
+  __hip_bfloat16* d = dst + (long)r * ldd;
+  const int step = gridDim.x * 1024;
+  for (int c0 = blockIdx.x * 1024 + threadIdx.x; c0 < C; c0 += step) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 256 * j;
+      v[j] = c < C ? __bfloat162float(s[c]) * (colmask ? colmask[c] : 1.f) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 256 * j;
+      if (c < C) d[c] = __float2bfloat16(v[j]);
+    }
+  }
+}
+
 // dst[r][c] = bf16(src[r][c])
 __global__ __launch_bounds__(256) void cast2d_kernel(const float* src, long lds_, __hip_bfloat16* dst, long ldd, int R,
                                                      int C) {
@@ -688,9 +712,16 @@ void first_layer_grad(uintptr_t tmp, int N, int H, int T, int A, uintptr_t mask,
 }
 
 void copy2d(uintptr_t src, long lds_, uintptr_t dst, long ldd, int R, int C, uintptr_t colmask, uintptr_t stream) {
-  hipLaunchKernelGGL(copy2d_kernel, dim3(grid_for((long)R * C)), dim3(256), 0, stream_of(stream),
-                     ptr<const __hip_bfloat16>(src), lds_, ptr<__hip_bfloat16>(dst), ldd, R, C,
-                     ptr<const float>(colmask));
+  const char* ce = getenv("GSC_COPY2D_ROWS");  // 0: the grid-stride kernel (A/B)
+  if (R <= 65535 && !(ce && ce[0] == '0')) {
+    const int cx = std::max(1, std::min((C + 1023) / 1024, 4096));
+    hipLaunchKernelGGL(copy2d_rows_kernel, dim3((unsigned)cx, (unsigned)R), dim3(256), 0, stream_of(stream),
+                       ptr<const __hip_bfloat16>(src), lds_, ptr<__hip_bfloat16>(dst), ldd, C, ptr<const float>(colmask));
+  } else {
+    hipLaunchKernelGGL(copy2d_kernel, dim3(grid_for((long)R * C)), dim3(256), 0, stream_of(stream),
+                       ptr<const __hip_bfloat16>(src), lds_, ptr<__hip_bfloat16>(dst), ldd, R, C,
+                       ptr<const float>(colmask));
+  }
   check_launch();
 }
 struct Cfg {

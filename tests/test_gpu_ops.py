@@ -331,6 +331,28 @@ def test_first_layer_grad_rows_kernel_bitwise(N, H, T, A, monkeypatch):
     assert torch.equal(outs[1][1], tmp[:, H])
 
 
+@pytest.mark.parametrize("R,C,masked", [(64, 360000, True), (3, 1001, False), (70, 257, True)])
+def test_copy2d_rows_kernel_bitwise(R, C, masked, monkeypatch):
+    """copy2d (dst = bf16(src * colmask), strided rows): the row-grid kernel equals the grid-stride kernel bit for bit
+    and the PyTorch product."""
+    from gsc_amd.native import load
+    nat = load()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    src = torch.randn(R, C + 9, device="cuda", generator=g).bfloat16()
+    cm = (torch.rand(C, device="cuda", generator=g) > 0.5).float()
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("GSC_COPY2D_ROWS", v)
+        dst = torch.full((R, C + 5), float("nan"), device="cuda").bfloat16()
+        nat.copy2d(src.data_ptr() + 2 * 3, src.stride(0), dst.data_ptr(), dst.stride(0), R, C,
+                   cm.data_ptr() if masked else 0, torch.cuda.current_stream().cuda_stream)
+        outs.append(dst)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][:, :C].view(torch.int16), outs[1][:, :C].view(torch.int16))
+    ref = (src[:, 3:3 + C].float() * (cm if masked else 1.0)).bfloat16()
+    assert torch.equal(outs[1][:, :C].view(torch.int16), ref.view(torch.int16))
+
+
 def test_splitk_linear_matches_linear():
     """Split-K weight gradient == plain GEMM gradient (fp32 reference, bf16 autocast tolerance)."""
     from gsc_amd.ops.linear import linear
