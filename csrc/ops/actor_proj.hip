@@ -39,7 +39,8 @@ constexpr int BM = 128;  // batch rows per workgroup
 constexpr int BN = 64;   // action columns per tile
 constexpr int NJ = 64;   // critic units (J <= NJ)
 constexpr int NT = 512;  // threads
-constexpr int LDP = BN + 8;
+constexpr int LDP = BN + 4;  // Wa row stride (bf16): 34 words, so the 32 rows of a b64 fragment read land on 32 distinct
+                             // bank pairs (BN + 8 = 36 words put rows r and r + 16 on the same banks)
 constexpr int PD = 3;    // tiles in flight (register ring; 4 spilled once the H fragments moved to registers)
 
 struct Args {
@@ -147,7 +148,10 @@ __global__ __launch_bounds__(NT) void actor_proj_kernel(Args a) {
       *reinterpret_cast<s16x8*>(sw + r * LDK + 8 * c) = wreg[d][i];
     }
     const int r = tid >> 3, c = tid & 7;
-    *reinterpret_cast<s16x8*>(s_wa0 + buf * NJ * LDP + r * LDP + 8 * c) = areg[d];
+    typedef __attribute__((ext_vector_type(4))) short s16x4w;
+    short* wdst = s_wa0 + buf * NJ * LDP + r * LDP + 8 * c;  // 8-byte aligned rows (LDP = 68): two b64 stores
+    *reinterpret_cast<s16x4w*>(wdst) = s16x4w{areg[d][0], areg[d][1], areg[d][2], areg[d][3]};
+    *reinterpret_cast<s16x4w*>(wdst + 4) = s16x4w{areg[d][4], areg[d][5], areg[d][6], areg[d][7]};
     if (tid < BN) {
       const long n = (long)tt * BN + tid;
       const bool live = tt < t1 && n < a.A;
